@@ -1,0 +1,168 @@
+#!/usr/bin/env python3
+"""Headline benchmark: fused map+reduce GB/s (+ dot GFLOP/s) on MI355X.
+
+Workload (BASELINE.json configs[1]): x, y ~ U[0,1), z ~ U[-1,1) fp32 of shape
+(32768, 32768) = 2^30 elements, resident in HBM before timing; one step =
+``sum(x*y + exp(z), axis=0).optimized().force()`` and the same for axis=1 --
+two fused map+reduce evaluations, each reading 3 x 4 B per element (12.885 GB)
+and writing 32768 fp32.  ``value`` = algorithmic bytes of all ranks / the max
+over ranks of the timed wall time.  Multi-GPU: launched by torchrun, one rank
+per GPU; the arrays are row-strip tiled over the ranks (weak in HBM per GPU is
+fixed by the global shape: strong scaling of the fixed 2^30 problem).
+
+Also reported (secondary, ``dot``): ``dot(A, B)`` for 32768^2 fp32 (configs[3])
+in GFLOP/s, and the CPU baseline (the reference's multi-worker NumPy model,
+oracle/cpu_baseline.py) on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
+MFMA_F32_TFS = 157.3       # dense fp32 MFMA (v_mfma_f32_32x32x2_f32)
+MFMA_F64_TFS = 78.6        # dense fp64 MFMA
+
+
+def main():
+  ap = argparse.ArgumentParser()
+  ap.add_argument('--gpus', type=int, default=1)
+  ap.add_argument('--steps', type=int, default=10)
+  ap.add_argument('--warmup', type=int, default=2)
+  ap.add_argument('--size', type=int, default=32768)
+  ap.add_argument('--dot', type=int, default=1, help='also time the dot config (1/0)')
+  ap.add_argument('--dot-size', type=int, default=32768)
+  ap.add_argument('--cpu-baseline', type=int, default=1)
+  ap.add_argument('--cpu-rows', type=int, default=4096)
+  args = ap.parse_args()
+
+  import torch
+  import spartan_amd
+  from spartan_amd import backend, comm, expr, runtime
+
+  ctx = spartan_amd.initialize()
+  be = backend.get()
+  assert isinstance(be, backend.HipBackend)
+  S = args.size
+  N = ctx.world_size
+
+  def sync():
+    torch.cuda.synchronize()
+
+  x = expr.rand(S, S, dtype=np.float32, seed=11).force()
+  y = expr.rand(S, S, dtype=np.float32, seed=12).force()
+  z = expr.rand(S, S, dtype=np.float32, seed=13, low=-1.0, high=1.0).force()
+  X, Y, Z = expr.lazify(x), expr.lazify(y), expr.lazify(z)
+
+  def step():
+    a0 = expr.sum(X * Y + expr.exp(Z), axis=0).optimized().force()
+    a1 = expr.sum(X * Y + expr.exp(Z), axis=1).optimized().force()
+    return a0, a1
+
+  for _ in range(args.warmup):
+    step()
+  sync()
+  comm.barrier()
+  sync()
+  be.kernel_events = []
+  t0 = time.perf_counter()
+  for _ in range(args.steps):
+    step()
+  sync()
+  comm.barrier()
+  sync()
+  elapsed = time.perf_counter() - t0
+  events = be.kernel_events
+  be.kernel_events = None
+  elapsed = comm.max_over_ranks(elapsed)
+
+  elems = S * S
+  bytes_per_eval = 3 * 4 * elems + 4 * S
+  total_bytes = 2 * bytes_per_eval * args.steps
+  value = total_bytes / elapsed / 1e9
+  # dominant kernel: the generated fused map+reduce kernel ('spx_reduce'),
+  # timed with HIP events on the stream it is launched on
+  red = [(s.elapsed_time(e) * 1e-3) for (n, s, e) in events if n == 'spx_reduce']
+  ax0 = red[0::2]
+  ax1 = red[1::2]
+  rows_local = sum(ex.shape[0] for ex in x.local) if hasattr(x, 'local') else S
+  bytes_launch = 3 * 4 * rows_local * S + 4 * S
+  avg = float(np.mean(red)) if red else float('nan')
+  achieved = bytes_launch / avg / 1e9 if red else None
+
+  result = {
+      'metric': 'fused map+reduce GB/s (x*y+exp(z), sum axis 0 and axis 1, 2^30 fp32)',
+      'value': round(value, 2),
+      'unit': 'GB/s',
+      'n_gpus': N,
+      'steps': args.steps,
+      'warmup': args.warmup,
+      'ms_per_step': round(elapsed / args.steps * 1e3, 4),
+      'higher_is_better': True,
+      'scaling': 'strong',
+      'vs_baseline': None,
+      'dtype': 'f32',
+      'data': 'synthetic (counter-based splitmix64 U[0,1) / U[-1,1), resident in HBM)',
+      'config': {'workload': 'cfg2: sum(x*y+exp(z), axis=0) + sum(x*y+exp(z), axis=1), x,y,z fp32 (%d,%d)'
+                             % (S, S), 'shape': [S, S], 'tiling': 'row strips over %d rank(s)' % N,
+                 'parallelism': 'tile-dp%d' % N},
+      'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1) if achieved else None,
+                   'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                   'frac': round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                   'traffic': None,
+                   'kernel': 'spx_reduce (generated fused map+reduce)',
+                   'bytes_per_launch': bytes_launch,
+                   'avg_launch_ms': round(avg * 1e3, 4) if red else None,
+                   'axis0_ms': round(float(np.mean(ax0)) * 1e3, 4) if ax0 else None,
+                   'axis1_ms': round(float(np.mean(ax1)) * 1e3, 4) if ax1 else None},
+  }
+  del x, y, z, X, Y, Z
+  torch.cuda.empty_cache()
+
+  if args.dot:
+    result['dot'] = bench_dot(args.dot_size, ctx, be, expr, comm, sync)
+
+  if args.cpu_baseline and N == 1 and ctx.rank == 0:
+    from oracle.cpu_baseline import cfg2_cpu_baseline
+    cb = cfg2_cpu_baseline(rows=min(args.cpu_rows, S), cols=S)
+    result['cpu_baseline'] = {k: cb[k] for k in ('value', 'unit', 'cores', 'kind', 'sample')}
+    result['cpu_baseline']['value'] = round(cb['value'], 3)
+  if ctx.rank == 0:
+    print(json.dumps(result), flush=True)
+  spartan_amd.shutdown()
+
+
+def bench_dot(S, ctx, be, expr, comm, sync):
+  """dot(A, B) for S x S fp32 and fp64 (configs[3]); GFLOP/s over all ranks."""
+  import torch
+  out = {}
+  for dt, peak in ((np.float32, MFMA_F32_TFS), (np.float64, MFMA_F64_TFS)):
+    a = expr.rand(S, S, dtype=dt, seed=31).force()
+    b = expr.rand(S, S, dtype=dt, seed=32).force()
+    A, B = expr.lazify(a), expr.lazify(b)
+    expr.dot(A, B).force()  # warm-up (JIT-free: spx_gemm is ahead-of-time)
+    sync()
+    comm.barrier()
+    be.kernel_events = None
+    t0 = time.perf_counter()
+    c = expr.dot(A, B).force()
+    sync()
+    comm.barrier()
+    el = comm.max_over_ranks(time.perf_counter() - t0)
+    flops = 2.0 * S ** 3
+    name = 'f32' if dt == np.float32 else 'f64'
+    out[name] = {'gflops': round(flops / el / 1e9, 1), 'seconds': round(el, 4),
+                 'mfma_frac_per_gpu': round(flops / el / 1e12 / (peak * ctx.world_size), 4)}
+    del a, b, A, B, c
+    torch.cuda.empty_cache()
+  out['config'] = 'dot(A, B), A, B ~ U[0,1) (%d, %d), K-split over ranks' % (S, S)
+  return out
+
+
+if __name__ == '__main__':
+  main()

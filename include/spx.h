@@ -1,0 +1,154 @@
+/*
+ * spx.h -- C ABI of libspx.so, the MI355X (gfx950) tile-execution backend
+ * underneath spartan_amd.expr.
+ *
+ * The reference (sdutheone/spartan) has no native boundary on its hot path:
+ * every tile operation is a NumPy/BLAS call made from a Python worker
+ * (spartan/expr/local.py:110-122, spartan/expr/dot.py:195-212) and tiles move
+ * over pickled ZeroMQ RPC.  Each entry point below replaces one of those
+ * per-tile call sites; the reference interface it replaces is cited on it.
+ *
+ * Conventions
+ *   - Every function returns 0 on success and a negative SPX_E* code on error;
+ *     spx_last_error() returns the message of the calling thread's last error.
+ *   - All device memory is owned by the caller (allocated through PyTorch-ROCm
+ *     on the GPU of this rank).  The library never frees caller buffers.
+ *   - Every compute call is asynchronous on the given hipStream_t (passed as
+ *     void*; NULL = the null stream).  Nothing here synchronises the host.
+ *   - Shapes, offsets and strides are in ELEMENTS, int64, row-major.
+ *   - No torch types cross this boundary: plain pointers and sizes only.
+ */
+#ifndef SPX_H
+#define SPX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPX_ABI_VERSION 1
+
+/* error codes */
+#define SPX_OK 0
+#define SPX_EINVAL -1   /* bad argument (shape / dtype / null pointer)      */
+#define SPX_EHIP -2     /* HIP runtime error (message has hipGetErrorString) */
+#define SPX_ENOTSUP -3  /* combination not supported by this build           */
+
+/* element types (NumPy dtype on the Python side) */
+#define SPX_BOOL 0 /* numpy.bool_  stored as uint8 0/1 */
+#define SPX_I32 1  /* numpy.int32  */
+#define SPX_I64 2  /* numpy.int64  */
+#define SPX_F32 3  /* numpy.float32 */
+#define SPX_F64 4  /* numpy.float64 */
+
+/* reduction / merge operators (reference accumulate_fn / reducer) */
+#define SPX_OP_SUM 0     /* np.add     */
+#define SPX_OP_MIN 1     /* np.minimum */
+#define SPX_OP_MAX 2     /* np.maximum */
+#define SPX_OP_ARGMIN 3  /* (value, first index) min */
+#define SPX_OP_ARGMAX 4  /* (value, first index) max */
+#define SPX_OP_REPLACE 5 /* reducer None: last write wins */
+
+/* fill kinds */
+#define SPX_FILL_CONST 0   /* value a                                   */
+#define SPX_FILL_ARANGE 1  /* a + b * global_flat_index                 */
+#define SPX_FILL_UNIFORM 2 /* a + (b-a) * U[0,1) from splitmix64(seed,i) */
+
+/* ---------------------------------------------------------------- basics */
+int spx_abi_version(void);
+const char* spx_last_error(void);
+
+/* ------------------------------------------------------------------- JIT
+ * Fused map / map+reduce kernels are generated from the LocalExpr tree by
+ * spartan_amd/codegen.py, compiled to a gfx950 code object, and launched
+ * through these three calls.  Replaces FnCallExpr.evaluate
+ * (spartan/expr/local.py:110-122) driven by tile_mapper (spartan/expr/map.py:48-88)
+ * and _reduce_mapper (spartan/expr/reduce.py:19-68); the reference's own
+ * codegen hook is ParakeetExpr (spartan/expr/local.py:154-200).
+ */
+int spx_module_load(const void* image, size_t nbytes, void** module_out);
+int spx_module_unload(void* module);
+int spx_module_function(void* module, const char* name, void** fn_out);
+/* args points to the packed kernel-argument struct (copied by the runtime). */
+int spx_launch(void* fn, uint32_t grid_x, uint32_t grid_y, uint32_t grid_z,
+               uint32_t block_x, uint32_t shared_bytes, const void* args,
+               size_t args_bytes, void* stream);
+
+/* ------------------------------------------------------------------ fills
+ * Replaces builtins._make_ones/_make_zeros (spartan/expr/builtins.py:370-375),
+ * _arange_mapper (:404-411) and np.random.rand per tile (:29-31; the
+ * reference RNG is not reproducible, ours is counter-based on the GLOBAL flat
+ * index, so values do not depend on the tiling).
+ * The tile is dense row-major with tile_shape; it sits at ul inside an array
+ * of array_shape (ndim <= 8).
+ */
+int spx_fill(int dtype, int kind, void* out, int ndim, const int64_t* tile_shape,
+             const int64_t* ul, const int64_t* array_shape, double a, double b,
+             uint64_t seed, void* stream);
+
+/* -------------------------------------------------------- reduce finalize
+ * Combines P partial rows (part_val[P][n], accumulator dtype acc_dtype, and
+ * for ARGMIN/ARGMAX part_idx[P][n] int64) into out[n] of out_dtype
+ * (for ARG* ops out is int64 indices and out_val may receive the values).
+ * Partials are combined in index order p = 0..P-1, so results are
+ * deterministic.  Replaces the per-tile partial merge of
+ * _reduce_mapper -> DistArray.update -> tile.merge
+ * (spartan/expr/reduce.py:53-67, spartan/array/tile.pyx:201-298).
+ */
+int spx_reduce_finalize(int op, int acc_dtype, int out_dtype, const void* part_val,
+                        const int64_t* part_idx, int64_t P, int64_t n, void* out,
+                        void* out_val, void* stream);
+
+/* ------------------------------------------------------------------ merge
+ * dst[region] = reducer(dst[region], src) with the reference's mask rule:
+ * elements whose mask byte is 0 are replaced (first write), others reduced;
+ * afterwards the region's mask bytes are 1.  With full_tile_fastpath != 0 and
+ * the region equal to the whole tile, the reference's fast path is used: the
+ * whole tile is reduced iff mask[0] is set, else replaced
+ * (spartan/array/tile.pyx:264-284).  mask may be NULL (treated as all-set
+ * for op != REPLACE).  src has src_dtype and is dense with region_shape.
+ */
+int spx_merge(int op, int dtype, void* dst, uint8_t* mask, int ndim,
+              const int64_t* dst_shape, const int64_t* region_ul,
+              const int64_t* region_shape, const void* src, int src_dtype,
+              int full_tile_fastpath, void* stream);
+
+/* ------------------------------------------------------------ copy region
+ * Strided N-d copy with dtype conversion: dst[dst_ul + i] = src[src_ul + i]
+ * for i in copy_shape.  Replaces the stitch loop of DistArrayImpl.fetch
+ * (spartan/array/distarray.py:315-365) and Tile.get (tile.pyx:69-114).
+ */
+int spx_copy_region(int dst_dtype, void* dst, const int64_t* dst_shape,
+                    const int64_t* dst_ul, int src_dtype, const void* src,
+                    const int64_t* src_shape, const int64_t* src_ul, int ndim,
+                    const int64_t* copy_shape, void* stream);
+
+/* ------------------------------------------------------------------- gemm
+ * C[M,N] = alpha * A[M,K] @ B[K,N] + beta * C, row-major with leading
+ * dimensions lda/ldb/ldc, dtype F32 (v_mfma_f32_32x32x2_f32) or F64
+ * (v_mfma_f64_16x16x4_f64).  Replaces tiles[0].dot(tiles[1]) in
+ * dot_map2_mapper (spartan/expr/dot.py:195-212), dot_outer_mapper (:217-233)
+ * and dot_map2_np_mapper (:172-187).
+ */
+int spx_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+             const void* B, int64_t ldb, void* C, int64_t ldc, double alpha,
+             double beta, void* stream);
+
+/* ------------------------------------------------- arg-reduction combine
+ * Element-wise combine of R (value, index) partial sets, e.g. gathered from
+ * all ranks: out_idx[n] / out_val[n] = best over r of (vals[r][n], idx[r][n]);
+ * smaller (ARGMIN) / larger (ARGMAX) value wins, ties go to the smaller
+ * index (first occurrence), matching the sentinel-min of _arg_mapper
+ * (spartan/expr/builtins.py:610-666).
+ */
+int spx_argreduce_combine(int op, int dtype, const void* vals, const int64_t* idx,
+                          int64_t R, int64_t n, void* out_val, int64_t* out_idx,
+                          void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SPX_H */

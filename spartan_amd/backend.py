@@ -1,0 +1,475 @@
+"""Kernel backend: libspx.so (C ABI, include/spx.h) + generated-kernel JIT.
+
+This is the only module that touches the GPU compute path.  It loads the
+in-tree ``libspx.so`` (built by ``__graft_entry__.build()`` with hipcc for
+gfx950) and fails loudly if it is missing -- there is no CPU fallback.  Tests
+may install a different backend object with ``set_backend`` to exercise the
+host logic without a GPU; product code never does.
+
+Tensors are PyTorch-ROCm device tensors (allocation and streams only); every
+call passes raw pointers and the current HIP stream to the C ABI.
+"""
+import ctypes
+import hashlib
+import os
+import subprocess
+import tempfile
+import threading
+
+import numpy as np
+
+from . import codegen
+from .config import FLAGS
+from .layout import broadcast_strides, coalesce, reduce_view, contiguous_strides
+from .util import prod
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libspx.so')
+SRC_PATH = os.path.join(_HERE, 'csrc', 'spx.hip')
+
+SPX_BOOL, SPX_I32, SPX_I64, SPX_F32, SPX_F64 = 0, 1, 2, 3, 4
+OP_CODE = {'sum': 0, 'min': 1, 'max': 2, 'argmin': 3, 'argmax': 4, 'replace': 5}
+FILL_CONST, FILL_ARANGE, FILL_UNIFORM = 0, 1, 2
+
+_DT = {np.dtype(np.bool_): SPX_BOOL, np.dtype(np.int32): SPX_I32, np.dtype(np.int64): SPX_I64,
+       np.dtype(np.float32): SPX_F32, np.dtype(np.float64): SPX_F64}
+
+
+def spx_dtype(dt):
+  dt = np.dtype(dt)
+  if dt not in _DT:
+    raise TypeError('dtype %s is not supported by the MI355X backend '
+                    '(bool, int32, int64, float32, float64)' % dt)
+  return _DT[dt]
+
+
+def torch_dtype(dt):
+  import torch
+  return {np.dtype(np.bool_): torch.bool, np.dtype(np.int32): torch.int32,
+          np.dtype(np.int64): torch.int64, np.dtype(np.float32): torch.float32,
+          np.dtype(np.float64): torch.float64}[np.dtype(dt)]
+
+
+def np_dtype(tdt):
+  import torch
+  return {torch.bool: np.dtype(np.bool_), torch.int32: np.dtype(np.int32),
+          torch.int64: np.dtype(np.int64), torch.float32: np.dtype(np.float32),
+          torch.float64: np.dtype(np.float64)}[tdt]
+
+
+# ------------------------------------------------------------------ library
+_lib = None
+_lib_lock = threading.Lock()
+
+_I64P = ctypes.POINTER(ctypes.c_int64)
+_SIGS = {
+    'spx_abi_version': ([], ctypes.c_int),
+    'spx_last_error': ([], ctypes.c_char_p),
+    'spx_module_load': ([ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    'spx_module_unload': ([ctypes.c_void_p], ctypes.c_int),
+    'spx_module_function': ([ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    'spx_launch': ([ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                    ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p], ctypes.c_int),
+    'spx_fill': ([ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, _I64P, _I64P, _I64P,
+                  ctypes.c_double, ctypes.c_double, ctypes.c_uint64, ctypes.c_void_p], ctypes.c_int),
+    'spx_reduce_finalize': ([ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_void_p], ctypes.c_int),
+    'spx_merge': ([ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, _I64P, _I64P,
+                   _I64P, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
+    'spx_copy_region': ([ctypes.c_int, ctypes.c_void_p, _I64P, _I64P, ctypes.c_int, ctypes.c_void_p, _I64P,
+                         _I64P, ctypes.c_int, _I64P, ctypes.c_void_p], ctypes.c_int),
+    'spx_gemm': ([ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                  ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                  ctypes.c_double, ctypes.c_double, ctypes.c_void_p], ctypes.c_int),
+    'spx_argreduce_combine': ([ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                               ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+}
+EXPORTED = tuple(_SIGS)
+
+
+def load_library(path=LIB_PATH):
+  """Load libspx.so (importing torch first so its HIP runtime is the one used)."""
+  global _lib
+  with _lib_lock:
+    if _lib is not None:
+      return _lib
+    import torch  # noqa: F401  (torch's libamdhip64.so.7 must be the loaded runtime)
+    if not os.path.exists(path):
+      raise RuntimeError('libspx.so not found at %s: run __graft_entry__.build() '
+                         '(hipcc --offload-arch=gfx950); there is no CPU fallback' % path)
+    lib = ctypes.CDLL(path)
+    for name, (args, res) in _SIGS.items():
+      fn = getattr(lib, name)
+      fn.argtypes = args
+      fn.restype = res
+    _lib = lib
+    return lib
+
+
+def _arr(vals):
+  vals = [int(v) for v in vals] or [0]
+  return (ctypes.c_int64 * len(vals))(*vals)
+
+
+def _check(rc, what):
+  if rc != 0:
+    raise RuntimeError('%s failed (%d): %s' % (what, rc, _lib.spx_last_error().decode()))
+
+
+# ------------------------------------------------------------ JIT compile
+def clang_path():
+  rocm = os.environ.get('ROCM_PATH', '/opt/rocm')
+  p = os.path.join(rocm, 'lib', 'llvm', 'bin', 'clang++')
+  if not os.path.exists(p):
+    raise RuntimeError('device compiler %s not found' % p)
+  return p
+
+
+COMPILE_FLAGS = ['-x', 'hip', '--offload-arch=gfx950', '--cuda-device-only', '--no-gpu-bundle-output',
+                 '-nogpuinc', '-O3', '-ffp-contract=off', '-std=c++17']
+
+
+def cache_dir():
+  d = FLAGS.kernel_cache_dir or os.path.join(_HERE, '_kcache')
+  try:
+    os.makedirs(d, exist_ok=True)
+    if os.access(d, os.W_OK):
+      return d
+  except OSError:
+    pass
+  d = os.path.join(tempfile.gettempdir(), 'spartan_amd_kcache')
+  os.makedirs(d, exist_ok=True)
+  return d
+
+
+def source_key(src):
+  h = hashlib.sha1()
+  h.update(' '.join(COMPILE_FLAGS).encode())
+  h.update(src.encode())
+  return h.hexdigest()[:24]
+
+
+def compile_code_object(src):
+  """Compile generated HIP source to a gfx950 code object (cached on disk)."""
+  key = source_key(src)
+  d = cache_dir()
+  path = os.path.join(d, key + '.hsaco')
+  if os.path.exists(path):
+    with open(path, 'rb') as f:
+      return f.read()
+  # also look in the in-tree cache when an override dir is used
+  intree = os.path.join(_HERE, '_kcache', key + '.hsaco')
+  if os.path.exists(intree):
+    with open(intree, 'rb') as f:
+      return f.read()
+  with tempfile.TemporaryDirectory() as td:
+    sp = os.path.join(td, 'k.hip')
+    op = os.path.join(td, 'k.hsaco')
+    with open(sp, 'w') as f:
+      f.write(src)
+    r = subprocess.run([clang_path()] + COMPILE_FLAGS + ['-o', op, sp], capture_output=True, text=True)
+    if r.returncode != 0:
+      raise RuntimeError('gfx950 codegen compile failed:\n%s\n--- source ---\n%s' % (r.stderr, src))
+    with open(op, 'rb') as f:
+      img = f.read()
+  tmp = path + '.%d.tmp' % os.getpid()
+  with open(tmp, 'wb') as f:
+    f.write(img)
+  os.replace(tmp, path)
+  return img
+
+
+class HipBackend:
+  """Launches libspx.so / generated kernels on the current HIP stream."""
+  name = 'hip'
+
+  def __init__(self):
+    self.lib = load_library()
+    self._fns = {}
+    self._modules = []
+    self._lock = threading.Lock()
+    self.launch_log = None   # optional list collecting grids (tests)
+    self.kernel_events = None  # optional list of (name, start, end) HIP events (bench)
+    self._names = {}
+
+  # ---------------------------------------------------------------- utils
+  def stream(self):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+  def kernel(self, src, name):
+    key = source_key(src)
+    with self._lock:
+      fn = self._fns.get(key)
+      if fn is not None:
+        return fn
+      img = compile_code_object(src)
+      mod = ctypes.c_void_p()
+      _check(self.lib.spx_module_load(img, len(img), ctypes.byref(mod)), 'spx_module_load')
+      self._modules.append(mod)
+      f = ctypes.c_void_p()
+      _check(self.lib.spx_module_function(mod, name.encode(), ctypes.byref(f)), 'spx_module_function')
+      self._fns[key] = f
+      self._names[f.value] = name
+      return f
+
+  def launch(self, fn, grid, args):
+    if self.launch_log is not None:
+      self.launch_log.append(grid)
+    args.grid = grid
+    ev = None
+    if self.kernel_events is not None:
+      import torch
+      ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+      ev[0].record()
+    _check(self.lib.spx_launch(fn, grid, 1, 1, 256, 0, ctypes.byref(args), ctypes.sizeof(args),
+                               self.stream()), 'spx_launch')
+    if ev is not None:
+      ev[1].record()
+      self.kernel_events.append((self._names.get(fn.value, '?'), ev[0], ev[1]))
+
+  # ---------------------------------------------------------------- fills
+  def fill(self, out, kind, a, b, seed, ul, array_shape):
+    shape = tuple(out.shape)
+    nd = len(shape)
+    _check(self.lib.spx_fill(spx_dtype(np_dtype(out.dtype)), kind, ctypes.c_void_p(out.data_ptr()), nd,
+                             _arr(shape), _arr(ul), _arr(array_shape), float(a), float(b),
+                             int(seed) & 0xFFFFFFFFFFFFFFFF, self.stream()), 'spx_fill')
+
+  # ------------------------------------------------------------------ map
+  def map(self, root, inputs, out):
+    """out[...] = root(inputs) elementwise.  inputs: {slot: tensor} (contiguous,
+    broadcastable to out.shape); scalar slots come from the IR's Sc leaves."""
+    shape = tuple(out.shape)
+    n = prod(shape)
+    if n == 0:
+      return
+    slots = sorted(inputs)
+    ins = [(s, np_dtype(inputs[s].dtype)) for s in slots]
+    strides = [broadcast_strides(tuple(inputs[s].shape), shape) for s in slots]
+    dense = all(tuple(inputs[s].shape) == shape for s in slots)
+    V = codegen.vec_width([dt for _, dt in ins] + [root.dtype])
+    args = codegen.KArgs()
+    _scalars_into(root, args)
+    for s in slots:
+      args.ptr[s] = inputs[s].data_ptr()
+    args.out0 = out.data_ptr()
+    args.n = n
+    if dense:
+      classes = ['c'] * len(slots)
+      ndim = 1
+      vec_ok = (n % V == 0) and all(inputs[s].data_ptr() % 16 == 0 for s in slots) and out.data_ptr() % 16 == 0
+    else:
+      cshape, cstr = coalesce(shape, strides)
+      ndim = len(cshape)
+      if ndim > codegen.MAX_DIM:
+        raise NotImplementedError('map over %d non-coalescible dims' % ndim)
+      for d in range(ndim):
+        args.dim[d] = cshape[d]
+      for k, s in enumerate(slots):
+        for d in range(ndim):
+          args.str[s][d] = cstr[k][d]
+      classes = [_cls(cstr[k][ndim - 1]) for k in range(len(slots))]
+      vec_ok = (cshape[-1] % V == 0) and out.data_ptr() % 16 == 0 and all(
+          _vec_aligned(inputs[s], cstr[k], classes[k], V) for k, s in enumerate(slots))
+    args.flags = 1 if (vec_ok and V > 1) else 0
+    src = codegen.gen_map(root, ins, classes, ndim, V, dense)
+    fn = self.kernel(src, 'spx_map')
+    per = V if args.flags else 1
+    grid = max(1, min(-(-n // (256 * per)), 256 * 16))
+    self.launch(fn, grid, args)
+
+  # --------------------------------------------------------------- reduce
+  def reduce(self, root, op, inputs, in_shape, axis, out_shape, out_dtype, idx_geom=None):
+    """Fused map+reduce over one tile -> the tile's partial, a device tensor of
+    out_shape and out_dtype; for argmin/argmax a (values, int64 indices) pair."""
+    import torch
+    slots = sorted(inputs)
+    ins = [(s, np_dtype(inputs[s].dtype)) for s in slots]
+    strides = [broadcast_strides(tuple(inputs[s].shape), in_shape) for s in slots]
+    view = reduce_view(in_shape, strides, axis)
+    if view is None:
+      raise NotImplementedError('reduction view not coalescible; materialise the map first')
+    O, R, I, vstr = view
+    dev = out_device(inputs, slots)
+    n_out = O * I
+    arg = op in ('argmin', 'argmax')
+    adt = codegen.acc_dtype(op, root.dtype)
+    if arg:
+      res_v = torch.empty(tuple(out_shape), dtype=torch_dtype(adt), device=dev)
+      result = torch.empty(tuple(out_shape), dtype=torch.int64, device=dev)
+    else:
+      result = torch.empty(tuple(out_shape), dtype=torch_dtype(out_dtype), device=dev)
+    if n_out == 0:
+      return (res_v, result) if arg else result
+    if R == 0:
+      raise ValueError('zero-size reduction')
+    V = codegen.vec_width([dt for _, dt in ins] + [adt])
+    args = codegen.KArgs()
+    _scalars_into(root, args)
+    for k, s in enumerate(slots):
+      args.ptr[s] = inputs[s].data_ptr()
+      for d in range(3):
+        args.str[s][d] = vstr[k][d]
+    args.dim[0], args.dim[1], args.dim[2] = O, R, I
+    target_blocks = 2048
+    if I == 1:
+      kind = 'rows'
+      classes = [_cls(vstr[k][1]) for k in range(len(slots))]
+      vec_ok = V > 1 and R % V == 0 and all(
+          _aligned_ptr(inputs[s], V) and (vstr[k][0] % V == 0 if classes[k] == 'c' else True)
+          for k, s in enumerate(slots))
+      per = V if vec_ok else 1
+      P = 1
+      if O < target_blocks:
+        P = max(1, min(-(-target_blocks // O), -(-R // (256 * per * 4))))
+      chunk = -(-R // P)
+      chunk = -(-chunk // per) * per
+      P = -(-R // chunk)
+      nblk = O * P
+      args.aux[0], args.aux[1] = P, chunk
+    else:
+      kind = 'cols'
+      classes = [_cls(vstr[k][2]) for k in range(len(slots))]
+      vec_ok = V > 1 and I % V == 0 and all(
+          _aligned_ptr(inputs[s], V) and ((vstr[k][0] % V == 0 and vstr[k][1] % V == 0)
+                                          if classes[k] == 'c' else True)
+          for k, s in enumerate(slots))
+      per = V if vec_ok else 1
+      need = -(-I // per)
+      lpr = 1
+      while lpr < need and lpr < 64:
+        lpr *= 2
+      CT = -(-I // (lpr * per))
+      rows_per_step = 4 * (64 // lpr)
+      base = CT * O
+      P = 1
+      if base < target_blocks:
+        P = max(1, min(-(-target_blocks // base), -(-R // (rows_per_step * 4))))
+      chunk = -(-R // P)
+      P = -(-R // chunk)
+      nblk = base * P
+      args.aux[0], args.aux[1], args.aux[2], args.aux[3] = P, chunk, lpr.bit_length() - 1, CT
+    if nblk > 0x7fffffff:
+      raise NotImplementedError('reduction grid too large')
+    args.flags = 1 if vec_ok else 0
+    if arg:
+      g = idx_geom or {}
+      args.aux[4] = g.get('offset', 0)
+      args.aux[5] = 1 if g.get('decompose') else 0
+      if g.get('decompose'):
+        tshape, tul, ashape = g['tshape'], g['tul'], g['ashape']
+        args.aux[6] = len(tshape)
+        for d in range(len(tshape)):
+          args.tshape[d], args.tul[d], args.ashape[d] = tshape[d], tul[d], ashape[d]
+    if arg:
+      direct = P == 1
+      part_v = res_v if direct else torch.empty((P * n_out,), dtype=torch_dtype(adt), device=dev)
+      part_i = result if direct else torch.empty((P * n_out,), dtype=torch.int64, device=dev)
+    else:
+      direct = (P == 1 and adt == np.dtype(out_dtype))
+      part_v = result if direct else torch.empty((P * n_out,), dtype=torch_dtype(adt), device=dev)
+      part_i = None
+    args.out0 = part_v.data_ptr()
+    args.out1 = part_i.data_ptr() if arg else 0
+    src = codegen.gen_reduce(root, ins, classes, kind, op, V)
+    fn = self.kernel(src, 'spx_reduce')
+    self.launch(fn, nblk, args)
+    if not direct:
+      _check(self.lib.spx_reduce_finalize(
+          OP_CODE[op], spx_dtype(adt), spx_dtype(np.int64 if arg else out_dtype),
+          ctypes.c_void_p(part_v.data_ptr()), ctypes.c_void_p(part_i.data_ptr() if arg else 0), P, n_out,
+          ctypes.c_void_p(result.data_ptr()), ctypes.c_void_p(res_v.data_ptr() if arg else 0),
+          self.stream()), 'spx_reduce_finalize')
+    return (res_v, result) if arg else result
+
+  # ------------------------------------------------------------ finalize
+  def argcombine(self, op, vals, idx):
+    """vals/idx: [R, n] -> (val[n], idx[n]) best-of-R with first-index ties."""
+    import torch
+    R, n = vals.shape[0], vals.shape[1] if vals.dim() > 1 else 1
+    out_i = torch.empty((n,), dtype=torch.int64, device=vals.device)
+    out_v = torch.empty((n,), dtype=vals.dtype, device=vals.device)
+    _check(self.lib.spx_argreduce_combine(OP_CODE[op], spx_dtype(np_dtype(vals.dtype)),
+                                          ctypes.c_void_p(vals.data_ptr()), ctypes.c_void_p(idx.data_ptr()),
+                                          R, n, ctypes.c_void_p(out_v.data_ptr()),
+                                          ctypes.c_void_p(out_i.data_ptr()), self.stream()),
+           'spx_argreduce_combine')
+    return out_v, out_i
+
+  # ---------------------------------------------------------------- merge
+  def merge(self, dst, mask, region_ul, src, op, fastpath=True):
+    shape = tuple(dst.shape)
+    _check(self.lib.spx_merge(OP_CODE[op], spx_dtype(np_dtype(dst.dtype)), ctypes.c_void_p(dst.data_ptr()),
+                              ctypes.c_void_p(mask.data_ptr() if mask is not None else 0), len(shape),
+                              _arr(shape), _arr(region_ul), _arr(tuple(src.shape) if src.dim() else ()),
+                              ctypes.c_void_p(src.data_ptr()), spx_dtype(np_dtype(src.dtype)),
+                              1 if fastpath else 0, self.stream()), 'spx_merge')
+
+  def copy_region(self, dst, dst_ul, src, src_ul, shape):
+    nd = len(shape)
+    _check(self.lib.spx_copy_region(spx_dtype(np_dtype(dst.dtype)), ctypes.c_void_p(dst.data_ptr()),
+                                    _arr(tuple(dst.shape)), _arr(dst_ul), spx_dtype(np_dtype(src.dtype)),
+                                    ctypes.c_void_p(src.data_ptr()), _arr(tuple(src.shape)), _arr(src_ul), nd,
+                                    _arr(shape), self.stream()), 'spx_copy_region')
+
+  # ----------------------------------------------------------------- gemm
+  def gemm(self, A, B, C, alpha=1.0, beta=0.0):
+    """C = alpha * A @ B + beta * C for 2-d contiguous row-major tensors."""
+    M, K = A.shape
+    K2, N = B.shape
+    assert K == K2 and tuple(C.shape) == (M, N)
+    dt = np_dtype(A.dtype)
+    _check(self.lib.spx_gemm(spx_dtype(dt), M, N, K, ctypes.c_void_p(A.data_ptr()), A.stride(0),
+                             ctypes.c_void_p(B.data_ptr()), B.stride(0), ctypes.c_void_p(C.data_ptr()),
+                             C.stride(0), float(alpha), float(beta), self.stream()), 'spx_gemm')
+
+
+def out_device(inputs, slots):
+  import torch
+  if slots:
+    return inputs[slots[0]].device
+  return torch.device('cuda', torch.cuda.current_device())
+
+
+def _cls(stride):
+  return 'c' if stride == 1 else ('b' if stride == 0 else 'g')
+
+
+def _aligned_ptr(t, V):
+  return t.data_ptr() % (V * t.element_size()) == 0
+
+
+def _vec_aligned(t, strides, cls, V):
+  if cls == 'c':
+    return _aligned_ptr(t, V) and all(s % V == 0 for s in strides[:-1])
+  return True
+
+
+def _scalars_into(root, args):
+  for node in codegen.walk(root):
+    if isinstance(node, codegen.Sc):
+      if node.pytype is float:
+        args.fsc[node.slot] = node.value
+      else:
+        args.isc[node.slot] = int(node.value)
+
+
+# ----------------------------------------------------------- active backend
+_backend = None
+
+
+def get():
+  global _backend
+  if _backend is None:
+    _backend = HipBackend()
+  return _backend
+
+
+def set_backend(b):
+  """Install a backend object (tests only); returns the previous one."""
+  global _backend
+  prev = _backend
+  _backend = b
+  return prev

@@ -1,0 +1,656 @@
+"""LocalExpr tree -> generated gfx950 HIP kernels.
+
+The reference evaluates a fused map as a tree of NumPy ufunc calls per tile,
+materialising one full-tile temporary per node (FnCallExpr.evaluate,
+spartan/expr/local.py:110-122); its only codegen hook is the default-off
+Parakeet pass (spartan/expr/optimize.py:260-365).  Here the tree that
+MapMapFusion / ReduceMapFusion build is lowered to a small IR (``In``, ``Sc``,
+``Const``, ``Op``, ``Cast``) with NumPy's own dtype resolution
+(``ufunc.resolve_dtypes``), and the IR is emitted as straight-line HIP C++
+inside one of three streaming kernel skeletons:
+
+  * ``map``      -- elementwise; a dense fast path (flat index, 16-byte vector
+                    loads/stores) and a general N-d strided/broadcast path;
+  * ``rows``     -- reduce over a contiguous axis, (O, R) view, one or more
+                    256-thread blocks per segment, wave/LDS tree at the end;
+  * ``cols``     -- reduce over a strided axis, (O, R, I) view, lanes along the
+                    contiguous I dim (coalesced 1 KiB per wave-instruction),
+                    waves interleaved over R, LDS combine.
+
+Reductions write partials [P][...] in the accumulator type; P > 1 partials are
+combined deterministically by spx_reduce_finalize.
+
+The source is compiled by ``backend.compile_kernel`` (device-only clang,
+code object cached on disk by source hash) and launched through the C ABI
+(spx_launch).  Nothing here executes on the CPU.
+"""
+import ctypes
+
+import numpy as np
+
+MAX_IN = 16
+MAX_DIM = 8
+
+# --------------------------------------------------------------------- IR
+
+class In:
+  """Array input ``slot`` (a device tile, possibly broadcast)."""
+  __slots__ = ('slot', 'dtype')
+
+  def __init__(self, slot, dtype):
+    self.slot, self.dtype = slot, np.dtype(dtype)
+
+  def sig(self):
+    return 'i%d:%s' % (self.slot, self.dtype.str)
+
+
+class Sc:
+  """Scalar constant passed through the kernel arguments (NumPy 'weak' scalar)."""
+  __slots__ = ('slot', 'pytype', 'dtype', 'value')
+
+  def __init__(self, slot, value):
+    if isinstance(value, (bool, np.bool_)):
+      self.pytype, self.dtype, self.value = bool, np.dtype(np.bool_), bool(value)
+    elif isinstance(value, (int, np.integer)):
+      self.pytype, self.dtype, self.value = int, np.dtype(np.int64), int(value)
+    else:
+      self.pytype, self.dtype, self.value = float, np.dtype(np.float64), float(value)
+    self.slot = slot
+
+  def sig(self):
+    return 's%d:%s' % (self.slot, self.pytype.__name__)
+
+
+class Const:
+  """Array-valued constant (``ones``/``zeros`` tiles): strong dtype, no memory."""
+  __slots__ = ('value', 'dtype')
+
+  def __init__(self, value, dtype):
+    self.value, self.dtype = value, np.dtype(dtype)
+
+  def sig(self):
+    return 'c%r:%s' % (self.value, self.dtype.str)
+
+
+class Op:
+  __slots__ = ('name', 'args', 'in_dtypes', 'dtype')
+
+  def __init__(self, name, args):
+    self.name = name
+    self.args = list(args)
+    uf = getattr(np, name)
+    keys = tuple(a.pytype if isinstance(a, Sc) else a.dtype for a in self.args)
+    try:
+      res = uf.resolve_dtypes(keys + (None,) * uf.nout)
+    except Exception as e:  # pragma: no cover - numpy raises for invalid combos
+      raise TypeError('ufunc %s has no loop for %s: %s' % (name, keys, e))
+    self.in_dtypes = tuple(np.dtype(d) for d in res[:uf.nin])
+    self.dtype = np.dtype(res[uf.nin])
+
+  def sig(self):
+    return '%s(%s)' % (self.name, ','.join(a.sig() for a in self.args))
+
+
+class Cast:
+  __slots__ = ('arg', 'dtype')
+
+  def __init__(self, arg, dtype):
+    self.arg, self.dtype = arg, np.dtype(dtype)
+
+  def sig(self):
+    return 'cast<%s>(%s)' % (self.dtype.str, self.arg.sig())
+
+
+def walk(node):
+  yield node
+  if isinstance(node, Op):
+    for a in node.args:
+      yield from walk(a)
+  elif isinstance(node, Cast):
+    yield from walk(node.arg)
+
+
+# ------------------------------------------------------------ C emission
+
+CTYPE = {'?': 'u8', 'i1': 'signed char', 'u1': 'u8', 'i2': 'short', 'i4': 'int', 'i8': 'i64',
+         'f4': 'float', 'f8': 'double'}
+
+
+def ctype(dt):
+  dt = np.dtype(dt)
+  key = '?' if dt.kind == 'b' else dt.str[1:]
+  if key not in CTYPE:
+    raise TypeError('dtype %s not supported by the gfx950 codegen' % dt)
+  return CTYPE[key]
+
+
+def is_float(dt):
+  return np.dtype(dt).kind == 'f'
+
+
+def is_bool(dt):
+  return np.dtype(dt).kind == 'b'
+
+
+OCML_1 = {  # name -> ocml suffix (f32/f64 variants)
+    'exp': 'exp', 'log': 'log', 'sqrt': 'sqrt', 'sin': 'sin', 'cos': 'cos', 'tan': 'tan',
+    'tanh': 'tanh', 'sinh': 'sinh', 'cosh': 'cosh', 'arcsin': 'asin', 'arccos': 'acos',
+    'arctan': 'atan', 'exp2': 'exp2', 'log2': 'log2', 'log10': 'log10', 'expm1': 'expm1',
+    'log1p': 'log1p', 'floor': 'floor', 'ceil': 'ceil', 'trunc': 'trunc', 'rint': 'rint',
+    'cbrt': 'cbrt', 'fabs': 'fabs',
+}
+OCML_2 = {'power': 'pow', 'arctan2': 'atan2', 'fmod': 'fmod', 'hypot': 'hypot'}
+
+
+class Emitter:
+  """Emits the statements computing one element of the IR tree."""
+
+  def __init__(self):
+    self.ocml = set()
+    self.lines = []
+    self.n = 0
+
+  def tmp(self, ct, expr):
+    name = 't%d' % self.n
+    self.n += 1
+    self.lines.append('%s %s = %s;' % (ct, name, expr))
+    return name
+
+  def conv(self, val, src_dt, dst_dt):
+    src_dt, dst_dt = np.dtype(src_dt), np.dtype(dst_dt)
+    if src_dt == dst_dt:
+      return val
+    if is_bool(dst_dt):
+      return '(u8)((%s) != 0)' % val
+    return '(%s)(%s)' % (ctype(dst_dt), val)
+
+  def ocml_call(self, fname, dt, args):
+    suf = 'f32' if np.dtype(dt) == np.float32 else 'f64'
+    full = '__ocml_%s_%s' % (fname, suf)
+    self.ocml.add((full, ctype(dt), len(args)))
+    return '%s(%s)' % (full, ', '.join(args))
+
+  def emit(self, node, leaf):
+    """Return a C expression (usually a temporary) of node.dtype."""
+    if isinstance(node, In):
+      return leaf(node)
+    if isinstance(node, Sc):
+      return leaf(node)
+    if isinstance(node, Const):
+      if is_float(node.dtype):
+        return '(%s)%r' % (ctype(node.dtype), float(node.value))
+      return '(%s)%d' % (ctype(node.dtype), int(node.value))
+    if isinstance(node, Cast):
+      v = self.emit(node.arg, leaf)
+      return self.tmp(ctype(node.dtype), self.conv(v, node.arg.dtype, node.dtype))
+    assert isinstance(node, Op)
+    args = [self.conv(self.emit(a, leaf), a.dtype, t) for a, t in zip(node.args, node.in_dtypes)]
+    return self.tmp(ctype(node.dtype), self.op_expr(node, args))
+
+  def op_expr(self, node, a):
+    name = node.name
+    T = node.in_dtypes[0] if node.in_dtypes else node.dtype
+    fl = is_float(T)
+    bl = is_bool(T)
+    ct = ctype(T)
+    if name == 'add':
+      return '(u8)(%s | %s)' % (a[0], a[1]) if bl else '%s + %s' % (a[0], a[1])
+    if name == 'subtract':
+      return '%s - %s' % (a[0], a[1])
+    if name == 'multiply':
+      return '(u8)(%s & %s)' % (a[0], a[1]) if bl else '%s * %s' % (a[0], a[1])
+    if name in ('true_divide', 'divide'):
+      return '%s / %s' % (a[0], a[1])
+    if name == 'floor_divide':
+      if fl:
+        return self.ocml_call('floor', T, ['%s / %s' % (a[0], a[1])])
+      return 'fdiv_i(%s, %s)' % (a[0], a[1])
+    if name in ('remainder', 'mod'):
+      if fl:
+        return 'fmod_py(%s, %s)' % (a[0], a[1]) if self.ocml_call('fmod', T, [a[0], a[1]]) else ''
+      return 'fmod_i(%s, %s)' % (a[0], a[1])
+    if name == 'negative':
+      return '-%s' % a[0]
+    if name == 'positive':
+      return a[0]
+    if name == 'absolute':
+      if fl:
+        return self.ocml_call('fabs', T, [a[0]])
+      return '(%s < 0 ? -%s : %s)' % (a[0], a[0], a[0]) if not bl else a[0]
+    if name == 'square':
+      return '%s * %s' % (a[0], a[0])
+    if name == 'reciprocal':
+      return '(%s)1 / %s' % (ct, a[0])
+    if name == 'sign':
+      return '(%s)((%s > 0) - (%s < 0))' % (ct, a[0], a[0]) if not fl else \
+             '(%s != %s ? %s : (%s)((%s > 0) - (%s < 0)))' % (a[0], a[0], a[0], ct, a[0], a[0])
+    if name in ('maximum', 'minimum'):
+      cmp = '>' if name == 'maximum' else '<'
+      if fl:  # NaN propagates like np.maximum / np.minimum
+        return '((%s != %s) ? %s : ((%s != %s) ? %s : (%s %s %s ? %s : %s)))' % (
+            a[0], a[0], a[0], a[1], a[1], a[1], a[0], cmp, a[1], a[0], a[1])
+      return '(%s %s %s ? %s : %s)' % (a[0], cmp, a[1], a[0], a[1])
+    if name in ('fmax', 'fmin'):
+      return self.ocml_call(name, T, [a[0], a[1]])
+    cmps = {'equal': '==', 'not_equal': '!=', 'less': '<', 'less_equal': '<=', 'greater': '>',
+            'greater_equal': '>='}
+    if name in cmps:
+      return '(u8)(%s %s %s)' % (a[0], cmps[name], a[1])
+    if name == 'logical_and':
+      return '(u8)((%s != 0) && (%s != 0))' % (a[0], a[1])
+    if name == 'logical_or':
+      return '(u8)((%s != 0) || (%s != 0))' % (a[0], a[1])
+    if name == 'logical_xor':
+      return '(u8)((%s != 0) != (%s != 0))' % (a[0], a[1])
+    if name == 'logical_not':
+      return '(u8)(%s == 0)' % a[0]
+    if name == 'isnan':
+      return '(u8)(%s != %s)' % (a[0], a[0])
+    if name == 'isinf':
+      return '(u8)(%s == (%s)__builtin_inf() || %s == -(%s)__builtin_inf())' % (a[0], ct, a[0], ct)
+    if name == 'isfinite':
+      return '(u8)(%s - %s == (%s)0)' % (a[0], a[0], ct)
+    if name == 'power':
+      if fl:
+        return self.ocml_call('pow', T, [a[0], a[1]])
+      return 'ipow(%s, %s)' % (a[0], a[1])
+    if name in OCML_1 and fl:
+      return self.ocml_call(OCML_1[name], T, [a[0]])
+    if name in OCML_2 and fl:
+      return self.ocml_call(OCML_2[name], T, [a[0], a[1]])
+    raise NotImplementedError('ufunc %s has no gfx950 lowering' % name)
+
+
+PRELUDE = r'''
+typedef long long i64;
+typedef unsigned long long u64;
+typedef unsigned int u32;
+typedef unsigned char u8;
+#define DEV static __attribute__((device)) inline __attribute__((always_inline))
+#define KERN extern "C" __attribute__((global)) __attribute__((amdgpu_flat_work_group_size(256, 256)))
+#define SHARED __attribute__((shared))
+#define GLOBAL __attribute__((address_space(1)))
+DEV u32 tid() { return __builtin_amdgcn_workitem_id_x(); }
+DEV u32 bidx() { return __builtin_amdgcn_workgroup_id_x(); }
+DEV void bsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+DEV i64 fdiv_i(i64 a, i64 b) { if (b == 0) return 0; i64 q = a / b; if ((a % b != 0) && ((a < 0) != (b < 0))) q -= 1; return q; }
+DEV i64 fmod_i(i64 a, i64 b) { if (b == 0) return 0; i64 r = a % b; if (r != 0 && ((r < 0) != (b < 0))) r += b; return r; }
+DEV i64 ipow(i64 a, i64 b) { i64 r = 1; while (b > 0) { if (b & 1) r *= a; a *= a; b >>= 1; } return r; }
+struct KArgs {
+  u64 ptr[16];
+  u64 out0, out1;
+  i64 dim[8];
+  i64 str[16][8];
+  double fsc[16];
+  i64 isc[16];
+  i64 n;
+  i64 aux[8];
+  i64 tshape[8], tul[8], ashape[8];
+  u32 flags, grid;
+};
+'''
+
+
+class KArgs(ctypes.Structure):
+  _fields_ = [
+      ('ptr', ctypes.c_uint64 * 16),
+      ('out0', ctypes.c_uint64),
+      ('out1', ctypes.c_uint64),
+      ('dim', ctypes.c_int64 * 8),
+      ('str', (ctypes.c_int64 * 8) * 16),
+      ('fsc', ctypes.c_double * 16),
+      ('isc', ctypes.c_int64 * 16),
+      ('n', ctypes.c_int64),
+      ('aux', ctypes.c_int64 * 8),
+      ('tshape', ctypes.c_int64 * 8),
+      ('tul', ctypes.c_int64 * 8),
+      ('ashape', ctypes.c_int64 * 8),
+      ('flags', ctypes.c_uint32),
+      ('grid', ctypes.c_uint32),
+  ]
+
+
+def _ocml_decls(ocml):
+  out = []
+  for full, ct, nargs in sorted(ocml):
+    out.append('extern "C" __attribute__((device)) %s %s(%s);' % (ct, full, ', '.join([ct] * nargs)))
+  if any(f.startswith('__ocml_fmod') for f, _, _ in ocml):
+    for full, ct, nargs in sorted(ocml):
+      if full.startswith('__ocml_fmod'):
+        out.append('DEV %s fmod_py(%s a, %s b) { %s r = %s(a, b); if (r != 0 && ((r < 0) != (b < 0))) r += b; return r; }'
+                   % (ct, ct, ct, ct, full))
+  return '\n'.join(out)
+
+
+# ---------------------------------------------------------- input classes
+# Per array input, how its innermost iteration dim is addressed:
+#   'c' contiguous (stride 1, vector loads), 'b' broadcast (stride 0),
+#   'g' gather (any other stride).
+
+def _load_vec(slot, dt, cls, off, V):
+  """Statements loading V consecutive elements (along the innermost dim) into x<slot>[V]."""
+  ct = ctype(dt)
+  p = '((const GLOBAL %s*)a.ptr[%d])' % (ct, slot)
+  if V == 1:
+    return ['%s x%d_0 = %s[%s];' % (ct, slot, p, off)]
+  if cls == 'c':
+    vt = '%s __attribute__((ext_vector_type(%d)))' % (ct, V)
+    lines = ['typedef %s vt%d;' % (vt, slot),
+             'vt%d xv%d = *(const GLOBAL vt%d*)(%s + %s);' % (slot, slot, slot, p, off)]
+    lines += ['%s x%d_%d = xv%d[%d];' % (ct, slot, j, slot, j) for j in range(V)]
+    return lines
+  if cls == 'b':
+    lines = ['%s x%d_0 = %s[%s];' % (ct, slot, p, off)]
+    lines += ['%s x%d_%d = x%d_0;' % (ct, slot, j, slot) for j in range(1, V)]
+    return lines
+  return ['%s x%d_%d = %s[%s + %d * s%d_in];' % (ct, slot, j, p, off, j, slot) for j in range(V)]
+
+
+def _expr_fn(root, n_in, name='fexpr'):
+  """Device function computing the tree for one element from x<slot> scalars."""
+  em = Emitter()
+
+  def leaf(node):
+    if isinstance(node, In):
+      return 'x%d' % node.slot
+    if node.pytype is float:
+      return 'a.fsc[%d]' % node.slot
+    return 'a.isc[%d]' % node.slot
+
+  val = em.emit(root, leaf)
+  params = ', '.join(['const KArgs& a'] + ['%s x%d' % (ctype(dt), s) for s, dt in n_in])
+  body = '\n  '.join(em.lines + ['return %s;' % val])
+  fn = 'DEV %s %s(%s) {\n  %s\n}' % (ctype(root.dtype), name, params, body)
+  return fn, em.ocml
+
+
+def _call_expr(inputs, j, name='fexpr'):
+  return '%s(a%s)' % (name, ''.join(', x%d_%d' % (s, j) for s, _ in inputs))
+
+
+# ---------------------------------------------------------------- map
+def gen_map(root, inputs, classes, ndim, vec, dense):
+  """Elementwise kernel.  inputs: [(slot, dtype)], classes: per-input 'c'/'b'/'g'.
+
+  dense=True: every input is contiguous with the output's shape (flat index).
+  Otherwise the N-d path: offsets from the iteration index via dim[] / str[][].
+  """
+  fn, ocml = _expr_fn(root, inputs)
+  out_ct = ctype(root.dtype)
+  L = []
+
+  def body(V, dense_):
+    b = []
+    if dense_:
+      offs = {s: 'e' for s, _ in inputs}
+    else:
+      b.append('i64 rem = e;')
+      for s, _ in inputs:
+        b.append('i64 o%d = 0;' % s)
+      for d in range(ndim - 1, -1, -1):
+        b.append('{ i64 q = rem / a.dim[%d]; i64 ix = rem - q * a.dim[%d]; rem = q;' % (d, d))
+        for s, _ in inputs:
+          b.append('  o%d += ix * a.str[%d][%d];' % (s, s, d))
+        b.append('}')
+      offs = {s: 'o%d' % s for s, _ in inputs}
+    for (s, dt), cls in zip(inputs, classes):
+      if not dense_ and cls == 'g' and V > 1:
+        b.append('const i64 s%d_in = a.str[%d][%d];' % (s, s, ndim - 1))
+      b += _load_vec(s, dt, 'c' if dense_ else cls, offs[s], V)
+    outp = '((GLOBAL %s*)a.out0)' % out_ct
+    if V == 1:
+      b.append('%s[e] = %s;' % (outp, _call_expr(inputs, 0)))
+    else:
+      b.append('typedef %s __attribute__((ext_vector_type(%d))) vo;' % (out_ct, V))
+      b.append('vo r;')
+      for j in range(V):
+        b.append('r[%d] = %s;' % (j, _call_expr(inputs, j)))
+      b.append('*(GLOBAL vo*)(%s + e) = r;' % outp)
+    return b
+
+  L.append('KERN void spx_map(KArgs a) {')
+  L.append('  const i64 n = a.n;')
+  L.append('  if (a.flags & 1) {')
+  L.append('    const i64 step = (i64)a.grid * 256 * %d;' % vec)
+  L.append('    for (i64 e = ((i64)bidx() * 256 + tid()) * %d; e < n; e += step) {' % vec)
+  L += ['      ' + x for x in body(vec, dense)]
+  L.append('    }')
+  L.append('  } else {')
+  L.append('    const i64 step = (i64)a.grid * 256;')
+  L.append('    for (i64 e = (i64)bidx() * 256 + tid(); e < n; e += step) {')
+  L += ['      ' + x for x in body(1, dense)]
+  L.append('    }')
+  L.append('  }')
+  L.append('}')
+  src = '\n'.join([PRELUDE, _ocml_decls(ocml), fn, '\n'.join(L)])
+  return src
+
+
+# -------------------------------------------------------------- reduce
+REDOPS = ('sum', 'min', 'max', 'argmin', 'argmax')
+
+
+def acc_dtype(op, dt):
+  dt = np.dtype(dt)
+  if op == 'sum':
+    if dt.kind in 'biu':
+      return np.dtype(np.int64)
+    return dt
+  if op in ('min', 'max'):
+    if dt.kind == 'b':
+      return np.dtype(np.int64)
+    return dt
+  # arg ops keep the value type
+  if dt.kind == 'b':
+    return np.dtype(np.int64)
+  return dt
+
+
+def _ident(op, dt):
+  ct = ctype(dt)
+  if op == 'sum':
+    return '(%s)0' % ct
+  if is_float(dt):
+    return '(%s)__builtin_inf()' % ct if op in ('min', 'argmin') else '-(%s)__builtin_inf()' % ct
+  if op in ('min', 'argmin'):
+    return '(%s)0x7fffffffffffffffLL' % ct
+  return '(%s)(-0x7fffffffffffffffLL - 1)' % ct
+
+
+def _comb_fns(op, adt):
+  """Device helpers: comb(acc, v) and for arg ops better(v, vi, b, bi)."""
+  ct = ctype(adt)
+  fl = is_float(adt)
+  if op == 'sum':
+    return 'DEV %s comb(%s x, %s y) { return x + y; }' % (ct, ct, ct)
+  if op in ('min', 'max'):
+    c = '<' if op == 'min' else '>'
+    if fl:
+      return ('DEV %s comb(%s x, %s y) { if (x != x) return x; if (y != y) return y; return (y %s x) ? y : x; }'
+              % (ct, ct, ct, c))
+    return 'DEV %s comb(%s x, %s y) { return (y %s x) ? y : x; }' % (ct, ct, ct, c)
+  c = '<' if op == 'argmin' else '>'
+  if fl:
+    return ('DEV bool better(%s v, i64 vi, %s b, i64 bi) {\n'
+            '  bool vn = v != v, bn = b != b;\n'
+            '  if (vn || bn) { if (vn && !bn) return true; if (!vn && bn) return false; return vi < bi; }\n'
+            '  if (v == b) return vi < bi;\n'
+            '  return v %s b;\n}' % (ct, ct, c))
+  return ('DEV bool better(%s v, i64 vi, %s b, i64 bi) { if (v == b) return vi < bi; return v %s b; }'
+          % (ct, ct, c))
+
+
+def _acc_update(op, j, val, idx_expr):
+  if op in ('argmin', 'argmax'):
+    return ('{ auto v_ = %s; i64 vi_ = %s; if (better(v_, vi_, acc%d, acci%d)) { acc%d = v_; acci%d = vi_; } }'
+            % (val, idx_expr, j, j, j, j))
+  return 'acc%d = comb(acc%d, %s);' % (j, j, val)
+
+
+def gen_reduce(root, inputs, classes, kind, op, vec):
+  """Fused map+reduce.  kind 'rows' (reduce over contiguous R of (O, R)) or
+  'cols' (reduce over R of (O, R, I), I contiguous).
+
+  classes: per-input addressing class of the vectorised dimension (R for rows,
+  I for cols): 'c', 'b' or 'g'.
+  """
+  assert op in REDOPS and kind in ('rows', 'cols')
+  fn, ocml = _expr_fn(root, inputs)
+  adt = acc_dtype(op, root.dtype)
+  act = ctype(adt)
+  arg = op in ('argmin', 'argmax')
+  L = [PRELUDE, _ocml_decls(ocml), fn, _comb_fns(op, adt)]
+
+  def val_j(j):
+    return '(%s)%s' % (act, _call_expr(inputs, j))
+
+  def loads(V, base_expr, vdim):
+    b = []
+    for (s, dt), cls in zip(inputs, classes):
+      b.append('const i64 off%d = %s;' % (s, base_expr(s)))
+      if cls == 'g' and V > 1:
+        b.append('const i64 s%d_in = a.str[%d][%d];' % (s, s, vdim))
+      b += _load_vec(s, dt, cls, 'off%d' % s, V)
+    return b
+
+  def gidx(r_expr):
+    # global index of element r along the reduced dim (axis) or flat (axis None)
+    return ('(a.aux[5] ? gflat(a, %s) : a.aux[4] + %s)' % (r_expr, r_expr))
+
+  if arg:
+    L.append('''DEV i64 gflat(const KArgs& a, i64 r) {
+  i64 rem = r, g = 0, mul = 1;
+  for (int d = (int)a.aux[6] - 1; d >= 0; --d) {
+    i64 q = rem / a.tshape[d]; i64 li = rem - q * a.tshape[d]; rem = q;
+    g += (li + a.tul[d]) * mul; mul *= a.ashape[d];
+  }
+  return g;
+}''')
+
+  if kind == 'rows':
+    def body(V):
+      b = []
+      b.append('for (i64 r = r0 + (i64)tid() * %d; r < r1; r += 256 * %d) {' % (V, V))
+      b += ['  ' + x for x in loads(V, lambda s: 'o * a.str[%d][0] + r * a.str[%d][1]' % (s, s), 1)]
+      for j in range(V):
+        b.append('  ' + _acc_update(op, j, val_j(j), gidx('r + %d' % j)))
+      b.append('}')
+      return b
+
+    L.append('KERN void spx_reduce(KArgs a) {')
+    L.append('  const i64 O = a.dim[0], R = a.dim[1], P = a.aux[0], chunk = a.aux[1];')
+    L.append('  const i64 blk = bidx(); const i64 o = blk / P, p = blk - o * P;')
+    L.append('  const i64 r0 = p * chunk; i64 r1 = r0 + chunk; if (r1 > R) r1 = R;')
+    for j in range(vec):
+      L.append('  %s acc%d = %s;' % (act, j, _ident(op, adt)))
+      if arg:
+        L.append('  i64 acci%d = 0x7fffffffffffffffLL;' % j)
+    L.append('  if (a.flags & 1) {')
+    L += ['    ' + x for x in body(vec)]
+    L.append('  } else {')
+    L += ['    ' + x for x in body(1)]
+    L.append('  }')
+    # fold the V slots in index order, then block tree
+    L.append('  %s accv = acc0;' % act)
+    if arg:
+      L.append('  i64 acci = acci0;')
+    for j in range(1, vec):
+      if arg:
+        L.append('  if (better(acc%d, acci%d, accv, acci)) { accv = acc%d; acci = acci%d; }' % (j, j, j, j))
+      else:
+        L.append('  accv = comb(accv, acc%d);' % j)
+    L.append('  SHARED %s sv[256];' % act)
+    if arg:
+      L.append('  SHARED i64 si[256];')
+    L.append('  const u32 t = tid();')
+    L.append('  sv[t] = accv;' + (' si[t] = acci;' if arg else ''))
+    L.append('  bsync();')
+    L.append('  for (u32 s = 128; s > 0; s >>= 1) {')
+    L.append('    if (t < s) {')
+    if arg:
+      L.append('      if (better(sv[t + s], si[t + s], sv[t], si[t])) { sv[t] = sv[t + s]; si[t] = si[t + s]; }')
+    else:
+      L.append('      sv[t] = comb(sv[t], sv[t + s]);')
+    L.append('    }')
+    L.append('    bsync();')
+    L.append('  }')
+    L.append('  if (t == 0) {')
+    L.append('    ((GLOBAL %s*)a.out0)[p * O + o] = sv[0];' % act)
+    if arg:
+      L.append('    ((GLOBAL i64*)a.out1)[p * O + o] = si[0];')
+    L.append('  }')
+    L.append('}')
+  else:
+    def body(V):
+      b = []
+      b.append('if (col < I) {')
+      b.append('  for (i64 r = r0 + w * RPW + sub; r < r1; r += 4 * RPW) {')
+      b += ['    ' + x for x in loads(
+          V, lambda s: 'o * a.str[%d][0] + r * a.str[%d][1] + col * a.str[%d][2]' % (s, s, s), 2)]
+      for j in range(V):
+        if V > 1:
+          b.append('    ' + _acc_update(op, j, val_j(j), gidx('r')))
+        else:
+          b.append('    ' + _acc_update(op, 0, val_j(0), gidx('r')))
+      b.append('  }')
+      b.append('}')
+      return b
+
+    L.append('KERN void spx_reduce(KArgs a) {')
+    L.append('  const i64 O = a.dim[0], R = a.dim[1], I = a.dim[2];')
+    L.append('  const i64 P = a.aux[0], chunk = a.aux[1], lpr_log = a.aux[2], CT = a.aux[3];')
+    L.append('  const i64 LPR = (i64)1 << lpr_log, RPW = 64 >> lpr_log;')
+    L.append('  const i64 blk = bidx(); const i64 ct = blk % CT; const i64 rest = blk / CT;')
+    L.append('  const i64 o = rest % O, p = rest / O;')
+    L.append('  const u32 t = tid(); const i64 lane = t & 63, w = t >> 6;')
+    L.append('  const i64 sub = lane >> lpr_log, cl = lane & (LPR - 1);')
+    L.append('  const i64 V = (a.flags & 1) ? %d : 1;' % vec)
+    L.append('  const i64 col = ct * (LPR * V) + cl * V;')
+    L.append('  const i64 r0 = p * chunk; i64 r1 = r0 + chunk; if (r1 > R) r1 = R;')
+    for j in range(vec):
+      L.append('  %s acc%d = %s;' % (act, j, _ident(op, adt)))
+      if arg:
+        L.append('  i64 acci%d = 0x7fffffffffffffffLL;' % j)
+    L.append('  if (a.flags & 1) {')
+    L += ['    ' + x for x in body(vec)]
+    L.append('  } else {')
+    L += ['    ' + x for x in body(1)]
+    L.append('  }')
+    # LDS combine over the 4*RPW row groups sharing a column, in row-group order
+    L.append('  SHARED %s sv[256 * %d];' % (act, vec))
+    if arg:
+      L.append('  SHARED i64 si[256 * %d];' % vec)
+    L.append('  const i64 grp = w * RPW + sub;')
+    L.append('  const i64 W = LPR * V;')
+    for j in range(vec):
+      L.append('  if (%d < V) { sv[grp * W + cl * V + %d] = acc%d;%s }'
+               % (j, j, j, (' si[grp * W + cl * V + %d] = acci%d;' % (j, j)) if arg else ''))
+    L.append('  bsync();')
+    L.append('  if ((i64)t < W) {')
+    L.append('    %s b = sv[t];' % act)
+    if arg:
+      L.append('    i64 bi = si[t];')
+    L.append('    for (i64 g = 1; g < 4 * RPW; ++g) {')
+    if arg:
+      L.append('      if (better(sv[g * W + t], si[g * W + t], b, bi)) { b = sv[g * W + t]; bi = si[g * W + t]; }')
+    else:
+      L.append('      b = comb(b, sv[g * W + t]);')
+    L.append('    }')
+    L.append('    const i64 gc = ct * W + t;')
+    L.append('    if (gc < I) {')
+    L.append('      ((GLOBAL %s*)a.out0)[(p * O + o) * I + gc] = b;' % act)
+    if arg:
+      L.append('      ((GLOBAL i64*)a.out1)[(p * O + o) * I + gc] = bi;')
+    L.append('    }')
+    L.append('  }')
+    L.append('}')
+  return '\n'.join(L)
+
+
+def vec_width(dtypes):
+  m = max(np.dtype(d).itemsize for d in dtypes)
+  return max(1, 16 // m)

@@ -1,0 +1,97 @@
+"""Cross-rank data movement for tiles (torch.distributed: RCCL on GPU, gloo in tests).
+
+Replaces the reference's pickled ZeroMQ point-to-point messages
+(spartan/rpc/common.py:52-62, spartan/blob_ctx.py:127-179): every exchange here
+is a collective that all ranks enter with identical arguments, because every
+rank computes the same tile plan (SPMD).
+"""
+import numpy as np
+
+from . import runtime
+
+_OPS = {'sum': 'SUM', 'min': 'MIN', 'max': 'MAX'}
+
+
+def _dist():
+  import torch.distributed as dist
+  return dist
+
+
+def all_reduce(t, op):
+  ctx = runtime.get()
+  if not ctx.distributed:
+    return t
+  dist = _dist()
+  dist.all_reduce(t, op=getattr(dist.ReduceOp, _OPS[op]))
+  return t
+
+
+def reduce_scatter_rows(out, full, op):
+  """out = rank-th equal row slab of the element-wise reduction of ``full``."""
+  ctx = runtime.get()
+  dist = _dist()
+  if ctx.dist_backend == 'gloo':  # gloo has no reduce_scatter: all_reduce + slice
+    dist.all_reduce(full, op=getattr(dist.ReduceOp, _OPS[op]))
+    n = out.shape[0]
+    out.copy_(full[ctx.rank * n:(ctx.rank + 1) * n])
+    return out
+  dist.reduce_scatter_tensor(out, full, op=getattr(dist.ReduceOp, _OPS[op]))
+  return out
+
+
+def all_gather_stack(t):
+  """[world, *t.shape] stack of every rank's ``t`` (same shape on all ranks)."""
+  import torch
+  ctx = runtime.get()
+  if not ctx.distributed:
+    return t.unsqueeze(0)
+  dist = _dist()
+  out = torch.empty((ctx.world_size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+  dist.all_gather_into_tensor(out, t.contiguous()) if ctx.dist_backend != 'gloo' else \
+      dist.all_gather(list(out.unbind(0)), t.contiguous())
+  return out
+
+
+def broadcast(t, src_rank):
+  ctx = runtime.get()
+  if not ctx.distributed:
+    return t
+  _dist().broadcast(t, src=src_rank)
+  return t
+
+
+def all_to_all_single(out, inp, out_splits, in_splits):
+  _dist().all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits)
+  return out
+
+
+def exchange(sends, recvs):
+  """Point-to-point batch.  sends: [(tensor, dst_rank)], recvs: [(tensor, src_rank)].
+
+  Every rank passes the pairs it takes part in; messages between the same pair
+  of ranks are matched in list order."""
+  ctx = runtime.get()
+  if not ctx.distributed or (not sends and not recvs):
+    return
+  dist = _dist()
+  ops = [dist.P2POp(dist.isend, t.contiguous(), peer) for t, peer in sends]
+  ops += [dist.P2POp(dist.irecv, t, peer) for t, peer in recvs]
+  for req in dist.batch_isend_irecv(ops):
+    req.wait()
+
+
+def barrier():
+  ctx = runtime.get()
+  if ctx.distributed:
+    _dist().barrier()
+
+
+def max_over_ranks(x):
+  """Max of a host float over all ranks (bench timing)."""
+  import torch
+  ctx = runtime.get()
+  if not ctx.distributed:
+    return x
+  t = torch.tensor([float(x)], dtype=torch.float64, device=ctx.device)
+  all_reduce(t, 'max')
+  return float(t.item())

@@ -1,0 +1,818 @@
+// libspx.so -- MI355X (gfx950) tile-execution kernels behind include/spx.h.
+//
+// This file holds the ahead-of-time kernels (fills, reduction finalize, tile
+// merge, region copy, MFMA GEMM, arg-reduction combine) and the module/launch
+// plumbing for the fused map / map+reduce kernels that spartan_amd/codegen.py
+// generates per expression.  Reference call sites replaced are cited per
+// entry point in include/spx.h.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <type_traits>
+
+#include "../../include/spx.h"
+
+typedef int64_t i64;
+typedef uint64_t u64;
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_err;
+
+static int set_err(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                         \
+  do {                                                                        \
+    hipError_t e_ = (expr);                                                   \
+    if (e_ != hipSuccess)                                                     \
+      return set_err(SPX_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+#define LAUNCH_CHECK(name)                                                    \
+  do {                                                                        \
+    hipError_t e_ = hipGetLastError();                                        \
+    if (e_ != hipSuccess)                                                     \
+      return set_err(SPX_EHIP, "%s launch failed: %s", name,                  \
+                     hipGetErrorString(e_));                                  \
+  } while (0)
+
+extern "C" int spx_abi_version(void) { return SPX_ABI_VERSION; }
+extern "C" const char* spx_last_error(void) { return g_err.c_str(); }
+
+static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+static bool valid_dtype(int d) { return d >= SPX_BOOL && d <= SPX_F64; }
+
+// ----------------------------------------------------- dtype-generic access
+// Used by the non-hot-path kernels (merge / copy / finalize) where a uniform
+// per-element switch is cheaper than instantiating every dtype pair.
+__device__ __forceinline__ double ld_f(const void* p, int dt, i64 i) {
+  switch (dt) {
+    case SPX_BOOL: return (double)((const uint8_t*)p)[i];
+    case SPX_I32: return (double)((const int32_t*)p)[i];
+    case SPX_I64: return (double)((const int64_t*)p)[i];
+    case SPX_F32: return (double)((const float*)p)[i];
+    default: return ((const double*)p)[i];
+  }
+}
+__device__ __forceinline__ i64 ld_i(const void* p, int dt, i64 i) {
+  switch (dt) {
+    case SPX_BOOL: return (i64)((const uint8_t*)p)[i];
+    case SPX_I32: return (i64)((const int32_t*)p)[i];
+    case SPX_I64: return ((const int64_t*)p)[i];
+    case SPX_F32: return (i64)((const float*)p)[i];
+    default: return (i64)((const double*)p)[i];
+  }
+}
+__device__ __forceinline__ bool is_float_dt(int dt) { return dt == SPX_F32 || dt == SPX_F64; }
+
+__device__ __forceinline__ void st_f(void* p, int dt, i64 i, double v) {
+  switch (dt) {
+    case SPX_BOOL: ((uint8_t*)p)[i] = (v != 0.0); break;
+    case SPX_I32: ((int32_t*)p)[i] = (int32_t)(i64)v; break;
+    case SPX_I64: ((int64_t*)p)[i] = (i64)v; break;
+    case SPX_F32: ((float*)p)[i] = (float)v; break;
+    default: ((double*)p)[i] = v; break;
+  }
+}
+__device__ __forceinline__ void st_i(void* p, int dt, i64 i, i64 v) {
+  switch (dt) {
+    case SPX_BOOL: ((uint8_t*)p)[i] = (v != 0); break;
+    case SPX_I32: ((int32_t*)p)[i] = (int32_t)v; break;  // wraps like astype
+    case SPX_I64: ((int64_t*)p)[i] = v; break;
+    case SPX_F32: ((float*)p)[i] = (float)v; break;
+    default: ((double*)p)[i] = (double)v; break;
+  }
+}
+
+struct Geom {  // up to 8-d row-major geometry passed by value
+  int ndim;
+  i64 a[8];
+  i64 b[8];
+  i64 c[8];
+  i64 d[8];
+};
+
+static int grid_for(i64 n, int per_thread = 1) {
+  i64 g = (n + 256LL * per_thread - 1) / (256LL * per_thread);
+  if (g < 1) g = 1;
+  if (g > 65536) g = 65536;
+  return (int)g;
+}
+
+// =================================================================== fills
+__device__ __forceinline__ u64 mix64(u64 z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+// counter-based splitmix64 stream: value at global flat index g
+__device__ __forceinline__ u64 rng_at(u64 seed, u64 g) {
+  return mix64(seed * 0xD1B54A32D192ED03ULL + (g + 1ULL) * 0x9E3779B97F4A7C15ULL);
+}
+
+template <typename T>
+__device__ __forceinline__ T fill_value(int kind, int dt, double a, double b, u64 seed, i64 g);
+
+template <>
+__device__ __forceinline__ float fill_value<float>(int kind, int, double a, double b, u64 seed, i64 g) {
+  if (kind == SPX_FILL_CONST) return (float)a;
+  if (kind == SPX_FILL_ARANGE) return (float)(a + b * (double)g);
+  float u = (float)(rng_at(seed, (u64)g) >> 40) * 5.9604644775390625e-08f;  // 2^-24
+  float lo = (float)a, span = (float)(b - a);
+  float t = span * u;  // separate rounding steps (fp-contract off) -- oracle does the same
+  return lo + t;
+}
+template <>
+__device__ __forceinline__ double fill_value<double>(int kind, int, double a, double b, u64 seed, i64 g) {
+  if (kind == SPX_FILL_CONST) return a;
+  if (kind == SPX_FILL_ARANGE) return a + b * (double)g;
+  double u = (double)(rng_at(seed, (u64)g) >> 11) * 1.1102230246251565e-16;  // 2^-53
+  double t = (b - a) * u;
+  return a + t;
+}
+__device__ __forceinline__ i64 sat_i64(double a) {  // saturating double -> int64
+  if (a >= 9.2233720368547758e18) return 0x7fffffffffffffffLL;
+  if (a <= -9.2233720368547758e18) return (i64)(-0x7fffffffffffffffLL - 1);
+  return (i64)a;
+}
+template <typename T>
+__device__ __forceinline__ T fill_value_int(int kind, double a, double b, u64 seed, i64 g) {
+  if (kind == SPX_FILL_CONST) return (T)sat_i64(a);
+  if (kind == SPX_FILL_ARANGE) return (T)((i64)a + (i64)b * g);
+  double u = (double)(rng_at(seed, (u64)g) >> 11) * 1.1102230246251565e-16;
+  return (T)(i64)floor(a + (b - a) * u);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_fill(T* out, i64 n, Geom geo, int contiguous, i64 base,
+                                              int kind, int dt, double a, double b, u64 seed) {
+  i64 stride = (i64)gridDim.x * 256;
+  for (i64 e = (i64)blockIdx.x * 256 + threadIdx.x; e < n; e += stride) {
+    i64 g;
+    if (contiguous) {
+      g = base + e;
+    } else {  // unravel over tile shape (a), shift by ul (b), ravel over array shape (c)
+      i64 rem = e, mul = 1;
+      g = 0;
+      for (int d = geo.ndim - 1; d >= 0; --d) {
+        i64 li = rem % geo.a[d];
+        rem /= geo.a[d];
+        g += (li + geo.b[d]) * mul;
+        mul *= geo.c[d];
+      }
+    }
+    T v;
+    if constexpr (sizeof(T) == 4 && (T)0.5f != (T)0) v = fill_value<float>(kind, dt, a, b, seed, g);
+    else if constexpr (sizeof(T) == 8 && (T)0.5 != (T)0) v = fill_value<double>(kind, dt, a, b, seed, g);
+    else v = fill_value_int<T>(kind, a, b, seed, g);
+    out[e] = v;
+  }
+}
+
+extern "C" int spx_fill(int dtype, int kind, void* out, int ndim, const int64_t* tile_shape,
+                        const int64_t* ul, const int64_t* array_shape, double a, double b,
+                        uint64_t seed, void* stream) {
+  if (!valid_dtype(dtype)) return set_err(SPX_EINVAL, "spx_fill: bad dtype %d", dtype);
+  if (ndim < 0 || ndim > 8) return set_err(SPX_EINVAL, "spx_fill: ndim %d > 8", ndim);
+  if (kind < SPX_FILL_CONST || kind > SPX_FILL_UNIFORM)
+    return set_err(SPX_EINVAL, "spx_fill: bad kind %d", kind);
+  Geom geo{};
+  geo.ndim = ndim;
+  i64 n = 1;
+  for (int d = 0; d < ndim; ++d) {
+    geo.a[d] = tile_shape[d] > 0 ? tile_shape[d] : 1;
+    geo.b[d] = ul[d];
+    geo.c[d] = array_shape[d] > 0 ? array_shape[d] : 1;
+    n *= tile_shape[d];
+  }
+  if (n == 0) return SPX_OK;
+  if (!out) return set_err(SPX_EINVAL, "spx_fill: null output");
+  // contiguous in the global flat index iff all dims after the first equal the array's
+  int contiguous = 1;
+  for (int d = 1; d < ndim; ++d)
+    if (geo.a[d] != geo.c[d] || geo.b[d] != 0) contiguous = 0;
+  i64 base = 0, mul = 1;
+  for (int d = ndim - 1; d >= 0; --d) {
+    base += geo.b[d] * mul;
+    mul *= geo.c[d];
+  }
+  int g = grid_for(n, 4);
+  switch (dtype) {
+    case SPX_F32: k_fill<float><<<g, 256, 0, S(stream)>>>((float*)out, n, geo, contiguous, base, kind, dtype, a, b, seed); break;
+    case SPX_F64: k_fill<double><<<g, 256, 0, S(stream)>>>((double*)out, n, geo, contiguous, base, kind, dtype, a, b, seed); break;
+    case SPX_I32: k_fill<int32_t><<<g, 256, 0, S(stream)>>>((int32_t*)out, n, geo, contiguous, base, kind, dtype, a, b, seed); break;
+    case SPX_I64: k_fill<int64_t><<<g, 256, 0, S(stream)>>>((int64_t*)out, n, geo, contiguous, base, kind, dtype, a, b, seed); break;
+    default: k_fill<uint8_t><<<g, 256, 0, S(stream)>>>((uint8_t*)out, n, geo, contiguous, base, kind, dtype, a, b, seed); break;
+  }
+  LAUNCH_CHECK("spx_fill");
+  return SPX_OK;
+}
+
+// ======================================================== reduce finalize
+__device__ __forceinline__ bool dnan(double x) { return x != x; }
+
+__device__ __forceinline__ double comb_f(int op, double acc, double v) {
+  if (op == SPX_OP_SUM) return acc + v;
+  if (dnan(acc) || dnan(v)) return dnan(acc) ? acc : v;  // NaN propagates (np.minimum)
+  if (op == SPX_OP_MIN) return v < acc ? v : acc;
+  return v > acc ? v : acc;
+}
+__device__ __forceinline__ i64 comb_i(int op, i64 acc, i64 v) {
+  if (op == SPX_OP_SUM) return (i64)((u64)acc + (u64)v);
+  if (op == SPX_OP_MIN) return v < acc ? v : acc;
+  return v > acc ? v : acc;
+}
+// index value marking an empty (value, index) slot: never wins, always loses
+#define ARG_EMPTY 0x7fffffffffffffffLL
+// (value, index) "is candidate better than best" for ARGMIN/ARGMAX with
+// numpy's NaN rule (first NaN wins) and first-index tie break.
+__device__ __forceinline__ bool arg_better(int op, double v, i64 vi, double b, i64 bi) {
+  bool vn = dnan(v), bn = dnan(b);
+  if (vn || bn) {
+    if (vn && !bn) return true;
+    if (!vn && bn) return false;
+    return vi < bi;
+  }
+  if (v == b) return vi < bi;
+  return op == SPX_OP_ARGMIN ? (v < b) : (v > b);
+}
+
+__global__ __launch_bounds__(256) void k_finalize(int op, int acc_dt, int out_dt, const void* pv,
+                                                  const i64* pi, i64 P, i64 n, void* out,
+                                                  void* out_val) {
+  i64 stride = (i64)gridDim.x * 256;
+  for (i64 i = (i64)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    if (op == SPX_OP_ARGMIN || op == SPX_OP_ARGMAX) {
+      double b = ld_f(pv, acc_dt, i);
+      i64 bi = pi[i];
+      for (i64 p = 1; p < P; ++p) {
+        double v = ld_f(pv, acc_dt, p * n + i);
+        i64 vi = pi[p * n + i];
+        if (vi != ARG_EMPTY && (bi == ARG_EMPTY || arg_better(op, v, vi, b, bi))) { b = v; bi = vi; }
+      }
+      ((i64*)out)[i] = bi;
+      if (out_val) st_f(out_val, acc_dt, i, b);
+    } else if (is_float_dt(acc_dt)) {
+      double acc = ld_f(pv, acc_dt, i);
+      if (acc_dt == SPX_F32) {  // keep fp32 rounding of each step for fp32 accumulators
+        float facc = (float)acc;
+        for (i64 p = 1; p < P; ++p) {
+          float v = ((const float*)pv)[p * n + i];
+          facc = (op == SPX_OP_SUM) ? facc + v : (float)comb_f(op, (double)facc, (double)v);
+        }
+        acc = facc;
+      } else {
+        for (i64 p = 1; p < P; ++p) acc = comb_f(op, acc, ld_f(pv, acc_dt, p * n + i));
+      }
+      if (is_float_dt(out_dt)) st_f(out, out_dt, i, acc);
+      else st_i(out, out_dt, i, (i64)acc);
+    } else {
+      i64 acc = ld_i(pv, acc_dt, i);
+      for (i64 p = 1; p < P; ++p) acc = comb_i(op, acc, ld_i(pv, acc_dt, p * n + i));
+      st_i(out, out_dt, i, acc);
+    }
+  }
+}
+
+extern "C" int spx_reduce_finalize(int op, int acc_dtype, int out_dtype, const void* part_val,
+                                   const int64_t* part_idx, int64_t P, int64_t n, void* out,
+                                   void* out_val, void* stream) {
+  if (!valid_dtype(acc_dtype) || !valid_dtype(out_dtype))
+    return set_err(SPX_EINVAL, "spx_reduce_finalize: bad dtype");
+  if (op < SPX_OP_SUM || op > SPX_OP_ARGMAX) return set_err(SPX_EINVAL, "spx_reduce_finalize: bad op %d", op);
+  if (P < 1 || n < 0) return set_err(SPX_EINVAL, "spx_reduce_finalize: bad P/n");
+  if (n == 0) return SPX_OK;
+  if ((op == SPX_OP_ARGMIN || op == SPX_OP_ARGMAX) && !part_idx)
+    return set_err(SPX_EINVAL, "spx_reduce_finalize: arg op needs part_idx");
+  k_finalize<<<grid_for(n), 256, 0, S(stream)>>>(op, acc_dtype, out_dtype, part_val, part_idx, P, n,
+                                                 out, out_val);
+  LAUNCH_CHECK("spx_reduce_finalize");
+  return SPX_OK;
+}
+
+// =================================================================== merge
+__global__ __launch_bounds__(256) void k_merge(int op, int dt, void* dst, uint8_t* mask, Geom g,
+                                               i64 n, const void* src, int sdt, int fast,
+                                               int fast_reduce) {
+  // g.a = dst_shape, g.b = region_ul, g.c = region_shape
+  i64 stride = (i64)gridDim.x * 256;
+  for (i64 e = (i64)blockIdx.x * 256 + threadIdx.x; e < n; e += stride) {
+    i64 di;
+    if (fast) {
+      di = e;
+    } else {
+      i64 rem = e, mul = 1;
+      di = 0;
+      for (int d = g.ndim - 1; d >= 0; --d) {
+        i64 li = rem % g.c[d];
+        rem /= g.c[d];
+        di += (li + g.b[d]) * mul;
+        mul *= g.a[d];
+      }
+    }
+    bool reduce;
+    if (op == SPX_OP_REPLACE) reduce = false;
+    else if (fast) reduce = fast_reduce;
+    else reduce = mask ? (mask[di] != 0) : true;
+    if (is_float_dt(dt)) {
+      double v = ld_f(src, sdt, e);
+      if (reduce) v = comb_f(op, ld_f(dst, dt, di), v);
+      st_f(dst, dt, di, v);
+    } else {
+      i64 v = is_float_dt(sdt) ? (i64)ld_f(src, sdt, e) : ld_i(src, sdt, e);
+      if (reduce) v = comb_i(op, ld_i(dst, dt, di), v);
+      st_i(dst, dt, di, v);
+    }
+    if (mask) mask[di] = 1;
+  }
+}
+
+extern "C" int spx_merge(int op, int dtype, void* dst, uint8_t* mask, int ndim,
+                         const int64_t* dst_shape, const int64_t* region_ul,
+                         const int64_t* region_shape, const void* src, int src_dtype,
+                         int full_tile_fastpath, void* stream) {
+  if (!valid_dtype(dtype) || !valid_dtype(src_dtype)) return set_err(SPX_EINVAL, "spx_merge: bad dtype");
+  if (!(op == SPX_OP_SUM || op == SPX_OP_MIN || op == SPX_OP_MAX || op == SPX_OP_REPLACE))
+    return set_err(SPX_EINVAL, "spx_merge: bad op %d", op);
+  if (ndim < 0 || ndim > 8) return set_err(SPX_EINVAL, "spx_merge: ndim > 8");
+  Geom g{};
+  g.ndim = ndim;
+  i64 n = 1;
+  bool full = true;
+  for (int d = 0; d < ndim; ++d) {
+    g.a[d] = dst_shape[d];
+    g.b[d] = region_ul[d];
+    g.c[d] = region_shape[d];
+    if (region_ul[d] < 0 || region_ul[d] + region_shape[d] > dst_shape[d])
+      return set_err(SPX_EINVAL, "spx_merge: region out of bounds on dim %d", d);
+    if (region_ul[d] != 0 || region_shape[d] != dst_shape[d]) full = false;
+    n *= region_shape[d];
+  }
+  if (n == 0) return SPX_OK;
+  if (!dst || !src) return set_err(SPX_EINVAL, "spx_merge: null pointer");
+  int fast = (full && full_tile_fastpath) ? 1 : 0;
+  int fast_reduce = 0;
+  if (fast && op != SPX_OP_REPLACE) {
+    if (mask) {
+      uint8_t m0 = 0;
+      HIP_TRY(hipMemcpyAsync(&m0, mask, 1, hipMemcpyDeviceToHost, S(stream)));
+      HIP_TRY(hipStreamSynchronize(S(stream)));
+      fast_reduce = m0 != 0;
+    } else {
+      fast_reduce = 1;
+    }
+  }
+  k_merge<<<grid_for(n), 256, 0, S(stream)>>>(op, dtype, dst, mask, g, n, src, src_dtype, fast, fast_reduce);
+  LAUNCH_CHECK("spx_merge");
+  return SPX_OK;
+}
+
+// ============================================================= copy region
+struct Geom2 {
+  int ndim;
+  i64 dshape[8], dul[8], sshape[8], sul[8], cshape[8];
+};
+
+__global__ __launch_bounds__(256) void k_copy2(int ddt, void* dst, int sdt, const void* src,
+                                               Geom2 g, i64 n) {
+  i64 stride = (i64)gridDim.x * 256;
+  for (i64 e = (i64)blockIdx.x * 256 + threadIdx.x; e < n; e += stride) {
+    i64 rem = e, dm = 1, sm = 1, di = 0, si = 0;
+    for (int d = g.ndim - 1; d >= 0; --d) {
+      i64 li = rem % g.cshape[d];
+      rem /= g.cshape[d];
+      di += (li + g.dul[d]) * dm;
+      si += (li + g.sul[d]) * sm;
+      dm *= g.dshape[d];
+      sm *= g.sshape[d];
+    }
+    if (ddt == sdt) {
+      switch (ddt) {
+        case SPX_BOOL: ((uint8_t*)dst)[di] = ((const uint8_t*)src)[si]; break;
+        case SPX_I32: ((int32_t*)dst)[di] = ((const int32_t*)src)[si]; break;
+        case SPX_F32: ((float*)dst)[di] = ((const float*)src)[si]; break;
+        case SPX_I64: ((int64_t*)dst)[di] = ((const int64_t*)src)[si]; break;
+        default: ((double*)dst)[di] = ((const double*)src)[si]; break;
+      }
+    } else if (is_float_dt(sdt)) {
+      if (is_float_dt(ddt)) st_f(dst, ddt, di, ld_f(src, sdt, si));
+      else st_i(dst, ddt, di, (i64)ld_f(src, sdt, si));
+    } else {
+      st_i(dst, ddt, di, ld_i(src, sdt, si));
+    }
+  }
+}
+
+extern "C" int spx_copy_region(int dst_dtype, void* dst, const int64_t* dst_shape,
+                               const int64_t* dst_ul, int src_dtype, const void* src,
+                               const int64_t* src_shape, const int64_t* src_ul, int ndim,
+                               const int64_t* copy_shape, void* stream) {
+  if (!valid_dtype(dst_dtype) || !valid_dtype(src_dtype)) return set_err(SPX_EINVAL, "spx_copy_region: bad dtype");
+  if (ndim < 0 || ndim > 8) return set_err(SPX_EINVAL, "spx_copy_region: ndim > 8");
+  Geom2 g{};
+  g.ndim = ndim;
+  i64 n = 1;
+  for (int d = 0; d < ndim; ++d) {
+    g.dshape[d] = dst_shape[d];
+    g.dul[d] = dst_ul[d];
+    g.sshape[d] = src_shape[d];
+    g.sul[d] = src_ul[d];
+    g.cshape[d] = copy_shape[d];
+    if (dst_ul[d] < 0 || dst_ul[d] + copy_shape[d] > dst_shape[d] || src_ul[d] < 0 ||
+        src_ul[d] + copy_shape[d] > src_shape[d])
+      return set_err(SPX_EINVAL, "spx_copy_region: region out of bounds on dim %d", d);
+    n *= copy_shape[d];
+  }
+  if (n == 0) return SPX_OK;
+  if (!dst || !src) return set_err(SPX_EINVAL, "spx_copy_region: null pointer");
+  k_copy2<<<grid_for(n), 256, 0, S(stream)>>>(dst_dtype, dst, src_dtype, src, g, n);
+  LAUNCH_CHECK("spx_copy_region");
+  return SPX_OK;
+}
+
+// ================================================== arg-reduction combine
+__global__ __launch_bounds__(256) void k_argcombine(int op, int dt, const void* vals, const i64* idx,
+                                                    i64 R, i64 n, void* out_val, i64* out_idx) {
+  i64 stride = (i64)gridDim.x * 256;
+  for (i64 i = (i64)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    double b = ld_f(vals, dt, i);
+    i64 bi = idx[i];
+    for (i64 r = 1; r < R; ++r) {
+      double v = ld_f(vals, dt, r * n + i);
+      i64 vi = idx[r * n + i];
+      if (vi != ARG_EMPTY && (bi == ARG_EMPTY || arg_better(op, v, vi, b, bi))) { b = v; bi = vi; }
+    }
+    out_idx[i] = bi;
+    if (out_val) st_f(out_val, dt, i, b);
+  }
+}
+
+extern "C" int spx_argreduce_combine(int op, int dtype, const void* vals, const int64_t* idx,
+                                     int64_t R, int64_t n, void* out_val, int64_t* out_idx,
+                                     void* stream) {
+  if (op != SPX_OP_ARGMIN && op != SPX_OP_ARGMAX) return set_err(SPX_EINVAL, "spx_argreduce_combine: bad op");
+  if (!valid_dtype(dtype)) return set_err(SPX_EINVAL, "spx_argreduce_combine: bad dtype");
+  if (R < 1 || n < 0) return set_err(SPX_EINVAL, "spx_argreduce_combine: bad R/n");
+  if (n == 0) return SPX_OK;
+  if (!vals || !idx || !out_idx) return set_err(SPX_EINVAL, "spx_argreduce_combine: null pointer");
+  k_argcombine<<<grid_for(n), 256, 0, S(stream)>>>(op, dtype, vals, idx, R, n, out_val, out_idx);
+  LAUNCH_CHECK("spx_argreduce_combine");
+  return SPX_OK;
+}
+
+// ==================================================================== GEMM
+// fp32: block tile 128x128, BK=16, 256 threads = 4 waves in 2x2, each wave
+// owns a 64x64 sub-tile = 2x2 v_mfma_f32_32x32x2_f32 accumulators.
+// A is staged transposed in LDS (As[k][m]) so that each MFMA operand read is
+// 32 consecutive dwords per half-wave (conflict-free ds_read_b32); B is
+// staged row-major (Bs[k][n]).  Register prefetch of the next K-tile overlaps
+// the global loads with the MFMAs of the current one (2 LDS buffers).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+#define G32_BM 128
+#define G32_BN 128
+#define G32_BK 16
+#define G32_PADA 4
+
+template <bool ALIGNED>
+__device__ __forceinline__ void g32_load_tiles(const float* __restrict__ A, i64 lda,
+                                               const float* __restrict__ B, i64 ldb, i64 M,
+                                               i64 N, i64 K, i64 row0, i64 col0, i64 k0, int t,
+                                               f32x4 ra[2], f32x4 rb[2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    int idx = t + i * 256;
+    int r = idx >> 2, kq = idx & 3;  // A: 128 rows x 4 float4
+    i64 gr = row0 + r, gk = k0 + kq * 4;
+    if (ALIGNED) {
+      ra[i] = *(const f32x4*)(A + gr * lda + gk);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        ra[i][j] = (gr < M && gk + j < K) ? A[gr * lda + gk + j] : 0.0f;
+    }
+    int kr = idx >> 5, cq = idx & 31;  // B: 16 rows x 32 float4
+    i64 bk = k0 + kr, bc = col0 + cq * 4;
+    if (ALIGNED) {
+      rb[i] = *(const f32x4*)(B + bk * ldb + bc);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        rb[i][j] = (bk < K && bc + j < N) ? B[bk * ldb + bc + j] : 0.0f;
+    }
+  }
+}
+
+__device__ __forceinline__ void g32_store_lds(float (*As)[G32_BM + G32_PADA], float (*Bs)[G32_BN], int t,
+                                              const f32x4 ra[2], const f32x4 rb[2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    int idx = t + i * 256;
+    int r = idx >> 2, kq = idx & 3;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) As[kq * 4 + j][r] = ra[i][j];
+    int kr = idx >> 5, cq = idx & 31;
+    *(f32x4*)(&Bs[kr][cq * 4]) = rb[i];
+  }
+}
+
+template <bool ALIGNED>
+__global__ __launch_bounds__(256) void k_gemm_f32(i64 M, i64 N, i64 K, const float* __restrict__ A,
+                                                  i64 lda, const float* __restrict__ B, i64 ldb,
+                                                  float* __restrict__ C, i64 ldc, float alpha,
+                                                  float beta, int tiles_n, int ntiles) {
+  __shared__ float As[2][G32_BK][G32_BM + G32_PADA];
+  __shared__ __attribute__((aligned(16))) float Bs[2][G32_BK][G32_BN];
+  // XCD-aware remap: consecutive tiles (sharing A row panels) land on one XCD.
+  int bid = blockIdx.x;
+  {
+    int q = ntiles / 8, rr = ntiles % 8, xcd = bid % 8;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+  }
+  int tm = bid / tiles_n, tn = bid % tiles_n;
+  i64 row0 = (i64)tm * G32_BM, col0 = (i64)tn * G32_BN;
+  int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int wm = w >> 1, wn = w & 1;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
+  f32x4 ra[2], rb[2];
+  int nk = (int)((K + G32_BK - 1) / G32_BK);
+  g32_load_tiles<ALIGNED>(A, lda, B, ldb, M, N, K, row0, col0, 0, t, ra, rb);
+  g32_store_lds(As[0], Bs[0], t, ra, rb);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    int cur = kt & 1;
+    if (kt + 1 < nk)
+      g32_load_tiles<ALIGNED>(A, lda, B, ldb, M, N, K, row0, col0, (i64)(kt + 1) * G32_BK, t, ra, rb);
+#pragma unroll
+    for (int kk = 0; kk < G32_BK / 2; ++kk) {
+      int k = kk * 2 + (lane >> 5);
+      float a0 = As[cur][k][wm * 64 + (lane & 31)];
+      float a1 = As[cur][k][wm * 64 + 32 + (lane & 31)];
+      float b0 = Bs[cur][k][wn * 64 + (lane & 31)];
+      float b1 = Bs[cur][k][wn * 64 + 32 + (lane & 31)];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      g32_store_lds(As[cur ^ 1], Bs[cur ^ 1], t, ra, rb);
+    }
+    __syncthreads();
+  }
+  // epilogue: 32x32 C/D map row = (r&3) + 8*(r>>2) + 4*(lane>>5), col = lane&31
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        i64 gr = row0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        i64 gc = col0 + wn * 64 + j * 32 + (lane & 31);
+        if (gr < M && gc < N) {
+          float v = alpha * acc[i][j][r];
+          if (beta != 0.0f) v += beta * C[gr * ldc + gc];
+          C[gr * ldc + gc] = v;
+        }
+      }
+}
+
+// fp64: block 128x128, BK=8, 4 waves 2x2, wave 64x64 = 4x4 v_mfma_f64_16x16x4_f64
+// accumulators (C/D map: col = lane&15, row = (lane>>4) + 4*reg).
+#define G64_BM 128
+#define G64_BN 128
+#define G64_BK 8
+#define G64_PADA 2
+
+template <bool ALIGNED>
+__global__ __launch_bounds__(256) void k_gemm_f64(i64 M, i64 N, i64 K, const double* __restrict__ A,
+                                                  i64 lda, const double* __restrict__ B, i64 ldb,
+                                                  double* __restrict__ C, i64 ldc, double alpha,
+                                                  double beta, int tiles_n, int ntiles) {
+  __shared__ double As[2][G64_BK][G64_BM + G64_PADA];
+  __shared__ __attribute__((aligned(16))) double Bs[2][G64_BK][G64_BN];
+  int bid = blockIdx.x;
+  {
+    int q = ntiles / 8, rr = ntiles % 8, xcd = bid % 8;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+  }
+  int tm = bid / tiles_n, tn = bid % tiles_n;
+  i64 row0 = (i64)tm * G64_BM, col0 = (i64)tn * G64_BN;
+  int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int wm = w >> 1, wn = w & 1;
+  f64x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f64x4){0, 0, 0, 0};
+  // per K-tile: A 128x8 doubles = 512 double2 (2 per thread); B 8x128 = 512 double2
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  d2 ra[2], rb[2];
+  int nk = (int)((K + G64_BK - 1) / G64_BK);
+  auto load = [&](i64 k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int idx = t + i * 256;
+      int r = idx >> 2, kq = idx & 3;  // 4 double2 per 8-wide row
+      i64 gr = row0 + r, gk = k0 + kq * 2;
+      if (ALIGNED) ra[i] = *(const d2*)(A + gr * lda + gk);
+      else {
+        ra[i][0] = (gr < M && gk < K) ? A[gr * lda + gk] : 0.0;
+        ra[i][1] = (gr < M && gk + 1 < K) ? A[gr * lda + gk + 1] : 0.0;
+      }
+      int kr = idx >> 6, cq = idx & 63;  // 64 double2 per 128-wide row
+      i64 bk = k0 + kr, bc = col0 + cq * 2;
+      if (ALIGNED) rb[i] = *(const d2*)(B + bk * ldb + bc);
+      else {
+        rb[i][0] = (bk < K && bc < N) ? B[bk * ldb + bc] : 0.0;
+        rb[i][1] = (bk < K && bc + 1 < N) ? B[bk * ldb + bc + 1] : 0.0;
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int idx = t + i * 256;
+      int r = idx >> 2, kq = idx & 3;
+      As[buf][kq * 2][r] = ra[i][0];
+      As[buf][kq * 2 + 1][r] = ra[i][1];
+      int kr = idx >> 6, cq = idx & 63;
+      *(d2*)(&Bs[buf][kr][cq * 2]) = rb[i];
+    }
+  };
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    int cur = kt & 1;
+    if (kt + 1 < nk) load((i64)(kt + 1) * G64_BK);
+#pragma unroll
+    for (int kk = 0; kk < G64_BK / 4; ++kk) {
+      int k = kk * 4 + (lane >> 4);
+      double a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = As[cur][k][wm * 64 + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = Bs[cur][k][wn * 64 + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store(cur ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        i64 gr = row0 + wm * 64 + i * 16 + (lane >> 4) + 4 * r;
+        i64 gc = col0 + wn * 64 + j * 16 + (lane & 15);
+        if (gr < M && gc < N) {
+          double v = alpha * acc[i][j][r];
+          if (beta != 0.0) v += beta * C[gr * ldc + gc];
+          C[gr * ldc + gc] = v;
+        }
+      }
+}
+
+// integer GEMM (exact, wrap-around like NumPy's int matmul): 16x16 output
+// tile per 256-thread block, K staged through LDS.  Used for integer dot
+// products (the reference's tests multiply arange ints); not a hot path.
+template <typename T>
+__global__ __launch_bounds__(256) void k_gemm_int(i64 M, i64 N, i64 K, const T* __restrict__ A, i64 lda,
+                                                  const T* __restrict__ B, i64 ldb, T* __restrict__ C,
+                                                  i64 ldc, T alpha, T beta) {
+  __shared__ T As[16][17];
+  __shared__ T Bs[16][17];
+  int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  i64 row = (i64)blockIdx.y * 16 + ty, col = (i64)blockIdx.x * 16 + tx;
+  typedef typename std::conditional<sizeof(T) == 8, u64, uint32_t>::type U;
+  U acc = 0;
+  for (i64 k0 = 0; k0 < K; k0 += 16) {
+    As[ty][tx] = (row < M && k0 + tx < K) ? A[row * lda + k0 + tx] : (T)0;
+    Bs[ty][tx] = (k0 + ty < K && col < N) ? B[(k0 + ty) * ldb + col] : (T)0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc += (U)As[ty][k] * (U)Bs[k][tx];
+    __syncthreads();
+  }
+  if (row < M && col < N) {
+    U v = (U)alpha * acc;
+    if (beta != 0) v += (U)beta * (U)C[row * ldc + col];
+    C[row * ldc + col] = (T)v;
+  }
+}
+
+extern "C" int spx_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                        const void* B, int64_t ldb, void* C, int64_t ldc, double alpha,
+                        double beta, void* stream) {
+  if (dtype != SPX_F32 && dtype != SPX_F64 && dtype != SPX_I32 && dtype != SPX_I64)
+    return set_err(SPX_ENOTSUP, "spx_gemm: dtype %d not supported (F32/F64/I32/I64)", dtype);
+  if (M < 0 || N < 0 || K < 0) return set_err(SPX_EINVAL, "spx_gemm: negative dimension");
+  if (lda < K || ldb < N || ldc < N) return set_err(SPX_EINVAL, "spx_gemm: leading dimension too small");
+  if (M == 0 || N == 0) return SPX_OK;
+  if (!A || !B || !C) return set_err(SPX_EINVAL, "spx_gemm: null pointer");
+  if (K == 0) {  // C = beta * C
+    return set_err(SPX_ENOTSUP, "spx_gemm: K == 0 not supported");
+  }
+  if (dtype == SPX_I32 || dtype == SPX_I64) {
+    dim3 grid((unsigned)((N + 15) / 16), (unsigned)((M + 15) / 16));
+    if (dtype == SPX_I64)
+      k_gemm_int<int64_t><<<grid, 256, 0, S(stream)>>>(M, N, K, (const int64_t*)A, lda, (const int64_t*)B, ldb,
+                                                       (int64_t*)C, ldc, (int64_t)alpha, (int64_t)beta);
+    else
+      k_gemm_int<int32_t><<<grid, 256, 0, S(stream)>>>(M, N, K, (const int32_t*)A, lda, (const int32_t*)B, ldb,
+                                                       (int32_t*)C, ldc, (int32_t)alpha, (int32_t)beta);
+    LAUNCH_CHECK("spx_gemm(int)");
+    return SPX_OK;
+  }
+  if (dtype == SPX_F32) {
+    i64 tm = (M + G32_BM - 1) / G32_BM, tn = (N + G32_BN - 1) / G32_BN;
+    if (tm * tn > 0x7fffffffLL) return set_err(SPX_EINVAL, "spx_gemm: too many tiles");
+    bool aligned = (M % G32_BM == 0) && (N % G32_BN == 0) && (K % G32_BK == 0) && (lda % 4 == 0) &&
+                   (ldb % 4 == 0) && ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0);
+    int nt = (int)(tm * tn);
+    if (aligned)
+      k_gemm_f32<true><<<nt, 256, 0, S(stream)>>>(M, N, K, (const float*)A, lda, (const float*)B, ldb,
+                                                  (float*)C, ldc, (float)alpha, (float)beta, (int)tn, nt);
+    else
+      k_gemm_f32<false><<<nt, 256, 0, S(stream)>>>(M, N, K, (const float*)A, lda, (const float*)B, ldb,
+                                                   (float*)C, ldc, (float)alpha, (float)beta, (int)tn, nt);
+    LAUNCH_CHECK("spx_gemm(f32)");
+  } else {
+    i64 tm = (M + G64_BM - 1) / G64_BM, tn = (N + G64_BN - 1) / G64_BN;
+    if (tm * tn > 0x7fffffffLL) return set_err(SPX_EINVAL, "spx_gemm: too many tiles");
+    bool aligned = (M % G64_BM == 0) && (N % G64_BN == 0) && (K % G64_BK == 0) && (lda % 2 == 0) &&
+                   (ldb % 2 == 0) && ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0);
+    int nt = (int)(tm * tn);
+    if (aligned)
+      k_gemm_f64<true><<<nt, 256, 0, S(stream)>>>(M, N, K, (const double*)A, lda, (const double*)B, ldb,
+                                                  (double*)C, ldc, alpha, beta, (int)tn, nt);
+    else
+      k_gemm_f64<false><<<nt, 256, 0, S(stream)>>>(M, N, K, (const double*)A, lda, (const double*)B, ldb,
+                                                   (double*)C, ldc, alpha, beta, (int)tn, nt);
+    LAUNCH_CHECK("spx_gemm(f64)");
+  }
+  return SPX_OK;
+}
+
+// ============================================================ JIT modules
+extern "C" int spx_module_load(const void* image, size_t nbytes, void** module_out) {
+  if (!image || nbytes == 0 || !module_out) return set_err(SPX_EINVAL, "spx_module_load: bad args");
+  hipModule_t m = nullptr;
+  HIP_TRY(hipModuleLoadData(&m, image));
+  *module_out = (void*)m;
+  return SPX_OK;
+}
+
+extern "C" int spx_module_unload(void* module) {
+  if (!module) return SPX_OK;
+  HIP_TRY(hipModuleUnload((hipModule_t)module));
+  return SPX_OK;
+}
+
+extern "C" int spx_module_function(void* module, const char* name, void** fn_out) {
+  if (!module || !name || !fn_out) return set_err(SPX_EINVAL, "spx_module_function: bad args");
+  hipFunction_t f = nullptr;
+  hipError_t e = hipModuleGetFunction(&f, (hipModule_t)module, name);
+  if (e != hipSuccess)
+    return set_err(SPX_EHIP, "hipModuleGetFunction(%s): %s", name, hipGetErrorString(e));
+  *fn_out = (void*)f;
+  return SPX_OK;
+}
+
+extern "C" int spx_launch(void* fn, uint32_t gx, uint32_t gy, uint32_t gz, uint32_t block_x,
+                          uint32_t shared_bytes, const void* args, size_t args_bytes, void* stream) {
+  if (!fn) return set_err(SPX_EINVAL, "spx_launch: null function");
+  if (gx == 0 || gy == 0 || gz == 0) return SPX_OK;
+  if (block_x == 0 || block_x > 1024) return set_err(SPX_EINVAL, "spx_launch: bad block %u", block_x);
+  size_t sz = args_bytes;
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, const_cast<void*>(args), HIP_LAUNCH_PARAM_BUFFER_SIZE,
+                 &sz, HIP_LAUNCH_PARAM_END};
+  HIP_TRY(hipModuleLaunchKernel((hipFunction_t)fn, gx, gy, gz, block_x, 1, 1, shared_bytes, S(stream),
+                                nullptr, cfg));
+  return SPX_OK;
+}

@@ -1,0 +1,18 @@
+"""spartan_amd.expr -- the spartan.expr API (spartan/expr/__init__.py:26-53)
+on the MI355X tile-execution backend."""
+from .base import (Expr, NotShapeable, as_array, eager, evaluate, force, glom, lazify,
+                   optimized_dag)
+from .builtins import (abs, add, arange, argmax, argmin, astype, count_nonzero, count_zero, exp,
+                       ln, log, maximum, max, mean, min, minimum, multiply, ones, power, rand,
+                       size, sqrt, square, sub, sum, zeros)
+from .dot import dot
+from .map import map
+from .ndarray import ndarray
+from .reduce import reduce
+from .write_array import from_numpy
+
+Expr.sum = sum
+Expr.mean = mean
+Expr.astype = astype
+Expr.argmin = argmin
+Expr.argmax = argmax

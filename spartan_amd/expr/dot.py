@@ -1,0 +1,231 @@
+"""``dot`` on MFMA (restates the decomposition of spartan/expr/dot.py:238-283).
+
+The reference builds a ``map2`` K-split join (square / wide A): every worker
+computes a full-size partial ``A[:, K_i] @ B[K_i, :]`` with BLAS
+(dot_map2_mapper, dot.py:195-212) and ships it to one owner tile where the
+partials are summed with ``np.add`` (map.py:326-328, tile.pyx:264-284).  Here
+that contraction is one ``DotExpr`` node:
+
+  * the rank owning B's K-block j gets A[:, K_j] (``gather_regions``: the
+    reference's A column-strip fetch, distarray.py:315-365, done as one P2P
+    exchange), and accumulates C_partial += A[:, K_j] @ B_j with spx_gemm
+    (v_mfma_f32_32x32x2_f32 / v_mfma_f64_16x16x4_f64);
+  * partials are summed across ranks by RCCL (reduce_scatter onto row-strip
+    output tiles, all_reduce otherwise) instead of a serial merge at one owner.
+
+Host NumPy operands (``dot(X, w)`` with ``w`` an ndarray, dot_map2_np_mapper
+dot.py:172-187) are replicated to every GPU; each rank multiplies its own A
+row strips, so the partials land on local output tiles with no exchange.
+Output tiling: ``tile_hint`` if given, else the default row strips (the
+reference forces a single (M, N) tile on worker 0; values are identical).
+"""
+import numpy as np
+
+from .. import backend, comm, runtime
+from ..array import distarray, extent as ext
+from ..array.distarray import LocalWrapper
+from .base import Expr, as_array
+
+
+def _shape(a, b):
+  if len(a.shape) == 1 and len(b.shape) == 1:
+    if a.shape[0] != b.shape[0]:
+      raise ValueError('objects are not aligned')
+    return (1,)
+  if len(a.shape) > 1 and len(b.shape) == 1:
+    if a.shape[1] != b.shape[0]:
+      raise ValueError('objects are not aligned')
+    return (a.shape[0],)
+  if len(a.shape) > 1 and len(b.shape) > 1:
+    if a.shape[1] != b.shape[0]:
+      raise ValueError('objects are not aligned')
+    return (a.shape[0], b.shape[1])
+  raise ValueError('objects are not aligned')
+
+
+class DotExpr(Expr):
+  _members = ('matrix_a', 'matrix_b')
+
+  def compute_shape(self):
+    return _shape(self.matrix_a, self.matrix_b)
+
+  def compute_dtype(self):
+    return np.result_type(self.matrix_a.dtype, self.matrix_b.dtype)
+
+  def pretty_str(self):
+    return 'Dot[%d](%s, %s)' % (self.expr_id, self.matrix_a, self.matrix_b)
+
+  def _evaluate(self, deps):
+    a, b = deps['matrix_a'], deps['matrix_b']
+    if isinstance(a, np.ndarray):
+      a = LocalWrapper(a)
+    if isinstance(b, np.ndarray):
+      b = LocalWrapper(b)
+    return run_dot(a, b, getattr(self, 'tile_hint', None))
+
+
+def dot(a, b, tile_hint=None):
+  """Matrix / vector product of two arrays (dot.py:238-283)."""
+  if not isinstance(b, Expr) and not isinstance(b, np.ndarray):
+    b = np.asarray(b)
+  e = DotExpr(matrix_a=as_array(a), matrix_b=as_array(b) if not isinstance(b, np.ndarray) else b)
+  e.tile_hint = tile_hint
+  e.compute_shape()  # raises ValueError early on misalignment, as the reference
+  return e
+
+
+# ---------------------------------------------------------------- engine
+class _As2D:
+  """2-d view of a 1-d array: 'row' (1, K) for the left operand, 'col' (K, 1) for the right."""
+
+  def __init__(self, arr, kind):
+    self.arr, self.kind = arr, kind
+    if len(arr.shape) == 2:
+      self.shape = tuple(arr.shape)
+    elif kind == 'row':
+      self.shape = (1, arr.shape[0])
+    else:
+      self.shape = (arr.shape[0], 1)
+
+  def to_base(self, region2):
+    if len(self.arr.shape) == 2:
+      return region2
+    d = 1 if self.kind == 'row' else 0
+    return ext.create((region2.ul[d],), (region2.lr[d],), self.arr.shape)
+
+  def tiles2(self):
+    """{2-d extent: worker} of the underlying array."""
+    out = {}
+    for ex, w in self.arr.tiles.items():
+      if len(self.arr.shape) == 2:
+        out[ex] = w
+      elif self.kind == 'row':
+        out[ext.create((0, ex.ul[0]), (1, ex.lr[0]), self.shape)] = w
+      else:
+        out[ext.create((ex.ul[0], 0), (ex.lr[0], 1), self.shape)] = w
+    return out
+
+
+def _as_dtype(t, dt):
+  import torch
+  tdt = backend.torch_dtype(dt)
+  if t.dtype == tdt:
+    return t.contiguous()
+  out = torch.empty(tuple(t.shape), dtype=tdt, device=t.device)
+  backend.get().copy_region(out, (0,) * t.dim(), t.contiguous(), (0,) * t.dim(), tuple(t.shape))
+  return out
+
+
+def run_dot(a, b, tile_hint=None):
+  import torch
+  ctx = runtime.get()
+  be = backend.get()
+  out_shape = _shape(a, b)
+  dtype = np.result_type(a.dtype, b.dtype)
+  A, B = _As2D(a, 'row'), _As2D(b, 'col')
+  M, K = A.shape
+  N = B.shape[1]
+  C = None
+  if b.replicated and not a.replicated:
+    # X @ w with w on every GPU: local row strips of X -> local output rows
+    Bd = _as_dtype(b.fetch(ext.from_shape(b.shape)).reshape(K, N), dtype)
+    partials = {}
+    for ex2, w in A.tiles2().items():
+      if not ctx.is_local(w):
+        continue
+      at = _as_dtype(a.fetch(A.to_base(ex2)).reshape(ex2.shape), dtype)
+      bk = Bd[ex2.ul[1]:ex2.lr[1]]
+      ct = torch.empty((ex2.shape[0], N), dtype=backend.torch_dtype(dtype), device=ctx.device)
+      be.gemm(at, bk.contiguous(), ct, 1.0, 0.0)
+      partials[ex2] = ct
+    return _combine_rows(partials, A, M, N, out_shape, dtype, tile_hint, k_split=any(
+        ex.ul[1] != 0 or ex.lr[1] != K for ex in A.tiles2()))
+  btiles = B.tiles2() if not b.replicated else {ext.from_shape((K, N)): -1}
+  # a lone rank whose B blocks tile every output column needs no zero fill:
+  # the first GEMM into each column block runs with beta = 0
+  col_blocks = sorted({(bex.ul[1], bex.lr[1]) for bex in btiles})
+  lone = not ctx.distributed
+  if lone:
+    C = torch.empty((M, N), dtype=backend.torch_dtype(dtype), device=ctx.device)
+  else:
+    C = torch.zeros((M, N), dtype=backend.torch_dtype(dtype), device=ctx.device)
+  started = set()
+  requests, plan = [], []
+  for bex, w in btiles.items():
+    dst = ctx.owner(w) if w != -1 else None
+    a_region = ext.create((0, bex.ul[0]), (M, bex.lr[0]), (M, K))
+    if dst is None:  # replicated B and A: rank 0 computes
+      dst = 0
+    requests.append((A.to_base(a_region), dst))
+    plan.append((bex, dst))
+  got = distarray.gather_regions(a, requests)
+  for qi, (bex, dst) in enumerate(plan):
+    if dst != ctx.rank:
+      continue
+    at = _as_dtype(got[qi].reshape(M, bex.shape[0]), dtype)
+    if b.replicated:
+      bt = b.fetch(ext.from_shape(b.shape)).reshape(K, N)
+    else:
+      bt = b.fetch(B.to_base(bex)).reshape(bex.shape)
+    bt = _as_dtype(bt, dtype)
+    cview = C[:, bex.ul[1]:bex.lr[1]]
+    key = (bex.ul[1], bex.lr[1])
+    beta = 0.0 if (lone and key not in started) else 1.0
+    started.add(key)
+    be.gemm(at, bt, cview, 1.0, beta)
+  output = distarray.create(out_shape, dtype, reducer=np.add, tile_hint=tile_hint)
+  _scatter_full(output, C.reshape(out_shape), 'sum')
+  return output
+
+
+def _scatter_full(output, full, op):
+  """Sum the per-rank full buffers and deliver each output tile to its owner."""
+  from .engine import _copy_out, _rank_slabs
+  ctx = runtime.get()
+  be = backend.get()
+  if not ctx.distributed and len(output.local) == 1:
+    (d, t), = output.local.items()
+    if tuple(d.ul) == (0,) * len(output.shape) and tuple(t.shape) == tuple(output.shape):
+      t.data = full.reshape(t.shape) if full.is_contiguous() else full.contiguous().reshape(t.shape)
+      t.written = [d]
+      return
+  if ctx.distributed:
+    if _rank_slabs(output, ctx) and ctx.dist_backend == 'nccl':
+      (d, t), = output.local.items()
+      comm.reduce_scatter_rows(t.data, full.contiguous(), op)
+      t.written = [d]
+      return
+    comm.all_reduce(full, op)
+  for d, t in output.local.items():
+    _copy_out(be, t, full.contiguous(), d)
+
+
+def _combine_rows(partials, A, M, N, out_shape, dtype, tile_hint, k_split):
+  """Row-block partials {A extent: (rows, N) tensor} -> output DistArray."""
+  import torch
+  ctx = runtime.get()
+  be = backend.get()
+  output = distarray.create(out_shape, dtype, reducer=np.add, tile_hint=tile_hint)
+  two_d = len(out_shape) == 2
+  # aligned: every A row block is exactly an output tile of the same rank, no K split
+  aligned = not k_split
+  if aligned:
+    for ex2, w in A.tiles2().items():
+      d = ext.create((ex2.ul[0], 0), (ex2.lr[0], N), (M, N)) if two_d else \
+          ext.create((ex2.ul[0],), (ex2.lr[0],), out_shape)
+      if d not in output.tiles or ctx.owner(output.tiles[d]) != ctx.owner(w):
+        aligned = False
+        break
+  if aligned:
+    for ex2, ct in partials.items():
+      d = ext.create((ex2.ul[0], 0), (ex2.lr[0], N), (M, N)) if two_d else \
+          ext.create((ex2.ul[0],), (ex2.lr[0],), out_shape)
+      t = output.local[d]
+      t.data = ct.reshape(t.shape)
+      t.written = [d]
+    return output
+  full = torch.zeros((M, N), dtype=backend.torch_dtype(dtype), device=ctx.device)
+  for ex2, ct in partials.items():
+    be.merge(full, None, (ex2.ul[0], 0), ct, 'sum', fastpath=False)
+  _scatter_full(output, full.reshape(out_shape), 'sum')
+  return output

@@ -1,0 +1,232 @@
+"""Local (tile-level) expressions and their lowering to the kernel IR.
+
+Restates the tree of spartan/expr/local.py (LocalInput :54-69, FnCallExpr
+:72-122, LocalMapExpr :127-128, LocalMapLocationExpr :130-142,
+LocalReduceExpr :144-145).  The reference *evaluates* this tree with one NumPy
+call per node per tile; here the tree is only ever *lowered* -- to the IR of
+``spartan_amd.codegen`` -- and executed as one generated gfx950 kernel.
+
+Lowering rules (``lower``):
+  * NumPy ufuncs                      -> ``codegen.Op`` (NumPy dtype resolution);
+  * registered builtin mappers        -> their IR (``ones``/``zeros`` constants,
+                                         ``astype`` casts, ``rand``/``arange``
+                                         generator leaves materialised by spx_fill);
+  * any other Python callable         -> traced once with symbolic proxies
+                                         (operators and ufuncs on the proxies
+                                         record IR); if tracing fails the map
+                                         cannot run on the GPU and
+                                         ``CodegenError`` is raised -- there is
+                                         no host fallback.
+"""
+import itertools
+
+import numpy as np
+
+from .. import codegen
+
+_var_ids = itertools.count()
+
+
+class CodegenError(NotImplementedError):
+  pass
+
+
+def make_var():
+  """Unique variable name for a tile input (reference local.py:27-29)."""
+  return 'key_%d' % next(_var_ids)
+
+
+class LocalExpr:
+  def __init__(self, deps=None):
+    self.deps = list(deps or [])
+
+  def add_dep(self, v):
+    self.deps.append(v)
+
+  def input_names(self):
+    out = []
+    for d in self.deps:
+      for n in d.input_names():
+        if n not in out:
+          out.append(n)
+    return out
+
+  def __repr__(self):
+    return self.pretty_str()
+
+
+class LocalInput(LocalExpr):
+  def __init__(self, idx):
+    super().__init__()
+    assert idx
+    self.idx = idx
+
+  def pretty_str(self):
+    return self.idx
+
+  def input_names(self):
+    return [self.idx]
+
+
+class FnCallExpr(LocalExpr):
+  def __init__(self, fn=None, deps=None, kw=None, pretty_fn=None):
+    super().__init__(deps)
+    assert fn is not None
+    self.fn = fn
+    self.kw = dict(kw or {})
+    self.pretty_fn = pretty_fn
+
+  def fn_name(self):
+    if self.pretty_fn:
+      return self.pretty_fn
+    return getattr(self.fn, '__name__', repr(self.fn))
+
+  def pretty_str(self):
+    args = ','.join(d.pretty_str() for d in self.deps)
+    return '%s(%s)' % (self.fn_name().split('.')[-1], args)
+
+
+class LocalMapExpr(FnCallExpr):
+  _op_type = 'map'
+
+
+class LocalMapLocationExpr(LocalMapExpr):
+  _op_type = 'map_location'
+
+
+class LocalReduceExpr(FnCallExpr):
+  _op_type = 'reduce'
+
+
+# ---------------------------------------------------------------- lowering
+class Pre(codegen.In):
+  """A generator leaf (rand / arange ...) materialised into a tile by spx_fill
+  before the fused kernel runs; it then becomes an ordinary array input."""
+  __slots__ = ('kind', 'params', 'src_var')
+
+  def __init__(self, kind, dtype, params, src_var):
+    super().__init__(-1, dtype)
+    self.kind, self.params, self.src_var = kind, params, src_var
+
+  def sig(self):
+    return 'i%d:%s' % (self.slot, self.dtype.str)
+
+
+# builtin mapper registry: fn -> (lowering callable(fn_expr, lowered_deps, env) -> IR)
+_BUILTIN_LOWERINGS = {}
+
+
+def register_lowering(fn, lowering):
+  _BUILTIN_LOWERINGS[fn] = lowering
+  return fn
+
+
+class LowerEnv:
+  """Maps LocalInput names to IR leaves while lowering one tree."""
+
+  def __init__(self, leaves):
+    self.leaves = leaves  # var name -> IR leaf (In / Sc / Const) or ('array', dtype) placeholders
+    self.pres = []        # Pre leaves created
+    self.scalars = []     # Sc leaves created
+
+  def new_scalar(self, value):
+    sc = codegen.Sc(len(self.scalars), value)
+    if len(self.scalars) >= codegen.MAX_IN:
+      raise CodegenError('too many scalar constants in one fused expression')
+    self.scalars.append(sc)
+    return sc
+
+
+def lower(op, env):
+  """Lower a LocalExpr tree to codegen IR."""
+  if isinstance(op, LocalInput):
+    if op.idx not in env.leaves:
+      raise CodegenError('unbound tile input %s' % op.idx)
+    return env.leaves[op.idx]
+  if not isinstance(op, FnCallExpr):
+    raise CodegenError('cannot lower %r' % (op,))
+  fn = op.fn
+  if fn in _BUILTIN_LOWERINGS:
+    return _BUILTIN_LOWERINGS[fn](op, env)
+  deps = [d for d in op.deps if not (isinstance(d, LocalInput) and d.idx == 'extent')]
+  args = [lower(d, env) for d in deps]
+  if isinstance(fn, np.ufunc):
+    if op.kw:
+      raise CodegenError('ufunc %s with keywords %s' % (fn.__name__, op.kw))
+    if fn.nout != 1 or fn.nin != len(args):
+      raise CodegenError('ufunc %s arity' % fn.__name__)
+    return codegen.Op(fn.__name__, args)
+  return trace_callable(fn, args, op.kw, env)
+
+
+# ------------------------------------------------------------------ tracing
+class Sym:
+  """Symbolic tile value used to trace user mapper functions into IR."""
+  __array_priority__ = 1000
+
+  def __init__(self, node, env):
+    self.node, self.env = node, env
+
+  @property
+  def dtype(self):
+    return self.node.dtype
+
+  def _wrap(self, v):
+    if isinstance(v, Sym):
+      return v.node
+    if isinstance(v, (bool, int, float, np.generic)) and np.ndim(v) == 0:
+      return self.env.new_scalar(v.item() if isinstance(v, np.generic) else v)
+    raise CodegenError('cannot trace operand of type %s' % type(v).__name__)
+
+  def __array_ufunc__(self, ufunc, method, *inputs, **kw):
+    if method != '__call__' or kw:
+      raise CodegenError('unsupported ufunc use %s.%s %s' % (ufunc.__name__, method, kw))
+    return Sym(codegen.Op(ufunc.__name__, [self._wrap(x) for x in inputs]), self.env)
+
+  def _bin(name, rev=False):
+    def f(self, other):
+      a, b = (other, self) if rev else (self, other)
+      return Sym(codegen.Op(name, [self._wrap(a), self._wrap(b)]), self.env)
+    return f
+
+  __add__, __radd__ = _bin('add'), _bin('add', True)
+  __sub__, __rsub__ = _bin('subtract'), _bin('subtract', True)
+  __mul__, __rmul__ = _bin('multiply'), _bin('multiply', True)
+  __truediv__, __rtruediv__ = _bin('true_divide'), _bin('true_divide', True)
+  __floordiv__, __rfloordiv__ = _bin('floor_divide'), _bin('floor_divide', True)
+  __mod__, __rmod__ = _bin('remainder'), _bin('remainder', True)
+  __pow__, __rpow__ = _bin('power'), _bin('power', True)
+  __lt__, __le__ = _bin('less'), _bin('less_equal')
+  __gt__, __ge__ = _bin('greater'), _bin('greater_equal')
+  __eq__, __ne__ = _bin('equal'), _bin('not_equal')
+  __and__, __or__, __xor__ = _bin('logical_and'), _bin('logical_or'), _bin('logical_xor')
+  del _bin
+
+  def __neg__(self):
+    return Sym(codegen.Op('negative', [self.node]), self.env)
+
+  def __abs__(self):
+    return Sym(codegen.Op('absolute', [self.node]), self.env)
+
+  def astype(self, dtype):
+    return Sym(codegen.Cast(self.node, np.dtype(dtype)), self.env)
+
+  def __bool__(self):
+    raise CodegenError('data-dependent control flow cannot be traced')
+
+  __hash__ = object.__hash__
+
+
+def trace_callable(fn, args, kw, env):
+  syms = [Sym(a, env) for a in args]
+  try:
+    out = fn(*syms, **kw)
+  except CodegenError:
+    raise
+  except Exception as e:
+    raise CodegenError('mapper %s cannot be lowered to a gfx950 kernel (%s: %s)'
+                       % (getattr(fn, '__name__', fn), type(e).__name__, e))
+  if isinstance(out, Sym):
+    return out.node
+  raise CodegenError('mapper %s did not return a traced tile value'
+                     % getattr(fn, '__name__', fn))

@@ -1,0 +1,103 @@
+"""Per-process runtime: which GPU this rank drives and who owns which worker.
+
+Replaces the reference's master/worker cluster (spartan/cluster.py:120-164,
+spartan/master.py, spartan/worker.py, spartan/blob_ctx.py) with the MI355X
+execution model: ONE process per GPU, launched by torchrun, all processes
+running the same (SPMD) program.  A tile *worker* index (the reference's
+``TileId.worker``, spartan/core.pyx:16-41) is owned by rank ``worker % world``.
+Every rank computes the same tile plan, runs the kernels for the tiles it owns
+on its own GPU, and exchanges data only through torch.distributed collectives
+(backend "nccl" == RCCL over xGMI on ROCm; "gloo" for CPU-only tests).
+"""
+import os
+
+from .config import FLAGS
+
+_ctx = None
+
+
+class Context:
+  def __init__(self, rank, world_size, local_rank, device, dist_backend):
+    self.rank = rank
+    self.world_size = world_size
+    self.local_rank = local_rank
+    self.device = device
+    self.dist_backend = dist_backend
+    self.num_workers = int(FLAGS.num_workers or world_size)
+    if self.num_workers < 1:
+      raise ValueError('num_workers must be >= 1')
+
+  # reference blob_ctx.BlobCtx.num_workers semantics
+  def owner(self, worker):
+    return worker % self.world_size
+
+  def is_local(self, worker):
+    return self.owner(worker) == self.rank
+
+  def is_master(self):
+    return self.rank == 0
+
+  @property
+  def distributed(self):
+    return self.world_size > 1
+
+  def __repr__(self):
+    return 'Context(rank=%d/%d, device=%s, workers=%d)' % (self.rank, self.world_size, self.device,
+                                                            self.num_workers)
+
+
+def initialize(argv=None, device=None):
+  """Bring up this rank (reference spartan.initialize, spartan/__init__.py:42-56).
+
+  Reads RANK / WORLD_SIZE / LOCAL_RANK from the torchrun environment, selects
+  cuda:LOCAL_RANK, and initialises torch.distributed (nccl on GPU) when the
+  world has more than one rank.  ``device`` overrides the device (tests run
+  the host logic on 'cpu' with a test backend and gloo)."""
+  global _ctx
+  import torch
+  if argv is not None:
+    FLAGS.parse(list(argv))
+  world = int(os.environ.get('WORLD_SIZE', '1'))
+  rank = int(os.environ.get('RANK', '0'))
+  local_rank = int(os.environ.get('LOCAL_RANK', str(rank)))
+  if device is None:
+    if not torch.cuda.is_available():
+      raise RuntimeError('spartan_amd needs a ROCm GPU (torch.cuda.is_available() is False)')
+    device = torch.device('cuda', local_rank % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(device)
+  device = torch.device(device)
+  backend = None
+  if world > 1:
+    import torch.distributed as dist
+    backend = 'nccl' if device.type == 'cuda' else 'gloo'
+    if not dist.is_initialized():
+      os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+      kw = {}
+      if device.type == 'cuda':
+        kw['device_id'] = device
+      dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+  _ctx = Context(rank, world, local_rank, device, backend)
+  return _ctx
+
+
+def shutdown():
+  global _ctx
+  if _ctx is not None and _ctx.distributed:
+    import torch.distributed as dist
+    if dist.is_initialized():
+      dist.barrier()
+      dist.destroy_process_group()
+  _ctx = None
+
+
+def get():
+  if _ctx is None:
+    initialize()
+  return _ctx
+
+
+def set_context(ctx):
+  global _ctx
+  prev = _ctx
+  _ctx = ctx
+  return prev

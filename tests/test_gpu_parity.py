@@ -1,0 +1,336 @@
+"""GPU parity: spartan_amd (libspx.so + generated gfx950 kernels) vs the oracle.
+
+Shapes and expectations restate the reference's own hot-path tests
+(tests/test_reduce.py, test_dot.py, test_matmul.py, test_maptiles.py) plus
+the BASELINE configs at oracle-friendly sizes.  Tolerances (BASELINE.json
+north_star): integer / index results bit-exact; fp32 1e-5 relative, fp64
+1e-12 relative -- for reductions either within that of the reference CPU
+result, or at least as close to the exact (fp64-accumulated) value as the
+reference CPU result is.
+"""
+import numpy as np
+import pytest
+
+from oracle import rng
+from oracle import spartan_cpu as O
+
+pytestmark = pytest.mark.gpu
+
+TEST_SIZE = 50
+WORKERS = [1, 3]
+
+
+def check_fp(gpu, cpu, exact, rtol):
+  gpu, cpu, exact = (np.asarray(v, dtype=np.float64) for v in (gpu, cpu, exact))
+  assert gpu.shape == cpu.shape
+  scale = np.maximum(np.abs(cpu), 1e-30)
+  close = np.abs(gpu - cpu) <= rtol * scale
+  better = np.abs(gpu - exact) <= np.abs(cpu - exact) + rtol * 1e-3 * scale
+  bad = ~(close | better)
+  assert not bad.any(), 'max rel err %g at %s' % (
+      (np.abs(gpu - cpu) / scale).max(), np.argwhere(bad)[:5])
+
+
+@pytest.fixture
+def ex(gpu_workers):
+  from spartan_amd import expr
+  return expr, gpu_workers
+
+
+# ------------------------------------------------------------ reduce KATs
+@pytest.mark.parametrize('W', WORKERS)
+def test_sum_3d(ex, W):
+  expr, setw = ex
+  setw(W)
+  x = expr.arange((TEST_SIZE,) * 3, dtype=np.int64)
+  nx = np.arange(TEST_SIZE ** 3, dtype=np.int64).reshape((TEST_SIZE,) * 3)
+  for axis in [None, 0, 1, 2]:
+    got = x.sum(axis).glom()
+    np.testing.assert_array_equal(got, nx.sum(axis))
+    np.testing.assert_array_equal(got, O.sum_tiles(nx, axis, W))
+
+
+@pytest.mark.parametrize('W', WORKERS)
+def test_sum_2d_1d(ex, W):
+  expr, setw = ex
+  setw(W)
+  x = expr.arange((TEST_SIZE, TEST_SIZE), dtype=np.int64)
+  nx = np.arange(TEST_SIZE * TEST_SIZE, dtype=np.int64).reshape((TEST_SIZE, TEST_SIZE))
+  for axis in [None, 0, 1]:
+    np.testing.assert_array_equal(x.sum(axis).glom(), nx.sum(axis))
+  y = expr.arange((TEST_SIZE,), dtype=np.int64)
+  np.testing.assert_array_equal(y.sum().glom(), np.arange(TEST_SIZE).sum())
+
+
+@pytest.mark.parametrize('W', WORKERS)
+@pytest.mark.parametrize('kind', ['argmin', 'argmax'])
+def test_arg_3d(ex, W, kind):
+  expr, setw = ex
+  setw(W)
+  x = expr.arange((TEST_SIZE,) * 3, dtype=np.int64)
+  nx = np.arange(TEST_SIZE ** 3, dtype=np.int64).reshape((TEST_SIZE,) * 3)
+  for axis in [None, 0, 1, 2]:
+    got = getattr(x, kind)(axis).glom()
+    np.testing.assert_array_equal(got, getattr(nx, kind)(axis))
+    np.testing.assert_array_equal(got, O.arg_tiles(nx, axis, W, kind))
+
+
+@pytest.mark.parametrize('W', WORKERS)
+def test_arg_1d_2d(ex, W):
+  expr, setw = ex
+  setw(W)
+  x = expr.arange((TEST_SIZE,), dtype=np.int64)
+  assert x.argmin().glom() == 0 and x.argmax().glom() == TEST_SIZE - 1
+  y = expr.arange((TEST_SIZE, TEST_SIZE), dtype=np.int64)
+  ny = np.arange(TEST_SIZE * TEST_SIZE).reshape(TEST_SIZE, TEST_SIZE)
+  np.testing.assert_array_equal(expr.glom(y.argmin(axis=1)), ny.argmin(axis=1))
+  np.testing.assert_array_equal(expr.glom(y.argmax(axis=1)), ny.argmax(axis=1))
+
+
+@pytest.mark.parametrize('W', WORKERS)
+def test_simple_sum_and_counts(ex, W):
+  expr, setw = ex
+  setw(W)
+  for axis in [0, 1, None]:
+    a = expr.ones((TEST_SIZE, TEST_SIZE)) + expr.ones((TEST_SIZE, TEST_SIZE))
+    np.testing.assert_array_equal(a.sum(axis=axis).glom(), 2 * np.ones((TEST_SIZE, TEST_SIZE)).sum(axis))
+  assert expr.count_nonzero(expr.ones((TEST_SIZE,))).glom() == TEST_SIZE
+  assert expr.count_nonzero(expr.zeros((TEST_SIZE,))).glom() == 0
+  assert expr.count_zero(expr.ones((TEST_SIZE,))).glom() == 0
+  assert expr.count_zero(expr.zeros((TEST_SIZE,))).glom() == TEST_SIZE
+
+
+# ------------------------------------------------------------------ maps
+@pytest.mark.parametrize('W', WORKERS)
+def test_maptiles(ex, W):
+  expr, setw = ex
+  setw(W)
+  a, b = expr.ones((20, 20)), expr.ones((20, 20))
+  np.testing.assert_array_equal((a + b).glom(), 2 * np.ones((20, 20)))
+  c = expr.ones((10, 10))
+  np.testing.assert_array_equal((a[0:10, 0:10] if False else c + c + c).glom(), 3 * np.ones((10, 10)))
+  many = expr.ones((10, 10))
+  m2 = expr.ones((10, 10))
+  s = many + m2 + many + m2 + many + m2 + many + m2 + many + m2
+  np.testing.assert_array_equal(s.glom(), 10 * np.ones((10, 10)))
+  l = 1.0 + expr.ones((100,), dtype=np.float32)
+  got = expr.ln(l).glom()
+  assert got.dtype == np.float32
+  np.testing.assert_allclose(got, np.log(1.0 + np.ones(100, np.float32)), rtol=1e-6)
+  d1, d2 = expr.ones((2, 1)), expr.ones((2, 5))
+  np.testing.assert_array_equal((d1 / d2).glom(), np.ones((2, 5)))
+  np.testing.assert_array_equal((d2 / d1).glom(), np.ones((2, 5)))
+
+
+@pytest.mark.parametrize('W', [1, 2, 3])
+def test_broadcast_and_scalars(ex, W):
+  expr, setw = ex
+  setw(W)
+  n = np.arange(24.0).reshape(4, 6)
+  x = expr.from_numpy(n)
+  row = expr.from_numpy(np.arange(6.0).reshape(1, 6))
+  col = expr.from_numpy(np.arange(4.0).reshape(4, 1))
+  np.testing.assert_array_equal((x + row).glom(), n + np.arange(6.0).reshape(1, 6))
+  np.testing.assert_array_equal((x * col - 2).glom(), n * np.arange(4.0).reshape(4, 1) - 2)
+  np.testing.assert_array_equal(expr.maximum(x, 7.5).glom(), np.maximum(n, 7.5))
+  np.testing.assert_array_equal(((x - row) * col).sum(axis=0).glom(),
+                                ((n - np.arange(6.0)) * np.arange(4.0).reshape(4, 1)).sum(0))
+
+
+def test_lambda_map_traced(ex):
+  expr, setw = ex
+  setw(2)
+  n = np.arange(12.0).reshape(3, 4)
+  x = expr.from_numpy(n)
+  got = expr.map(x, lambda v: np.sqrt(v) * 2 + 1).glom()
+  np.testing.assert_allclose(got, np.sqrt(n) * 2 + 1, rtol=1e-15)
+
+
+# ------------------------------------------------------------------- dot
+@pytest.mark.parametrize('W', WORKERS)
+def test_dot_kats(ex, W):
+  expr, setw = ex
+  setw(W)
+  for (m, k, n) in [(132, 100, 77), (67, 100, 77)]:
+    av, bv = expr.arange((m, k)), expr.arange((k, n))
+    na, nb = np.arange(m * k).reshape(m, k), np.arange(k * n).reshape(k, n)
+    got = expr.dot(av, bv).glom()
+    np.testing.assert_array_equal(got, np.dot(na, nb))
+    np.testing.assert_array_equal(got, O.dot_tiles(na.astype(np.float64), nb.astype(np.float64), W))
+  cv, dv = expr.arange((77, 100)), np.arange(8800).reshape(100, 88)
+  np.testing.assert_array_equal(expr.dot(cv, dv).glom(), np.dot(np.arange(7700).reshape(77, 100), dv))
+
+
+@pytest.mark.parametrize('W', WORKERS)
+def test_dot_vectors(ex, W):
+  expr, setw = ex
+  setw(W)
+  av, bv = expr.arange(stop=100), expr.arange(stop=100)
+  np.testing.assert_array_equal(expr.dot(av, bv).glom(), np.dot(np.arange(100), np.arange(100)))
+  for (m, k) in [(100, 77), (77, 100)]:
+    a2, b1 = expr.arange((m, k)), expr.arange(stop=k)
+    np.testing.assert_array_equal(expr.dot(a2, b1).glom(), np.dot(np.arange(m * k).reshape(m, k), np.arange(k)))
+  np.testing.assert_array_equal(expr.dot(expr.arange(stop=100), np.arange(100)).glom(),
+                                np.dot(np.arange(100), np.arange(100)))
+  np.testing.assert_array_equal(expr.dot(expr.arange((77, 100)), np.arange(100)).glom(),
+                                np.dot(np.arange(7700).reshape(77, 100), np.arange(100)))
+  with pytest.raises(ValueError):
+    expr.dot(expr.arange((3, 4)), expr.arange((5, 2)))
+
+
+@pytest.mark.parametrize('W', WORKERS)
+def test_matmul_int_and_f64(ex, W):
+  expr, setw = ex
+  setw(W)
+  x = expr.arange((100, 50), dtype=np.int64).astype(np.float64)
+  y = expr.arange((50, 100), dtype=np.int64).astype(np.float64)
+  nx = np.arange(5000, dtype=np.int64).reshape(100, 50).astype(np.float64)
+  ny = np.arange(5000, dtype=np.int64).reshape(50, 100).astype(np.float64)
+  np.testing.assert_array_equal(expr.dot(x, y).glom(), np.dot(nx, ny))
+
+
+@pytest.mark.parametrize('dtype,rtol', [(np.float32, 1e-5), (np.float64, 1e-12)])
+@pytest.mark.parametrize('shape', [(256, 192, 160), (512, 512, 512), (130, 70, 33)])
+@pytest.mark.parametrize('W', [1, 4])
+def test_gemm_random(ex, dtype, rtol, shape, W):
+  expr, setw = ex
+  setw(W)
+  m, k, n = shape
+  a = rng.rand((m, k), 31, dtype)
+  b = rng.rand((k, n), 32, dtype)
+  got = expr.dot(expr.from_numpy(a), expr.from_numpy(b)).glom()
+  assert got.dtype == dtype
+  cpu = O.dot_tiles(a, b, W)
+  exact = a.astype(np.float64) @ b.astype(np.float64)
+  check_fp(got, cpu, exact, rtol)
+
+
+def test_gemm_layout_asymmetric(ex):
+  """A = I with an asymmetric B catches a transposed C write."""
+  expr, setw = ex
+  setw(1)
+  for dt in (np.float32, np.float64):
+    a = np.eye(128, dtype=dt)
+    b = np.arange(128 * 128, dtype=dt).reshape(128, 128) % 97
+    np.testing.assert_array_equal(expr.dot(expr.from_numpy(a), expr.from_numpy(b)).glom(), b)
+
+
+# ------------------------------------------------ fills (bit-exact generator)
+@pytest.mark.parametrize('dtype', [np.float32, np.float64])
+@pytest.mark.parametrize('W', [1, 3])
+def test_rand_bit_exact(ex, dtype, W):
+  expr, setw = ex
+  setw(W)
+  got = expr.rand(97, 53, dtype=dtype, seed=7).glom()
+  np.testing.assert_array_equal(got, rng.rand((97, 53), 7, dtype))
+  got = expr.rand(64, 33, dtype=dtype, seed=8, low=-1.0, high=1.0).glom()
+  np.testing.assert_array_equal(got, rng.rand((64, 33), 8, dtype, -1.0, 1.0))
+
+
+# ------------------------------------------------ cfg2 class: fused map+reduce
+def _cfg2_inputs(shape):
+  x = rng.rand(shape, 11, np.float32)
+  y = rng.rand(shape, 12, np.float32)
+  z = rng.rand(shape, 13, np.float32, -1.0, 1.0)
+  return x, y, z
+
+
+@pytest.mark.parametrize('shape', [(96, 80), (257, 131), (1024, 3000)])
+@pytest.mark.parametrize('W', [1, 2, 3, 8])
+def test_fused_map_reduce_cfg2(ex, shape, W):
+  expr, setw = ex
+  setw(W)
+  nx, ny, nz = _cfg2_inputs(shape)
+  x = expr.rand(*shape, dtype=np.float32, seed=11)
+  y = expr.rand(*shape, dtype=np.float32, seed=12)
+  z = expr.rand(*shape, dtype=np.float32, seed=13, low=-1.0, high=1.0)
+  mapped = O.map_tiles(lambda a, b, c: a * b + np.exp(c), [nx, ny, nz], W)
+  # materialised map: elementwise, within 1e-5 relative of the CPU result
+  m = (x * y + expr.exp(z)).optimized().glom()
+  np.testing.assert_allclose(m, mapped, rtol=1e-6)
+  exact_src = mapped.astype(np.float64)
+  for axis in [None, 0, 1]:
+    got = expr.sum(x * y + expr.exp(z), axis=axis).optimized().glom()
+    cpu = O.sum_tiles(mapped, axis, W)
+    check_fp(got, cpu, exact_src.sum(axis), 1e-5)
+    for red, oref in [(expr.min, O.min_tiles), (expr.max, O.max_tiles)]:
+      got = red(x * y + expr.exp(z), axis=axis).optimized().glom()
+      np.testing.assert_allclose(got, oref(mapped, axis, W), rtol=1e-6)
+    for kind in ['argmin', 'argmax']:
+      got = getattr(expr, kind)(x * y + expr.exp(z), axis=axis).optimized().glom()
+      want = O.arg_tiles(mapped, axis, W, kind)
+      # indices must be bit-exact wherever the mapped values are bit-exact
+      agree = (m == mapped)
+      if agree.all():
+        np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize('W', [1, 3, 4])
+def test_argmin_ties_cross_tiles(ex, W):
+  expr, setw = ex
+  setw(W)
+  a = np.zeros((12, 10), dtype=np.float64)
+  a[3, 4] = a[7, 4] = a[11, 9] = -5.0  # ties in different row strips
+  a[5, :] = -1.0
+  x = expr.from_numpy(a)
+  for axis in [None, 0, 1]:
+    np.testing.assert_array_equal(x.argmin(axis).glom(), a.argmin(axis))
+    np.testing.assert_array_equal(x.argmin(axis).glom(), O.arg_tiles(a, axis, W))
+    np.testing.assert_array_equal((-x).argmax(axis).glom(), (-a).argmax(axis))
+
+
+def test_empty_and_ragged(ex):
+  expr, setw = ex
+  setw(3)
+  for shape in [(1,), (2,), (5, 1), (1, 7), (3, 3, 1), (7, 13)]:
+    n = np.arange(int(np.prod(shape)), dtype=np.float64).reshape(shape) - 3.5
+    x = expr.from_numpy(n)
+    for axis in [None] + list(range(len(shape))):
+      np.testing.assert_array_equal(x.sum(axis).glom(), n.sum(axis))
+      np.testing.assert_array_equal(x.max(axis).glom() if hasattr(x, 'max') else expr.max(x, axis).glom(),
+                                    n.max(axis))
+      np.testing.assert_array_equal(x.argmin(axis).glom(), n.argmin(axis))
+
+
+def test_int32_and_bool_semantics(ex):
+  expr, setw = ex
+  setw(3)
+  n = (np.arange(60, dtype=np.int32).reshape(6, 10) * 1000003)
+  x = expr.from_numpy(n)
+  for axis in [None, 0, 1]:
+    got = x.sum(axis).glom()
+    assert got.dtype == np.int32
+    np.testing.assert_array_equal(got, O.sum_tiles(n, axis, 3))
+  b = expr.from_numpy(n % 3 == 0)
+  np.testing.assert_array_equal(expr.count_nonzero(b).glom(), np.count_nonzero(n % 3 == 0))
+  m = expr.mean(x, 0).glom()
+  np.testing.assert_array_equal(m, n.sum(0) // 6)
+
+
+def test_full_size_checksums(ex):
+  """cfg2 at its BASELINE size (2^30 fp32): size-independent properties --
+  the axis-0, axis-1 and full sums agree (checksum of checksums) and the
+  reductions equal the reduction of the materialised map."""
+  expr, setw = ex
+  setw(1)
+  shape = (32768, 32768)
+  x = expr.rand(*shape, dtype=np.float32, seed=11).force()
+  y = expr.rand(*shape, dtype=np.float32, seed=12).force()
+  z = expr.rand(*shape, dtype=np.float32, seed=13, low=-1.0, high=1.0).force()
+  xs, ys, zs = expr.lazify(x), expr.lazify(y), expr.lazify(z)
+  s0 = expr.sum(xs * ys + expr.exp(zs), axis=0).optimized().glom().astype(np.float64)
+  s1 = expr.sum(xs * ys + expr.exp(zs), axis=1).optimized().glom().astype(np.float64)
+  s = float(expr.sum(xs * ys + expr.exp(zs)).optimized().glom())
+  assert s0.shape == (32768,) and s1.shape == (32768,)
+  assert abs(s0.sum() - s1.sum()) <= 1e-5 * abs(s1.sum())
+  assert abs(s - s1.sum()) <= 1e-5 * abs(s1.sum())
+  # E[x*y + exp(z)] = 1/4 + (e - 1/e)/2
+  mean = s / (32768.0 * 32768.0)
+  assert abs(mean - (0.25 + (np.e - 1 / np.e) / 2)) < 1e-3
+  # spot rows against the oracle restatement
+  for r in (0, 12345, 32767):
+    g = np.arange(r * 32768, (r + 1) * 32768, dtype=np.uint64)
+    row = (rng.uniform_values(g, 11, 0.0, 1.0, np.float32) * rng.uniform_values(g, 12, 0.0, 1.0, np.float32)
+           + np.exp(rng.uniform_values(g, 13, -1.0, 1.0, np.float32)))
+    check_fp(s1[r:r + 1].astype(np.float32), np.array([row.sum()], np.float32),
+             np.array([row.astype(np.float64).sum()]), 1e-5)
