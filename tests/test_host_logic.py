@@ -1,0 +1,124 @@
+"""Host-side logic of the expression engine (tiling, fusion, partial combine,
+tile merge) on CPU, with the TEST-DOUBLE backend standing in for libspx.so.
+Numerics of the real kernels are covered by the -m gpu tests."""
+import numpy as np
+import pytest
+
+from oracle import rng
+from oracle import spartan_cpu as O
+
+
+@pytest.mark.parametrize('W', [1, 2, 3, 5, 8])
+def test_reductions_all_workers(host_ctx, W):
+  host_ctx(W)
+  from spartan_amd import expr
+  for shape in [(50,), (50, 50), (12, 7, 5)]:
+    nx = np.arange(int(np.prod(shape)), dtype=np.int64).reshape(shape)
+    x = expr.arange(shape, dtype=np.int64)
+    for axis in [None] + list(range(len(shape))):
+      np.testing.assert_array_equal(x.sum(axis).glom(), O.sum_tiles(nx, axis, W))
+      np.testing.assert_array_equal(x.argmin(axis).glom(), O.arg_tiles(nx, axis, W))
+      np.testing.assert_array_equal(x.argmax(axis).glom(), O.arg_tiles(nx, axis, W, 'argmax'))
+      np.testing.assert_array_equal(expr.max(x, axis).glom(), O.max_tiles(nx, axis, W))
+
+
+def test_fusion_builds_one_node(host_ctx):
+  host_ctx(1)
+  from spartan_amd import expr
+  from spartan_amd.expr.map import MapExpr
+  from spartan_amd.expr.reduce import ReduceExpr
+  x = expr.rand(8, 8, dtype=np.float32, seed=1).force()
+  y = expr.rand(8, 8, dtype=np.float32, seed=2).force()
+  X, Y = expr.lazify(x), expr.lazify(y)
+  e = expr.sum(X * Y + expr.exp(Y), axis=0).optimized()
+  assert isinstance(e, ReduceExpr)
+  assert len(e.children) == 3 or len(e.children) == 2
+  assert not any(isinstance(c, MapExpr) for c in e.children)
+  assert 'exp' in repr(e.op.deps[1])
+  m = (X * Y + 1.0).optimized()
+  assert isinstance(m, MapExpr) and not any(isinstance(c, MapExpr) for c in m.children)
+
+
+def test_force_does_not_optimize_and_cache(host_ctx):
+  host_ctx(1)
+  from spartan_amd import expr
+  a = expr.ones((4, 4))
+  b = a + a
+  r1 = b.force()
+  r2 = b.force()
+  assert r1 is r2  # expression cache (base.py:259-300)
+  o = b.optimized()
+  assert o is b.optimized()
+
+
+def test_update_merge_semantics(host_ctx):
+  host_ctx(3)
+  import torch
+  from spartan_amd.array import distarray, extent
+  a = distarray.create((6, 4), np.float64, reducer=np.add)
+  a.update(extent.create((0, 0), (6, 4), (6, 4)), np.ones((6, 4)))
+  a.update(extent.create((1, 0), (3, 4), (6, 4)), np.full((2, 4), 5.0))
+  want = np.ones((6, 4))
+  want[1:3] += 5
+  np.testing.assert_array_equal(a.glom(), want)
+  b = distarray.create((6,), np.float64, reducer=np.maximum)
+  b.update(extent.create((0,), (4,), (6,)), np.array([1., 9., 3., 4.]))
+  b.update(extent.create((2,), (6,), (6,)), np.array([7., 2., 8., 8.]))
+  np.testing.assert_array_equal(b.glom(), O_merge_expect())
+
+
+def O_merge_expect():
+  out = O.OArray((6,), np.float64, 3, reducer=np.maximum)
+  out.update(O.ext_create((0,), (4,), (6,)), np.array([1., 9., 3., 4.]))
+  out.update(O.ext_create((2,), (6,), (6,)), np.array([7., 2., 8., 8.]))
+  return out.glom()
+
+
+def test_dtype_rules(host_ctx):
+  host_ctx(2)
+  from spartan_amd import expr
+  f = expr.ones((3,), dtype=np.float32)
+  assert (f * 2.0).glom().dtype == np.float32        # weak python scalar
+  assert (f + f).glom().dtype == np.float32
+  i = expr.arange((4,), dtype=np.int32)
+  assert (i + 1).glom().dtype == np.int32
+  assert (i / 2).glom().dtype == np.float64
+  assert expr.sum(i).glom().dtype == np.int32        # dtype_fn(input)
+  assert expr.argmin(f).glom().dtype == np.int64
+  np.testing.assert_array_equal(expr.mean(i).glom(), np.arange(4).sum() // 4)
+
+
+def test_rand_is_tiling_independent(host_ctx):
+  outs = []
+  for W in (1, 3, 7):
+    host_ctx(W)
+    from spartan_amd import expr
+    outs.append(expr.rand(13, 11, dtype=np.float32, seed=5).glom())
+  for o in outs[1:]:
+    np.testing.assert_array_equal(o, outs[0])
+  np.testing.assert_array_equal(outs[0], rng.rand((13, 11), 5, np.float32))
+
+
+def test_unlowerable_mapper_raises(host_ctx):
+  host_ctx(1)
+  from spartan_amd import expr
+  from spartan_amd.expr.local import CodegenError
+  x = expr.ones((4,))
+  with pytest.raises(CodegenError):
+    expr.map(x, lambda v: np.sort(v)).glom()
+  with pytest.raises(CodegenError):
+    expr.map(x, lambda v: v if v > 0 else -v).glom()
+
+
+def test_dot_paths(host_ctx):
+  for W in (1, 2, 3):
+    host_ctx(W)
+    from spartan_amd import expr
+    a = rng.rand((40, 30), 1, np.float64)
+    b = rng.rand((30, 20), 2, np.float64)
+    got = expr.dot(expr.from_numpy(a), expr.from_numpy(b)).glom()
+    np.testing.assert_allclose(got, a @ b, rtol=1e-12)
+    got = expr.dot(expr.from_numpy(a), b).glom()
+    np.testing.assert_allclose(got, a @ b, rtol=1e-12)
+    v = rng.rand((30,), 3, np.float64)
+    np.testing.assert_allclose(expr.dot(expr.from_numpy(a), expr.from_numpy(v)).glom(), a @ v, rtol=1e-12)
