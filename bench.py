@@ -1,14 +1,16 @@
 #!/usr/bin/env python3
 """Headline benchmark: fused map+reduce GB/s (+ dot GFLOP/s) on MI355X.
 
-Workload (BASELINE.json configs[1]): x, y ~ U[0,1), z ~ U[-1,1) fp32 of shape
-(32768, 32768) = 2^30 elements, resident in HBM before timing; one step =
+Workload (BASELINE.json configs[1]): x, y ~ U[0,1), z ~ U[-1,1) fp32, 2^30
+elements (32768 x 32768) per GPU, resident in HBM before timing; one step =
 ``sum(x*y + exp(z), axis=0).optimized().force()`` and the same for axis=1 --
-two fused map+reduce evaluations, each reading 3 x 4 B per element (12.885 GB)
-and writing 32768 fp32.  ``value`` = algorithmic bytes of all ranks / the max
-over ranks of the timed wall time.  Multi-GPU: launched by torchrun, one rank
-per GPU; the arrays are row-strip tiled over the ranks (weak in HBM per GPU is
-fixed by the global shape: strong scaling of the fixed 2^30 problem).
+two fused map+reduce evaluations, each reading 3 x 4 B per element and writing
+32768 fp32 per GPU.  ``value`` = algorithmic bytes of all ranks / the max over
+ranks of the timed wall time.  Multi-GPU: launched by torchrun, one rank per
+GPU; the global arrays are (32768 * N, 32768), row-strip tiled so every rank
+owns one 2^30-element strip (weak scaling: per-GPU work fixed); the axis-0 sum
+combines the per-rank partials with an RCCL reduce-scatter, the axis-1 sum is
+local.  ``--strong`` keeps the global array at 2^30 instead.
 
 Also reported (secondary, ``dot``): ``dot(A, B)`` for 32768^2 fp32 (configs[3])
 in GFLOP/s, and the CPU baseline (the reference's multi-worker NumPy model,
@@ -39,6 +41,7 @@ def main():
   ap.add_argument('--dot-size', type=int, default=32768)
   ap.add_argument('--cpu-baseline', type=int, default=1)
   ap.add_argument('--cpu-rows', type=int, default=4096)
+  ap.add_argument('--strong', action='store_true', help='fixed 2^30 global array (strong scaling)')
   args = ap.parse_args()
 
   import torch
@@ -54,9 +57,10 @@ def main():
   def sync():
     torch.cuda.synchronize()
 
-  x = expr.rand(S, S, dtype=np.float32, seed=11).force()
-  y = expr.rand(S, S, dtype=np.float32, seed=12).force()
-  z = expr.rand(S, S, dtype=np.float32, seed=13, low=-1.0, high=1.0).force()
+  R = S if args.strong else S * N   # global rows
+  x = expr.rand(R, S, dtype=np.float32, seed=11).force()
+  y = expr.rand(R, S, dtype=np.float32, seed=12).force()
+  z = expr.rand(R, S, dtype=np.float32, seed=13, low=-1.0, high=1.0).force()
   X, Y, Z = expr.lazify(x), expr.lazify(y), expr.lazify(z)
 
   def step():
@@ -81,8 +85,8 @@ def main():
   be.kernel_events = None
   elapsed = comm.max_over_ranks(elapsed)
 
-  elems = S * S
-  bytes_per_eval = 3 * 4 * elems + 4 * S
+  elems = R * S
+  bytes_per_eval = 3 * 4 * elems + 4 * S * N   # + each rank's output write
   total_bytes = 2 * bytes_per_eval * args.steps
   value = total_bytes / elapsed / 1e9
   # dominant kernel: the generated fused map+reduce kernel ('spx_reduce'),
@@ -95,8 +99,13 @@ def main():
   avg = float(np.mean(red)) if red else float('nan')
   achieved = bytes_launch / avg / 1e9 if red else None
 
+  traffic = None
+  tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r01_pmc_traffic.json')
+  if os.path.exists(tpath) and rows_local == 32768 and S == 32768:
+    with open(tpath) as f:
+      traffic = json.load(f)['hbm_bytes_per_launch']
   result = {
-      'metric': 'fused map+reduce GB/s (x*y+exp(z), sum axis 0 and axis 1, 2^30 fp32)',
+      'metric': 'fused map+reduce GB/s (x*y+exp(z), sum axis 0 and axis 1, 2^30 fp32 per GPU)',
       'value': round(value, 2),
       'unit': 'GB/s',
       'n_gpus': N,
@@ -104,17 +113,19 @@ def main():
       'warmup': args.warmup,
       'ms_per_step': round(elapsed / args.steps * 1e3, 4),
       'higher_is_better': True,
-      'scaling': 'strong',
+      'scaling': 'strong' if args.strong else 'weak',
       'vs_baseline': None,
       'dtype': 'f32',
       'data': 'synthetic (counter-based splitmix64 U[0,1) / U[-1,1), resident in HBM)',
       'config': {'workload': 'cfg2: sum(x*y+exp(z), axis=0) + sum(x*y+exp(z), axis=1), x,y,z fp32 (%d,%d)'
-                             % (S, S), 'shape': [S, S], 'tiling': 'row strips over %d rank(s)' % N,
+                             % (R, S), 'shape': [R, S], 'tiling': 'row strips, one per rank (%d)' % N,
                  'parallelism': 'tile-dp%d' % N},
       'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1) if achieved else None,
                    'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                    'frac': round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                   'traffic': None,
+                   'traffic': traffic,
+                   'traffic_source': 'profiles/r01_pmc_traffic.json (FETCH_SIZE/WRITE_SIZE passes)' if traffic
+                   else None,
                    'kernel': 'spx_reduce (generated fused map+reduce)',
                    'bytes_per_launch': bytes_launch,
                    'avg_launch_ms': round(avg * 1e3, 4) if red else None,

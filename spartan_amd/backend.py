@@ -192,6 +192,7 @@ class HipBackend:
     self.launch_log = None   # optional list collecting grids (tests)
     self.kernel_events = None  # optional list of (name, start, end) HIP events (bench)
     self._names = {}
+    self._sig_fns = {}
 
   # ---------------------------------------------------------------- utils
   def stream(self):
@@ -274,8 +275,10 @@ class HipBackend:
       vec_ok = (cshape[-1] % V == 0) and out.data_ptr() % 16 == 0 and all(
           _vec_aligned(inputs[s], cstr[k], classes[k], V) for k, s in enumerate(slots))
     args.flags = 1 if (vec_ok and V > 1) else 0
-    src = codegen.gen_map(root, ins, classes, ndim, V, dense)
-    fn = self.kernel(src, 'spx_map')
+    sig = ('map', root.sig(), tuple(ins), tuple(classes), ndim, V, dense)
+    fn = self._sig_fns.get(sig)
+    if fn is None:
+      fn = self._sig_fns[sig] = self.kernel(codegen.gen_map(root, ins, classes, ndim, V, dense), 'spx_map')
     per = V if args.flags else 1
     grid = max(1, min(-(-n // (256 * per)), 256 * 16))
     self.launch(fn, grid, args)
@@ -373,8 +376,10 @@ class HipBackend:
       part_i = None
     args.out0 = part_v.data_ptr()
     args.out1 = part_i.data_ptr() if arg else 0
-    src = codegen.gen_reduce(root, ins, classes, kind, op, V)
-    fn = self.kernel(src, 'spx_reduce')
+    sig = ('reduce', root.sig(), tuple(ins), tuple(classes), kind, op, V)
+    fn = self._sig_fns.get(sig)
+    if fn is None:
+      fn = self._sig_fns[sig] = self.kernel(codegen.gen_reduce(root, ins, classes, kind, op, V), 'spx_reduce')
     self.launch(fn, nblk, args)
     if not direct:
       _check(self.lib.spx_reduce_finalize(

@@ -1,0 +1,111 @@
+"""Multi-rank (SPMD) host logic with world_size 2 on CPU over gloo.
+
+Each rank runs the same program with the TEST-DOUBLE backend; this exercises
+round-robin placement across ranks, the collective region gather, the
+reduce-scatter / all-reduce / all-gather partial combines and the K-split dot
+exchange -- the N>1 path that runs over RCCL on the GPUs.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+  s = socket.socket()
+  s.bind(('127.0.0.1', 0))
+  p = s.getsockname()[1]
+  s.close()
+  return p
+
+
+def _body(rank, world, port, W, q):
+  try:
+    sys.path.insert(0, os.path.dirname(HERE))
+    sys.path.insert(0, HERE)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch
+    from spartan_amd import backend, runtime, expr
+    from spartan_amd.config import FLAGS
+    from fake_backend import FakeBackend
+    from oracle import rng
+    from oracle import spartan_cpu as O
+    backend.set_backend(FakeBackend())
+    FLAGS.num_workers = W
+    runtime.initialize(device='cpu')
+    ctx = runtime.get()
+    assert ctx.world_size == world and ctx.dist_backend == 'gloo'
+
+    # placement: only the local tiles hold data
+    x = expr.arange((40, 30), dtype=np.int64).force()
+    for ex, w in x.tiles.items():
+      assert (ex in x.local) == (w % world == rank)
+    nx = np.arange(1200).reshape(40, 30)
+    np.testing.assert_array_equal(x.glom(), nx)
+    X = expr.lazify(x)
+    for axis in (None, 0, 1):
+      np.testing.assert_array_equal(X.sum(axis).glom(), O.sum_tiles(nx, axis, W))
+      np.testing.assert_array_equal(X.argmin(axis).glom(), nx.argmin(axis))
+      np.testing.assert_array_equal(X.argmax(axis).glom(), nx.argmax(axis))
+      np.testing.assert_array_equal(expr.min(X, axis).glom(), nx.min(axis))
+
+    # fused cfg2 class over ranks
+    shape = (64, 48)
+    xs = expr.rand(*shape, dtype=np.float32, seed=11)
+    ys = expr.rand(*shape, dtype=np.float32, seed=12)
+    zs = expr.rand(*shape, dtype=np.float32, seed=13, low=-1.0, high=1.0)
+    mapped = O.map_tiles(lambda a, b, c: a * b + np.exp(c),
+                         [rng.rand(shape, 11, np.float32), rng.rand(shape, 12, np.float32),
+                          rng.rand(shape, 13, np.float32, -1.0, 1.0)], W)
+    for axis in (None, 0, 1):
+      got = expr.sum(xs * ys + expr.exp(zs), axis=axis).optimized().glom()
+      np.testing.assert_allclose(got, mapped.sum(axis), rtol=1e-5)
+
+    # broadcast child that lives on other ranks -> collective gather_regions
+    row = expr.from_numpy(np.arange(30.0).reshape(1, 30))
+    np.testing.assert_array_equal((X + row).glom(), nx + np.arange(30.0))
+    col = expr.from_numpy(np.arange(40.0).reshape(40, 1))
+    np.testing.assert_array_equal((X * col).sum(0).glom(), (nx * np.arange(40.0).reshape(40, 1)).sum(0))
+
+    # dot: K-split with the A column-strip exchange and the partial reduction
+    a = rng.rand((24, 36), 1, np.float64)
+    b = rng.rand((36, 20), 2, np.float64)
+    got = expr.dot(expr.from_numpy(a), expr.from_numpy(b)).glom()
+    np.testing.assert_allclose(got, a @ b, rtol=1e-12)
+    np.testing.assert_allclose(expr.dot(expr.from_numpy(a), b).glom(), a @ b, rtol=1e-12)
+    v = rng.rand((36,), 3, np.float64)
+    np.testing.assert_allclose(expr.dot(expr.from_numpy(a), expr.from_numpy(v)).glom(), a @ v, rtol=1e-12)
+    q.put((rank, 'ok'))
+  except Exception as e:  # pragma: no cover - reported to the parent
+    import traceback
+    q.put((rank, traceback.format_exc()))
+  finally:
+    try:
+      from spartan_amd import runtime
+      runtime.shutdown()
+    except Exception:
+      pass
+
+
+@pytest.mark.parametrize('W', [2, 3, 4])
+def test_world2_gloo(W):
+  import multiprocessing as mp
+  ctx = mp.get_context('spawn')
+  q = ctx.Queue()
+  port = _free_port()
+  procs = [ctx.Process(target=_body, args=(r, 2, port, W, q)) for r in range(2)]
+  for p in procs:
+    p.start()
+  res = {}
+  for _ in procs:
+    r, msg = q.get(timeout=240)
+    res[r] = msg
+  for p in procs:
+    p.join(timeout=60)
+  for r in range(2):
+    assert res.get(r) == 'ok', res.get(r)
