@@ -474,229 +474,18 @@ extern "C" int spx_argreduce_combine(int op, int dtype, const void* vals, const 
 }
 
 // ==================================================================== GEMM
-// fp32: block tile 128x128, BK=16, 256 threads = 4 waves in 2x2, each wave
-// owns a 64x64 sub-tile = 2x2 v_mfma_f32_32x32x2_f32 accumulators.
-// A is staged transposed in LDS (As[k][m]) so that each MFMA operand read is
-// 32 consecutive dwords per half-wave (conflict-free ds_read_b32); B is
-// staged row-major (Bs[k][n]).  Register prefetch of the next K-tile overlaps
-// the global loads with the MFMAs of the current one (2 LDS buffers).
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef double f64x4 __attribute__((ext_vector_type(4)));
+// fp32 / fp64 MFMA kernels live in gemm_kernels.h (shared with the tuning
+// harness tools/gemm_tune.hip).  Configurations chosen by measurement on
+// MI355X (profiles/r01_gemm_tune.txt):
+//   fp32 large: 256x256x16, 16 waves (4x4), grouped order GM=8  -> 136 TF (86.6 %)
+//   fp32 small: 128x128x16, 4 waves (2x2), GM=8                 -> 131 TF at 8192
+//   fp64      : 128x128x16, 16 waves (4x4)                      -> 69.3 TF (88.2 %)
+// (the 4-wave fp64 layout needs 304 registers -> 1 wave per SIMD -> 40 TF).
+#include "gemm_kernels.h"
 
-#define G32_BM 128
-#define G32_BN 128
-#define G32_BK 16
-#define G32_PADA 4
-
-template <bool ALIGNED>
-__device__ __forceinline__ void g32_load_tiles(const float* __restrict__ A, i64 lda,
-                                               const float* __restrict__ B, i64 ldb, i64 M,
-                                               i64 N, i64 K, i64 row0, i64 col0, i64 k0, int t,
-                                               f32x4 ra[2], f32x4 rb[2]) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    int idx = t + i * 256;
-    int r = idx >> 2, kq = idx & 3;  // A: 128 rows x 4 float4
-    i64 gr = row0 + r, gk = k0 + kq * 4;
-    if (ALIGNED) {
-      ra[i] = *(const f32x4*)(A + gr * lda + gk);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        ra[i][j] = (gr < M && gk + j < K) ? A[gr * lda + gk + j] : 0.0f;
-    }
-    int kr = idx >> 5, cq = idx & 31;  // B: 16 rows x 32 float4
-    i64 bk = k0 + kr, bc = col0 + cq * 4;
-    if (ALIGNED) {
-      rb[i] = *(const f32x4*)(B + bk * ldb + bc);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        rb[i][j] = (bk < K && bc + j < N) ? B[bk * ldb + bc + j] : 0.0f;
-    }
-  }
-}
-
-__device__ __forceinline__ void g32_store_lds(float (*As)[G32_BM + G32_PADA], float (*Bs)[G32_BN], int t,
-                                              const f32x4 ra[2], const f32x4 rb[2]) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    int idx = t + i * 256;
-    int r = idx >> 2, kq = idx & 3;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) As[kq * 4 + j][r] = ra[i][j];
-    int kr = idx >> 5, cq = idx & 31;
-    *(f32x4*)(&Bs[kr][cq * 4]) = rb[i];
-  }
-}
-
-template <bool ALIGNED>
-__global__ __launch_bounds__(256) void k_gemm_f32(i64 M, i64 N, i64 K, const float* __restrict__ A,
-                                                  i64 lda, const float* __restrict__ B, i64 ldb,
-                                                  float* __restrict__ C, i64 ldc, float alpha,
-                                                  float beta, int tiles_n, int ntiles) {
-  __shared__ float As[2][G32_BK][G32_BM + G32_PADA];
-  __shared__ __attribute__((aligned(16))) float Bs[2][G32_BK][G32_BN];
-  // XCD-aware remap: consecutive tiles (sharing A row panels) land on one XCD.
-  int bid = blockIdx.x;
-  {
-    int q = ntiles / 8, rr = ntiles % 8, xcd = bid % 8;
-    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
-  }
-  int tm = bid / tiles_n, tn = bid % tiles_n;
-  i64 row0 = (i64)tm * G32_BM, col0 = (i64)tn * G32_BN;
-  int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  int wm = w >> 1, wn = w & 1;
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
-  f32x4 ra[2], rb[2];
-  int nk = (int)((K + G32_BK - 1) / G32_BK);
-  g32_load_tiles<ALIGNED>(A, lda, B, ldb, M, N, K, row0, col0, 0, t, ra, rb);
-  g32_store_lds(As[0], Bs[0], t, ra, rb);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    int cur = kt & 1;
-    if (kt + 1 < nk)
-      g32_load_tiles<ALIGNED>(A, lda, B, ldb, M, N, K, row0, col0, (i64)(kt + 1) * G32_BK, t, ra, rb);
-#pragma unroll
-    for (int kk = 0; kk < G32_BK / 2; ++kk) {
-      int k = kk * 2 + (lane >> 5);
-      float a0 = As[cur][k][wm * 64 + (lane & 31)];
-      float a1 = As[cur][k][wm * 64 + 32 + (lane & 31)];
-      float b0 = Bs[cur][k][wn * 64 + (lane & 31)];
-      float b1 = Bs[cur][k][wn * 64 + 32 + (lane & 31)];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-    }
-    if (kt + 1 < nk) {
-      g32_store_lds(As[cur ^ 1], Bs[cur ^ 1], t, ra, rb);
-    }
-    __syncthreads();
-  }
-  // epilogue: 32x32 C/D map row = (r&3) + 8*(r>>2) + 4*(lane>>5), col = lane&31
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        i64 gr = row0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        i64 gc = col0 + wn * 64 + j * 32 + (lane & 31);
-        if (gr < M && gc < N) {
-          float v = alpha * acc[i][j][r];
-          if (beta != 0.0f) v += beta * C[gr * ldc + gc];
-          C[gr * ldc + gc] = v;
-        }
-      }
-}
-
-// fp64: block 128x128, BK=8, 4 waves 2x2, wave 64x64 = 4x4 v_mfma_f64_16x16x4_f64
-// accumulators (C/D map: col = lane&15, row = (lane>>4) + 4*reg).
-#define G64_BM 128
-#define G64_BN 128
-#define G64_BK 8
-#define G64_PADA 2
-
-template <bool ALIGNED>
-__global__ __launch_bounds__(256) void k_gemm_f64(i64 M, i64 N, i64 K, const double* __restrict__ A,
-                                                  i64 lda, const double* __restrict__ B, i64 ldb,
-                                                  double* __restrict__ C, i64 ldc, double alpha,
-                                                  double beta, int tiles_n, int ntiles) {
-  __shared__ double As[2][G64_BK][G64_BM + G64_PADA];
-  __shared__ __attribute__((aligned(16))) double Bs[2][G64_BK][G64_BN];
-  int bid = blockIdx.x;
-  {
-    int q = ntiles / 8, rr = ntiles % 8, xcd = bid % 8;
-    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
-  }
-  int tm = bid / tiles_n, tn = bid % tiles_n;
-  i64 row0 = (i64)tm * G64_BM, col0 = (i64)tn * G64_BN;
-  int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  int wm = w >> 1, wn = w & 1;
-  f64x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f64x4){0, 0, 0, 0};
-  // per K-tile: A 128x8 doubles = 512 double2 (2 per thread); B 8x128 = 512 double2
-  typedef double d2 __attribute__((ext_vector_type(2)));
-  d2 ra[2], rb[2];
-  int nk = (int)((K + G64_BK - 1) / G64_BK);
-  auto load = [&](i64 k0) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int idx = t + i * 256;
-      int r = idx >> 2, kq = idx & 3;  // 4 double2 per 8-wide row
-      i64 gr = row0 + r, gk = k0 + kq * 2;
-      if (ALIGNED) ra[i] = *(const d2*)(A + gr * lda + gk);
-      else {
-        ra[i][0] = (gr < M && gk < K) ? A[gr * lda + gk] : 0.0;
-        ra[i][1] = (gr < M && gk + 1 < K) ? A[gr * lda + gk + 1] : 0.0;
-      }
-      int kr = idx >> 6, cq = idx & 63;  // 64 double2 per 128-wide row
-      i64 bk = k0 + kr, bc = col0 + cq * 2;
-      if (ALIGNED) rb[i] = *(const d2*)(B + bk * ldb + bc);
-      else {
-        rb[i][0] = (bk < K && bc < N) ? B[bk * ldb + bc] : 0.0;
-        rb[i][1] = (bk < K && bc + 1 < N) ? B[bk * ldb + bc + 1] : 0.0;
-      }
-    }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int idx = t + i * 256;
-      int r = idx >> 2, kq = idx & 3;
-      As[buf][kq * 2][r] = ra[i][0];
-      As[buf][kq * 2 + 1][r] = ra[i][1];
-      int kr = idx >> 6, cq = idx & 63;
-      *(d2*)(&Bs[buf][kr][cq * 2]) = rb[i];
-    }
-  };
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    int cur = kt & 1;
-    if (kt + 1 < nk) load((i64)(kt + 1) * G64_BK);
-#pragma unroll
-    for (int kk = 0; kk < G64_BK / 4; ++kk) {
-      int k = kk * 4 + (lane >> 4);
-      double a[4], b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = As[cur][k][wm * 64 + i * 16 + (lane & 15)];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = Bs[cur][k][wn * 64 + j * 16 + (lane & 15)];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
-    if (kt + 1 < nk) store(cur ^ 1);
-    __syncthreads();
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        i64 gr = row0 + wm * 64 + i * 16 + (lane >> 4) + 4 * r;
-        i64 gc = col0 + wn * 64 + j * 16 + (lane & 15);
-        if (gr < M && gc < N) {
-          double v = alpha * acc[i][j][r];
-          if (beta != 0.0) v += beta * C[gr * ldc + gc];
-          C[gr * ldc + gc] = v;
-        }
-      }
-}
+typedef spx_mfma::Config<float, 256, 256, 16, 4, 4, 8> GemmF32Big;
+typedef spx_mfma::Config<float, 128, 128, 16, 2, 2, 8> GemmF32Small;
+typedef spx_mfma::Config<double, 128, 128, 16, 4, 4, 0> GemmF64;
 
 // integer GEMM (exact, wrap-around like NumPy's int matmul): 16x16 output
 // tile per 256-thread block, K staged through LDS.  Used for integer dot
@@ -749,32 +538,25 @@ extern "C" int spx_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* 
     LAUNCH_CHECK("spx_gemm(int)");
     return SPX_OK;
   }
+  hipError_t e;
   if (dtype == SPX_F32) {
-    i64 tm = (M + G32_BM - 1) / G32_BM, tn = (N + G32_BN - 1) / G32_BN;
-    if (tm * tn > 0x7fffffffLL) return set_err(SPX_EINVAL, "spx_gemm: too many tiles");
-    bool aligned = (M % G32_BM == 0) && (N % G32_BN == 0) && (K % G32_BK == 0) && (lda % 4 == 0) &&
-                   (ldb % 4 == 0) && ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0);
-    int nt = (int)(tm * tn);
-    if (aligned)
-      k_gemm_f32<true><<<nt, 256, 0, S(stream)>>>(M, N, K, (const float*)A, lda, (const float*)B, ldb,
-                                                  (float*)C, ldc, (float)alpha, (float)beta, (int)tn, nt);
-    else
-      k_gemm_f32<false><<<nt, 256, 0, S(stream)>>>(M, N, K, (const float*)A, lda, (const float*)B, ldb,
-                                                   (float*)C, ldc, (float)alpha, (float)beta, (int)tn, nt);
-    LAUNCH_CHECK("spx_gemm(f32)");
+    const float *a = (const float*)A, *b = (const float*)B;
+    i64 big_tiles = ((M + 255) / 256) * ((N + 255) / 256);
+    if (big_tiles >= 512) {
+      if (big_tiles > 0x7fffffffLL) return set_err(SPX_EINVAL, "spx_gemm: too many tiles");
+      e = GemmF32Big::launch(M, N, K, a, lda, b, ldb, (float*)C, ldc, (float)alpha, (float)beta,
+                             GemmF32Big::is_aligned(M, N, K, A, lda, B, ldb), S(stream));
+    } else {
+      e = GemmF32Small::launch(M, N, K, a, lda, b, ldb, (float*)C, ldc, (float)alpha, (float)beta,
+                               GemmF32Small::is_aligned(M, N, K, A, lda, B, ldb), S(stream));
+    }
+    if (e != hipSuccess) return set_err(SPX_EHIP, "spx_gemm(f32) launch failed: %s", hipGetErrorString(e));
   } else {
-    i64 tm = (M + G64_BM - 1) / G64_BM, tn = (N + G64_BN - 1) / G64_BN;
-    if (tm * tn > 0x7fffffffLL) return set_err(SPX_EINVAL, "spx_gemm: too many tiles");
-    bool aligned = (M % G64_BM == 0) && (N % G64_BN == 0) && (K % G64_BK == 0) && (lda % 2 == 0) &&
-                   (ldb % 2 == 0) && ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0);
-    int nt = (int)(tm * tn);
-    if (aligned)
-      k_gemm_f64<true><<<nt, 256, 0, S(stream)>>>(M, N, K, (const double*)A, lda, (const double*)B, ldb,
-                                                  (double*)C, ldc, alpha, beta, (int)tn, nt);
-    else
-      k_gemm_f64<false><<<nt, 256, 0, S(stream)>>>(M, N, K, (const double*)A, lda, (const double*)B, ldb,
-                                                   (double*)C, ldc, alpha, beta, (int)tn, nt);
-    LAUNCH_CHECK("spx_gemm(f64)");
+    i64 tiles = ((M + 127) / 128) * ((N + 127) / 128);
+    if (tiles > 0x7fffffffLL) return set_err(SPX_EINVAL, "spx_gemm: too many tiles");
+    e = GemmF64::launch(M, N, K, (const double*)A, lda, (const double*)B, ldb, (double*)C, ldc, alpha, beta,
+                        GemmF64::is_aligned(M, N, K, A, lda, B, ldb), S(stream));
+    if (e != hipSuccess) return set_err(SPX_EHIP, "spx_gemm(f64) launch failed: %s", hipGetErrorString(e));
   }
   return SPX_OK;
 }

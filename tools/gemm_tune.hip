@@ -1,0 +1,113 @@
+// Dev tool: time GEMM configurations of spartan_amd/csrc/gemm_kernels.h (the
+// product kernels) in one process, interleaved rounds (cdna_hip_programming.md
+// 5.4 rule 24), each checked against the first configuration of its dtype.
+//   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -o tools/bin/gemm_tune tools/gemm_tune.hip
+//   ./tools/bin/gemm_tune <size> <rounds> <f32|f64|both>
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../spartan_amd/csrc/gemm_kernels.h"
+
+using spx_mfma::Config;
+using spx_mfma::i64;
+
+#define CK(x)                                                         \
+  do {                                                                \
+    hipError_t e = (x);                                               \
+    if (e != hipSuccess) {                                            \
+      printf("%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+      exit(1);                                                        \
+    }                                                                 \
+  } while (0)
+
+template <typename T>
+struct Variant {
+  std::string name;
+  hipError_t (*launch)(i64, i64, i64, const T*, i64, const T*, i64, T*, i64, T, T, bool, hipStream_t);
+};
+
+#define V(T, BM, BN, BK, WM, WN, GM) \
+  Variant<T>{#BM "x" #BN "x" #BK " w" #WM "x" #WN " g" #GM, Config<T, BM, BN, BK, WM, WN, GM>::launch}
+
+template <typename T>
+__global__ void init(T* p, i64 n, unsigned seed) {
+  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
+    unsigned long long z = (i + 1) * 0x9E3779B97F4A7C15ULL + seed;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    p[i] = (T)((double)((z ^ (z >> 31)) >> 11) * 1.1102230246251565e-16);
+  }
+}
+
+template <typename T>
+void run(i64 S, int rounds, std::vector<Variant<T>> vs, double peak) {
+  T *A, *B, *C, *R;
+  size_t n = (size_t)S * S;
+  CK(hipMalloc(&A, n * sizeof(T)));
+  CK(hipMalloc(&B, n * sizeof(T)));
+  CK(hipMalloc(&C, n * sizeof(T)));
+  CK(hipMalloc(&R, n * sizeof(T)));
+  init<<<4096, 256>>>(A, (i64)n, 1);
+  init<<<4096, 256>>>(B, (i64)n, 2);
+  CK(vs[0].launch(S, S, S, A, S, B, S, R, S, (T)1, (T)0, true, 0));
+  CK(hipDeviceSynchronize());
+  std::vector<T> ref(64), got(64);
+  CK(hipMemcpy(ref.data(), R + 12345, 64 * sizeof(T), hipMemcpyDeviceToHost));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<std::vector<float>> ms(vs.size());
+  for (int r = 0; r < rounds; ++r)
+    for (size_t v = 0; v < vs.size(); ++v) {
+      CK(vs[v].launch(S, S, S, A, S, B, S, C, S, (T)1, (T)0, true, 0));
+      CK(hipEventRecord(e0));
+      CK(vs[v].launch(S, S, S, A, S, B, S, C, S, (T)1, (T)0, true, 0));
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float t;
+      CK(hipEventElapsedTime(&t, e0, e1));
+      ms[v].push_back(t);
+      CK(hipMemcpy(got.data(), C + 12345, 64 * sizeof(T), hipMemcpyDeviceToHost));
+      double err = 0;
+      for (int i = 0; i < 64; ++i) err = fmax(err, fabs((double)got[i] - (double)ref[i]) / fabs((double)ref[i]));
+      if (err > (sizeof(T) == 8 ? 1e-12 : 1e-5)) printf("  MISMATCH %s rel %g\n", vs[v].name.c_str(), err);
+    }
+  double fl = 2.0 * S * S * S;
+  for (size_t v = 0; v < vs.size(); ++v) {
+    float best = 1e30f;
+    for (float t : ms[v]) best = fminf(best, t);
+    printf("%s %-24s S=%lld best %9.3f ms %7.1f TF (%.1f%% of %.1f)\n", sizeof(T) == 8 ? "f64" : "f32",
+           vs[v].name.c_str(), (long long)S, best, fl / best / 1e9, fl / best / 1e9 / peak * 100, peak);
+  }
+  CK(hipFree(A));
+  CK(hipFree(B));
+  CK(hipFree(C));
+  CK(hipFree(R));
+}
+
+int main(int argc, char** argv) {
+  i64 S = argc > 1 ? atoll(argv[1]) : 8192;
+  int rounds = argc > 2 ? atoi(argv[2]) : 2;
+  std::string which = argc > 3 ? argv[3] : "both";
+  if (which != "f64") {
+    run<float>(S, rounds,
+               {V(float, 128, 128, 16, 2, 2, 0), V(float, 128, 128, 16, 2, 2, 8), V(float, 128, 128, 32, 2, 2, 8),
+                V(float, 256, 128, 16, 4, 2, 8), V(float, 128, 256, 16, 2, 4, 8), V(float, 256, 256, 16, 4, 4, 8),
+                V(float, 128, 128, 32, 4, 4, 8), V(float, 256, 128, 32, 4, 2, 8)},
+               157.3);
+  }
+  if (which != "f32") {
+    run<double>(S, rounds,
+                {V(double, 128, 128, 8, 2, 2, 0), V(double, 128, 128, 16, 4, 4, 8), V(double, 128, 128, 16, 4, 4, 0),
+                 V(double, 128, 128, 16, 2, 2, 8), V(double, 256, 128, 16, 4, 4, 8), V(double, 128, 256, 16, 4, 4, 8),
+                 V(double, 256, 256, 16, 4, 4, 8)},
+                78.6);
+  }
+  return 0;
+}
