@@ -317,7 +317,23 @@ class HipBackend:
         args.str[s][d] = vstr[k][d]
     args.dim[0], args.dim[1], args.dim[2] = O, R, I
     target_blocks = 2048
-    if I == 1:
+    if I == 1 and R <= 64 * V * 16:
+      # short segments: several per wave (LPR lanes each), grid-stride over O
+      kind = 'rowsp'
+      classes = [_cls(vstr[k][1]) for k in range(len(slots))]
+      vec_ok = V > 1 and R % V == 0 and all(
+          _aligned_ptr(inputs[s], V) and (vstr[k][0] % V == 0 if classes[k] == 'c' else True)
+          for k, s in enumerate(slots))
+      per = V if vec_ok else 1
+      need = -(-R // per)
+      lpr = 1
+      while lpr < need and lpr < 64:
+        lpr *= 2
+      seg_per_block = 4 * (64 // lpr)
+      P = 1
+      nblk = max(1, min(-(-O // seg_per_block), 256 * 16))
+      args.aux[0], args.aux[1], args.aux[2] = 1, R, lpr.bit_length() - 1
+    elif I == 1:
       kind = 'rows'
       classes = [_cls(vstr[k][1]) for k in range(len(slots))]
       vec_ok = V > 1 and R % V == 0 and all(

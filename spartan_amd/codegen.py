@@ -492,13 +492,15 @@ def _acc_update(op, j, val, idx_expr):
 
 
 def gen_reduce(root, inputs, classes, kind, op, vec):
-  """Fused map+reduce.  kind 'rows' (reduce over contiguous R of (O, R)) or
-  'cols' (reduce over R of (O, R, I), I contiguous).
+  """Fused map+reduce.  kind 'rows' (reduce over contiguous R of (O, R), one
+  or more blocks per segment), 'rowsp' (the same for short R: several
+  segments per wave, LPR lanes each, butterfly combine) or 'cols' (reduce over
+  R of (O, R, I), I contiguous).
 
   classes: per-input addressing class of the vectorised dimension (R for rows,
   I for cols): 'c', 'b' or 'g'.
   """
-  assert op in REDOPS and kind in ('rows', 'cols')
+  assert op in REDOPS and kind in ('rows', 'rowsp', 'cols')
   fn, ocml = _expr_fn(root, inputs)
   adt = acc_dtype(op, root.dtype)
   act = ctype(adt)
@@ -584,6 +586,59 @@ def gen_reduce(root, inputs, classes, kind, op, vec):
       L.append('    ((GLOBAL i64*)a.out1)[p * O + o] = si[0];')
     L.append('  }')
     L.append('}')
+  elif kind == 'rowsp':
+    def body(V):
+      b = []
+      b.append('if (o < O) {')
+      b.append('  for (i64 r = cl * %d; r < R; r += LPR * %d) {' % (V, V))
+      b += ['    ' + x for x in loads(V, lambda s: 'o * a.str[%d][0] + r * a.str[%d][1]' % (s, s), 1)]
+      for j in range(V):
+        b.append('    ' + _acc_update(op, j, val_j(j), gidx('r + %d' % j)))
+      b.append('  }')
+      b.append('}')
+      return b
+
+    L.append(SHFL)
+    L.append('KERN void spx_reduce(KArgs a) {')
+    L.append('  const i64 O = a.dim[0], R = a.dim[1];')
+    L.append('  const i64 lpr_log = a.aux[2], LPR = (i64)1 << lpr_log, SPW = 64 >> lpr_log;')
+    L.append('  const u32 t = tid(); const i64 lane = t & 63, w = t >> 6;')
+    L.append('  const i64 sub = lane >> lpr_log, cl = lane & (LPR - 1);')
+    L.append('  const i64 step = (i64)a.grid * 4 * SPW;')
+    L.append('  for (i64 sb = (i64)bidx() * 4 * SPW; sb < O; sb += step) {')
+    L.append('    const i64 o = sb + w * SPW + sub;')
+    for j in range(vec):
+      L.append('    %s acc%d = %s;' % (act, j, _ident(op, adt)))
+      if arg:
+        L.append('    i64 acci%d = 0x7fffffffffffffffLL;' % j)
+    L.append('    if (a.flags & 1) {')
+    L += ['      ' + x for x in body(vec)]
+    L.append('    } else {')
+    L += ['      ' + x for x in body(1)]
+    L.append('    }')
+    L.append('    %s accv = acc0;' % act)
+    if arg:
+      L.append('    i64 acci = acci0;')
+    for j in range(1, vec):
+      if arg:
+        L.append('    if (better(acc%d, acci%d, accv, acci)) { accv = acc%d; acci = acci%d; }' % (j, j, j, j))
+      else:
+        L.append('    accv = comb(accv, acc%d);' % j)
+    L.append('    for (i64 m = 1; m < LPR; m <<= 1) {')
+    L.append('      %s ov = shfl_xor(accv, (int)m);' % act)
+    if arg:
+      L.append('      i64 oi = shfl_xor(acci, (int)m);')
+      L.append('      if (better(ov, oi, accv, acci)) { accv = ov; acci = oi; }')
+    else:
+      L.append('      accv = (cl & m) ? comb(ov, accv) : comb(accv, ov);')
+    L.append('    }')
+    L.append('    if (cl == 0 && o < O) {')
+    L.append('      ((GLOBAL %s*)a.out0)[o] = accv;' % act)
+    if arg:
+      L.append('      ((GLOBAL i64*)a.out1)[o] = acci;')
+    L.append('    }')
+    L.append('  }')
+    L.append('}')
   else:
     def body(V):
       b = []
@@ -649,6 +704,25 @@ def gen_reduce(root, inputs, classes, kind, op, vec):
     L.append('  }')
     L.append('}')
   return '\n'.join(L)
+
+
+SHFL = r'''
+DEV u32 shfl_u32(u32 v, int m) {
+  const int lane = (int)(tid() & 63);
+  return (u32)__builtin_amdgcn_ds_bpermute((lane ^ m) << 2, (int)v);
+}
+template <typename T> DEV T shfl_xor(T v, int m) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "shfl size");
+  if constexpr (sizeof(T) == 4) {
+    u32 u = __builtin_bit_cast(u32, v);
+    return __builtin_bit_cast(T, shfl_u32(u, m));
+  } else {
+    u64 u = __builtin_bit_cast(u64, v);
+    u32 lo = shfl_u32((u32)u, m), hi = shfl_u32((u32)(u >> 32), m);
+    return __builtin_bit_cast(T, ((u64)hi << 32) | lo);
+  }
+}
+'''
 
 
 def vec_width(dtypes):

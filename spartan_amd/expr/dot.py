@@ -116,6 +116,32 @@ def _as_dtype(t, dt):
   return out
 
 
+SKINNY_N = 4
+
+
+def _skinny(at, bk, dtype):
+  """A (R, K) @ B (K, n) for n <= 4: per column, a generated fused
+  multiply + row-sum (packed-rows reduce), which streams A at HBM rate instead
+  of padding an MFMA tile to 128 columns."""
+  import torch
+  from .. import codegen
+  R, K = at.shape
+  n = bk.shape[1]
+  dt = np.dtype(dtype)
+  root = codegen.Op('multiply', [codegen.In(0, dt), codegen.In(1, dt)])
+  be = backend.get()
+  cols = []
+  for j in range(n):
+    bj = bk[:, j].contiguous().reshape(1, K)
+    cols.append(be.reduce(root, 'sum', {0: at, 1: bj}, (R, K), 1, (R,), dt))
+  if n == 1:
+    return cols[0].reshape(R, 1)
+  out = torch.empty((R, n), dtype=backend.torch_dtype(dt), device=at.device)
+  for j, c in enumerate(cols):
+    be.copy_region(out, (0, j), c.reshape(R, 1), (0, 0), (R, 1))
+  return out
+
+
 def run_dot(a, b, tile_hint=None):
   import torch
   ctx = runtime.get()
@@ -135,9 +161,12 @@ def run_dot(a, b, tile_hint=None):
         continue
       at = _as_dtype(a.fetch(A.to_base(ex2)).reshape(ex2.shape), dtype)
       bk = Bd[ex2.ul[1]:ex2.lr[1]]
-      ct = torch.empty((ex2.shape[0], N), dtype=backend.torch_dtype(dtype), device=ctx.device)
-      be.gemm(at, bk.contiguous(), ct, 1.0, 0.0)
-      partials[ex2] = ct
+      if N <= SKINNY_N and np.dtype(dtype).kind == 'f':
+        partials[ex2] = _skinny(at, bk, dtype)
+      else:
+        ct = torch.empty((ex2.shape[0], N), dtype=backend.torch_dtype(dtype), device=ctx.device)
+        be.gemm(at, bk.contiguous(), ct, 1.0, 0.0)
+        partials[ex2] = ct
     return _combine_rows(partials, A, M, N, out_shape, dtype, tile_hint, k_split=any(
         ex.ul[1] != 0 or ex.lr[1] != K for ex in A.tiles2()))
   btiles = B.tiles2() if not b.replicated else {ext.from_shape((K, N)): -1}

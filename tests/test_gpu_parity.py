@@ -334,3 +334,50 @@ def test_full_size_checksums(ex):
            + np.exp(rng.uniform_values(g, 13, -1.0, 1.0, np.float32)))
     check_fp(s1[r:r + 1].astype(np.float32), np.array([row.sum()], np.float32),
              np.array([row.astype(np.float64).sum()]), 1e-5)
+
+
+# ------------------------------------------------------ cfg5: lreg gradient
+@pytest.mark.parametrize('W', [1, 3])
+def test_lreg_cfg5_small(ex, W):
+  from oracle import workloads as OW
+  from spartan_amd import workloads
+  expr, setw = ex
+  setw(W)
+  n, d = 10000, 64
+  X = rng.rand((n, d), 41, np.float32)
+  Yv = rng.rand((n, 1), 42, np.float32)
+  w = rng.rand((d, 1), 43, np.float32)
+  x = expr.rand(n, d, dtype=np.float32, seed=41)
+  y = expr.rand(n, 1, dtype=np.float32, seed=42)
+  alpha = 1e-6
+  got = workloads.linear_regression_update(x, y, w, alpha)
+  want = OW.linear_regression_update(X, Yv, w, alpha, W)
+  # the update differs from the CPU one by alpha * (gradient difference): bound it
+  # by the gradient tolerance (1e-5 relative) -- the gradient is checked below
+  gmax = np.abs((X.astype(np.float64) * (X.astype(np.float64) @ w - Yv)).sum(0)).max()
+  np.testing.assert_allclose(got, want, rtol=0, atol=alpha * 1e-5 * gmax + 1e-7)
+  # gradient itself (not damped by alpha): vs fp64 exact and the CPU path
+  yp = expr.dot(x, w).glom()
+  np.testing.assert_allclose(yp, X @ w, rtol=2e-6)
+  g = expr.sum(x * (expr.dot(x, w) - y), axis=0).optimized().glom()
+  exact = (X.astype(np.float64) * (X.astype(np.float64) @ w.astype(np.float64) - Yv)).sum(0)
+  cpu = (X * (X @ w - Yv)).sum(0)
+  check_fp(g, cpu, exact, 1e-5)
+
+
+# ---------------------------------------------- short rows (packed kernel)
+@pytest.mark.parametrize('R', [1, 3, 64, 77, 256, 1000, 4096, 5000])
+def test_short_rows(ex, R):
+  expr, setw = ex
+  setw(2)
+  n = 300
+  a = rng.rand((n, R), 5, np.float64) - 0.5
+  x = expr.from_numpy(a)
+  np.testing.assert_allclose(x.sum(1).glom(), a.sum(1), rtol=1e-12, atol=1e-12)
+  np.testing.assert_array_equal(x.argmin(1).glom(), a.argmin(1))
+  np.testing.assert_array_equal(x.argmax(1).glom(), a.argmax(1))
+  np.testing.assert_array_equal(expr.max(x, 1).glom(), a.max(1))
+  f = a.astype(np.float32)
+  xf = expr.from_numpy(f)
+  np.testing.assert_array_equal(xf.argmin(1).glom(), f.argmin(1))
+  np.testing.assert_allclose(expr.sum(xf * xf, axis=1).optimized().glom(), (f * f).sum(1), rtol=1e-5)

@@ -122,3 +122,18 @@ def test_dot_paths(host_ctx):
     np.testing.assert_allclose(got, a @ b, rtol=1e-12)
     v = rng.rand((30,), 3, np.float64)
     np.testing.assert_allclose(expr.dot(expr.from_numpy(a), expr.from_numpy(v)).glom(), a @ v, rtol=1e-12)
+
+
+def test_lreg_update_matches_oracle(host_ctx):
+  from oracle import workloads as OW
+  for W in (1, 3):
+    host_ctx(W)
+    from spartan_amd import expr, workloads
+    n, d = 200, 8
+    X = rng.rand((n, d), 41, np.float32)
+    Yv = rng.rand((n, 1), 42, np.float32)
+    w = rng.rand((d, 1), 43, np.float32)
+    x, y = expr.from_numpy(X), expr.from_numpy(Yv)
+    got = workloads.linear_regression_update(x, y, w, 1e-3)
+    want = OW.linear_regression_update(X, Yv, w, 1e-3, W)
+    np.testing.assert_allclose(got, want, rtol=1e-5)
