@@ -42,6 +42,9 @@ def main():
   ap.add_argument('--cpu-baseline', type=int, default=1)
   ap.add_argument('--cpu-rows', type=int, default=4096)
   ap.add_argument('--strong', action='store_true', help='fixed 2^30 global array (strong scaling)')
+  ap.add_argument('--workloads', type=int, default=1, help='also time k-means (cfg3) and lreg (cfg5)')
+  ap.add_argument('--km-points', type=int, default=100000000)
+  ap.add_argument('--lreg-points', type=int, default=100000000)
   args = ap.parse_args()
 
   import torch
@@ -138,6 +141,10 @@ def main():
   if args.dot:
     result['dot'] = bench_dot(args.dot_size, ctx, be, expr, comm, sync)
 
+  if args.workloads:
+    result['kmeans'] = bench_kmeans(args.km_points, ctx, expr, comm, sync)
+    result['lreg'] = bench_lreg(args.lreg_points, ctx, expr, comm, sync)
+
   if args.cpu_baseline and N == 1 and ctx.rank == 0:
     from oracle.cpu_baseline import cfg2_cpu_baseline
     cb = cfg2_cpu_baseline(rows=min(args.cpu_rows, S), cols=S)
@@ -172,6 +179,58 @@ def bench_dot(S, ctx, be, expr, comm, sync):
     del a, b, A, B, c
     torch.cuda.empty_cache()
   out['config'] = 'dot(A, B), A, B ~ U[0,1) (%d, %d), K-split over ranks' % (S, S)
+  return out
+
+
+def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
+  """configs[2]: one k-means iteration (exact-order fp64 assign + fp64
+  centroid accumulation + all-reduce) over npts x 128 fp32 points, k=256."""
+  import torch
+  from spartan_amd import workloads
+  X = expr.rand(npts * ctx.world_size, D, dtype=np.float32, seed=21).force()
+  workloads.kmeans_fit(X, K, 1)          # warm-up + initial centres = first K points
+  sync()
+  comm.barrier()
+  t0 = time.perf_counter()
+  c, labels = workloads.kmeans_fit(X, K, iters)
+  sync()
+  comm.barrier()
+  el = comm.max_over_ranks(time.perf_counter() - t0) / iters
+  n = npts * ctx.world_size
+  out = {'ms_per_iter': round(el * 1e3, 3), 'points_per_s': round(n / el, 1),
+         'gemm_form_tflops': round(2.0 * n * K * D / el / 1e12, 2),
+         'fp64_valu_frac_per_gpu': round(3.0 * n * K * D / el / 1e12 / (78.6 / 2 * ctx.world_size), 4),
+         'config': 'cfg3: %d x %d fp32 points (U[0,1), seed 21) per GPU, k=%d, centres = first %d points, '
+                   'exact-order fp64 assign (bit-exact labels)' % (npts, D, K, K)}
+  del X, labels
+  torch.cuda.empty_cache()
+  return out
+
+
+def bench_lreg(npts, ctx, expr, comm, sync, D=64, iters=5):
+  """configs[4]: linear-regression gradient step X^T(Xw - y) + all-reduce."""
+  import torch
+  from spartan_amd import workloads
+  X = expr.rand(npts * ctx.world_size, D, dtype=np.float32, seed=41).force()
+  Y = expr.rand(npts * ctx.world_size, 1, dtype=np.float32, seed=42).force()
+  w = np.random.default_rng(43).random((D, 1)).astype(np.float32)
+  Xe, Ye = expr.lazify(X), expr.lazify(Y)
+  workloads.linear_regression_update(Xe, Ye, w, 1e-6)
+  sync()
+  comm.barrier()
+  t0 = time.perf_counter()
+  workloads.sgd_train(Xe, Ye, w, 1e-6, iters)
+  sync()
+  comm.barrier()
+  el = comm.max_over_ranks(time.perf_counter() - t0) / iters
+  n = npts * ctx.world_size
+  nbytes = 2 * (4.0 * n * D) + 3 * 4.0 * n   # GEMV reads X, fused reduce reads X + yp + y; yp written
+  out = {'ms_per_iter': round(el * 1e3, 3), 'algorithmic_GBps': round(nbytes / el / 1e9, 1),
+         'single_pass_bytes_GBps': round((4.0 * n * D + 4.0 * n) / el / 1e9, 1),
+         'config': 'cfg5: X %d x %d fp32, y %d x 1, w 64 x 1 host; dot (GEMV) + fused x*(yp-y) sum axis 0 '
+                   '+ all-reduce; two passes over X' % (n, D, n)}
+  del X, Y, Xe, Ye
+  torch.cuda.empty_cache()
   return out
 
 

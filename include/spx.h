@@ -147,6 +147,27 @@ int spx_argreduce_combine(int op, int dtype, const void* vals, const int64_t* id
                           int64_t R, int64_t n, void* out_val, int64_t* out_idx,
                           void* stream);
 
+/* ---------------------------------------------------------------- k-means
+ * Assignment step of KMeans.fit (spartan/examples/sklearn/cluster/k_means_.py:
+ * 126-128): labels[p] = first argmin over c of cdist(P[p], C[c]) computed
+ * exactly as scipy's fp64 euclidean cdist (sequential sum of squared
+ * differences, separately rounded, then sqrt) -> bit-exact labels.  points
+ * F32/F64 (N, D) with row stride ldp; centers fp64 (K, D); mindist optional.
+ */
+int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
+                      const double* centers, int64_t* labels, double* mindist, void* stream);
+/* Per-centre sums (fp64, K x D) and counts (K) of the points carrying each
+ * label (labels outside [0, K) are skipped), ADDED into sums/counts (which are
+ * overwritten instead when zero_first != 0): replaces kmeans_center_mapper /
+ * kmeans_count_mapper (k_means_.py:61-89).  No float atomics: per-block fp64
+ * partials go to the caller's workspace and are summed in a fixed order, so
+ * the result is deterministic.  workspace_bytes must be at least
+ * spx_kmeans_accumulate_workspace(dtype, N, D, K) (< 0 on bad arguments). */
+int64_t spx_kmeans_accumulate_workspace(int dtype, int64_t N, int64_t D, int64_t K);
+int spx_kmeans_accumulate(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
+                          const int64_t* labels, double* sums, uint64_t* counts, int zero_first,
+                          void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -395,5 +395,11 @@ def glom(array):
 
 
 def glom_region(array, region):
-  full = glom(array)
-  return full[region.to_slice()] if region.ndim else full
+  """Collective: ``region`` of ``array`` as a NumPy array on every rank; only
+  the region's bytes move (one gather_regions exchange + one D2H copy)."""
+  if isinstance(array, LocalWrapper) or region.ndim == 0:
+    full = glom(array)
+    return full[region.to_slice()] if region.ndim else full
+  ctx = runtime.get()
+  got = gather_regions(array, [(region, r) for r in range(ctx.world_size)])
+  return got[ctx.rank].cpu().numpy().reshape(region.shape)

@@ -84,6 +84,14 @@ _SIGS = {
                   ctypes.c_double, ctypes.c_double, ctypes.c_void_p], ctypes.c_int),
     'spx_argreduce_combine': ([ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    'spx_kmeans_assign': ([ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                           ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
+                          ctypes.c_int),
+    'spx_kmeans_accumulate_workspace': ([ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64],
+                                         ctypes.c_int64),
+    'spx_kmeans_accumulate': ([ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                               ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                               ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p], ctypes.c_int),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -445,6 +453,47 @@ class HipBackend:
     _check(self.lib.spx_gemm(spx_dtype(dt), M, N, K, ctypes.c_void_p(A.data_ptr()), A.stride(0),
                              ctypes.c_void_p(B.data_ptr()), B.stride(0), ctypes.c_void_p(C.data_ptr()),
                              C.stride(0), float(alpha), float(beta), self.stream()), 'spx_gemm')
+
+
+  # --------------------------------------------------------------- k-means
+  def kmeans_assign(self, points, centers, labels, mindist=None):
+    """labels[p] = first argmin_c cdist(points[p], centers[c]) (exact fp64 order)."""
+    N, D = points.shape
+    K = centers.shape[0]
+    assert centers.dtype == self._f64() and tuple(centers.shape) == (K, D) and labels.shape[0] == N
+    _check(self.lib.spx_kmeans_assign(spx_dtype(np_dtype(points.dtype)), N, D, K,
+                                      ctypes.c_void_p(points.data_ptr()), points.stride(0),
+                                      ctypes.c_void_p(centers.data_ptr()), ctypes.c_void_p(labels.data_ptr()),
+                                      ctypes.c_void_p(mindist.data_ptr() if mindist is not None else 0),
+                                      self.stream()), 'spx_kmeans_assign')
+
+  def kmeans_accumulate(self, points, labels, sums, counts, zero_first=True):
+    N, D = points.shape
+    K = sums.shape[0]
+    dt = spx_dtype(np_dtype(points.dtype))
+    need = self.lib.spx_kmeans_accumulate_workspace(dt, N, D, K)
+    if need < 0:
+      raise RuntimeError('spx_kmeans_accumulate_workspace: bad arguments')
+    ws = self._workspace(max(int(need), 8), points.device)
+    _check(self.lib.spx_kmeans_accumulate(dt, N, D, K, ctypes.c_void_p(points.data_ptr()), points.stride(0),
+                                          ctypes.c_void_p(labels.data_ptr()), ctypes.c_void_p(sums.data_ptr()),
+                                          ctypes.c_void_p(counts.data_ptr()), 1 if zero_first else 0,
+                                          ctypes.c_void_p(ws.data_ptr()), ws.numel(), self.stream()),
+           'spx_kmeans_accumulate')
+
+  def _workspace(self, nbytes, device):
+    """Grow-only scratch buffer on ``device`` (reuse is stream-ordered)."""
+    import torch
+    ws = getattr(self, '_ws', None)
+    if ws is None or ws.numel() < nbytes or ws.device != device:
+      ws = torch.empty((nbytes,), dtype=torch.uint8, device=device)
+      self._ws = ws
+    return ws
+
+  @staticmethod
+  def _f64():
+    import torch
+    return torch.float64
 
 
 def out_device(inputs, slots):

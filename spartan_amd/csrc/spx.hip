@@ -561,6 +561,296 @@ extern "C" int spx_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* 
   return SPX_OK;
 }
 
+// ================================================================ k-means
+// Assignment: labels[p] = argmin_c ||P[p] - C[c]||_2 in exactly the order of
+// scipy.spatial.distance.cdist (k_means_.py:58 via kmeans_dist_mapper): fp64,
+// s = sum_d (x_d - c_d)^2 accumulated sequentially over d with separately
+// rounded multiply and add (this file is compiled with -ffp-contract=off),
+// dist = sqrt(s); first index wins ties of the sqrt'd distances
+// (argmin(distances, axis=1), builtins.py:631-647).  Zero-padding the d loop
+// past D appends exact +0.0 terms, so chunking does not change a bit.
+// One point per lane; KM_CC centre accumulators live in registers while the
+// dims stream through KM_DC-wide register chunks; the centre tile is staged
+// in LDS and read as a broadcast.
+#define KM_CC 64
+#define KM_DC 16
+template <typename TP>
+__global__ __launch_bounds__(256) void k_kmeans_assign(i64 N, i64 D, i64 K, const TP* __restrict__ P, i64 ldp,
+                                                       const double* __restrict__ C, i64* __restrict__ labels,
+                                                       double* __restrict__ mind) {
+  __shared__ double Cs[KM_CC][KM_DC];
+  const i64 p = (i64)blockIdx.x * 256 + threadIdx.x;
+  const bool valid = p < N;
+  double best = 0.0;
+  i64 bi = -1;
+  for (i64 c0 = 0; c0 < K; c0 += KM_CC) {
+    double s[KM_CC];
+#pragma unroll
+    for (int cc = 0; cc < KM_CC; ++cc) s[cc] = 0.0;
+    for (i64 d0 = 0; d0 < D; d0 += KM_DC) {
+      __syncthreads();
+      for (int e = threadIdx.x; e < KM_CC * KM_DC; e += 256) {
+        int cc = e / KM_DC, dd = e % KM_DC;
+        Cs[cc][dd] = (c0 + cc < K && d0 + dd < D) ? C[(c0 + cc) * D + d0 + dd] : 0.0;
+      }
+      __syncthreads();
+      double x[KM_DC];
+#pragma unroll
+      for (int dd = 0; dd < KM_DC; ++dd) x[dd] = (valid && d0 + dd < D) ? (double)P[p * ldp + d0 + dd] : 0.0;
+#pragma unroll
+      for (int cc = 0; cc < KM_CC; ++cc) {
+        double acc = s[cc];
+#pragma unroll
+        for (int dd = 0; dd < KM_DC; ++dd) {
+          double df = x[dd] - Cs[cc][dd];
+          double sq = df * df;
+          acc = acc + sq;
+        }
+        s[cc] = acc;
+      }
+    }
+#pragma unroll
+    for (int cc = 0; cc < KM_CC; ++cc) {
+      if (c0 + cc < K) {
+        double dist = sqrt(s[cc]);
+        if (bi < 0 || dist < best || (dist != dist && best == best)) {
+          best = dist;
+          bi = c0 + cc;
+        }
+      }
+    }
+  }
+  if (valid) {
+    labels[p] = bi;
+    if (mind) mind[p] = best;
+  }
+}
+
+// Accumulation: sums[c][:] += P[p][:] and counts[c] += 1 for labels[p] == c,
+// replacing kmeans_center_mapper / kmeans_count_mapper (k_means_.py:61-89,
+// which sum in fp32; fp64 here is at least as exact).  No float atomics and a
+// fixed summation order, so the result is deterministic:
+//   k_kmeans_accum    persistent 1024-lane blocks; block (x, y) owns the
+//                     accumulator tile of CB centres x DB columns picked by y
+//                     and the point chunks x, x+G, x+2G, ...  Lane (cg, col)
+//                     keeps 32 fp64 accumulators in registers, for centres
+//                     cg, cg+NCG, ... of the tile.  Per chunk of CH points the
+//                     rows are prefetched into registers one chunk ahead,
+//                     staged in LDS, the labels are stable counting-sorted in
+//                     LDS, and each lane adds its centres' rows in point order.
+//                     The block's tile is written once to its partial slot.
+//   k_kmeans_reduce   out[i] (+)= sum over g = 0..G-1 of part[g][i], in order.
+constexpr int KA_THREADS = 1024;
+constexpr int KA_SLOTS = 32;
+constexpr int KA_CHUNK_BYTES = 32768;  // rows staged in LDS per chunk
+
+template <int DB>
+struct KaShape {
+  static constexpr int NCG = KA_THREADS / DB;  // centre groups per block
+  static constexpr int CB = KA_SLOTS * NCG;    // centres per accumulator tile
+};
+
+template <typename TP, int DB>
+__global__ __launch_bounds__(KA_THREADS) void k_kmeans_accum(i64 N, i64 D, i64 K, const TP* __restrict__ P, i64 ldp,
+                                                             const i64* __restrict__ labels, double* __restrict__ psum,
+                                                             unsigned long long* __restrict__ pcnt, int ndb) {
+  constexpr int NCG = KaShape<DB>::NCG, CB = KaShape<DB>::CB;
+  constexpr int CH = KA_CHUNK_BYTES / (DB * (int)sizeof(TP));  // points per chunk
+  constexpr int PF = CH * DB / KA_THREADS;            // prefetched elements per lane
+  static_assert(CH <= KA_THREADS && CB <= KA_THREADS, "chunk / tile larger than the block");
+  __shared__ TP xs[CH * DB];
+  __shared__ int lab_s[CH];
+  __shared__ unsigned short order[CH];
+  __shared__ unsigned int hist[CB], start[CB], cnt[CB];
+  __shared__ unsigned int wsum[KA_THREADS / 64];
+  const int t = threadIdx.x, lane = t & 63, col = t % DB, cg = t / DB;
+  const int cb = blockIdx.y / ndb, db = blockIdx.y % ndb;
+  const i64 c0 = (i64)cb * CB, d0 = (i64)db * DB;
+  const i64 nch = (N + CH - 1) / CH;
+  double acc[KA_SLOTS];
+#pragma unroll
+  for (int j = 0; j < KA_SLOTS; ++j) acc[j] = 0.0;
+  if (t < CB) cnt[t] = 0;
+  TP pf[PF];
+  int plab = -1;
+  auto load = [&](i64 ch) {
+    const i64 p0 = ch * CH;
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+      const int e = t + KA_THREADS * k, p = e / DB, d = e % DB;
+      pf[k] = (p0 + p < N && d0 + d < D) ? P[(p0 + p) * ldp + d0 + d] : TP(0);
+    }
+    if (t < CH) {
+      const i64 l = p0 + t < N ? labels[p0 + t] : -1;
+      plab = (l >= c0 && l < K && l - c0 < CB) ? (int)(l - c0) : -1;
+    }
+  };
+  i64 ch = blockIdx.x;
+  if (ch < nch) load(ch);
+  for (; ch < nch; ch += gridDim.x) {
+#pragma unroll
+    for (int k = 0; k < PF; ++k) xs[t + KA_THREADS * k] = pf[k];
+    if (t < CH) lab_s[t] = plab;
+    if (t < CB) hist[t] = 0;
+    __syncthreads();
+    if (ch + gridDim.x < nch) load(ch + gridDim.x);  // next chunk in flight during sort + sums
+    // stable rank of each point among the chunk's points with its label
+    int r = -1, rank = 0;
+    if (t < CH) {
+      r = lab_s[t];
+      if (r >= 0) {
+        for (int j = 0; j < t; ++j) rank += lab_s[j] == r;
+        atomicAdd(&hist[r], 1u);
+      }
+    }
+    __syncthreads();
+    // exclusive scan of hist -> start (wave scans + one scan of wave totals)
+    const unsigned int h = t < CB ? hist[t] : 0u;
+    unsigned int v = h;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned int u = __shfl_up(v, o, 64);
+      if (lane >= o) v += u;
+    }
+    if (lane == 63) wsum[t >> 6] = v;
+    __syncthreads();
+    if (t < 64) {
+      const unsigned int w = t < KA_THREADS / 64 ? wsum[t] : 0u;
+      unsigned int s2 = w;
+#pragma unroll
+      for (int o = 1; o < KA_THREADS / 64; o <<= 1) {
+        const unsigned int u = __shfl_up(s2, o, 64);
+        if (lane >= o) s2 += u;
+      }
+      if (t < KA_THREADS / 64) wsum[t] = s2 - w;
+    }
+    __syncthreads();
+    if (t < CB) {
+      start[t] = v - h + wsum[t >> 6];
+      cnt[t] += h;
+    }
+    __syncthreads();
+    if (r >= 0) order[start[r] + rank] = (unsigned short)t;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < KA_SLOTS; ++j) {
+      const int rel = cg + NCG * j;
+      const unsigned int b = start[rel], e = b + hist[rel];
+      double a = acc[j];
+      for (unsigned int q = b; q < e; ++q) a += (double)xs[order[q] * DB + col];
+      acc[j] = a;
+    }
+    __syncthreads();
+  }
+  const i64 g = blockIdx.x;
+#pragma unroll
+  for (int j = 0; j < KA_SLOTS; ++j) {
+    const i64 c = c0 + cg + NCG * j;
+    if (c < K && d0 + col < D) psum[(g * K + c) * D + d0 + col] = acc[j];
+  }
+  if (db == 0 && t < CB && c0 + t < K) pcnt[g * K + c0 + t] = cnt[t];
+}
+
+template <typename T>
+__global__ void k_kmeans_reduce(i64 n, i64 G, const T* __restrict__ part, T* __restrict__ out, int add) {
+  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
+    T s = add ? out[i] : T(0);
+    for (i64 g = 0; g < G; ++g) s += part[g * n + i];
+    out[i] = s;
+  }
+}
+
+static int ka_db(i64 D) { return D > 64 ? 128 : (D > 32 ? 64 : 32); }
+static int ka_cb(int db) { return KA_SLOTS * (KA_THREADS / db); }
+
+// Grid of the accumulation for (N, D, K): x = G point-chunk streams, y = tiles.
+static void ka_grid(int dtype, i64 N, i64 D, i64 K, i64* G, i64* ndb, i64* ncb) {
+  const int db = ka_db(D);
+  const i64 ch = KA_CHUNK_BYTES / (db * (dtype == SPX_F32 ? 4 : 8));
+  *ndb = (D + db - 1) / db;
+  *ncb = (K + ka_cb(db) - 1) / ka_cb(db);
+  const i64 nch = (N + ch - 1) / ch;
+  i64 g = 512 / (*ndb * *ncb);  // ~2 blocks per CU over all tiles
+  if (g < 1) g = 1;
+  if (g > nch) g = nch;
+  *G = g < 1 ? 1 : g;
+}
+
+extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
+                                 const double* centers, int64_t* labels, double* mindist, void* stream) {
+  if (dtype != SPX_F32 && dtype != SPX_F64) return set_err(SPX_ENOTSUP, "spx_kmeans_assign: points must be F32/F64");
+  if (N < 0 || D < 1 || K < 1 || ldp < D) return set_err(SPX_EINVAL, "spx_kmeans_assign: bad N/D/K/ldp");
+  if (N == 0) return SPX_OK;
+  if (!points || !centers || !labels) return set_err(SPX_EINVAL, "spx_kmeans_assign: null pointer");
+  i64 g = (N + 255) / 256;
+  if (g > 0x7fffffffLL) return set_err(SPX_EINVAL, "spx_kmeans_assign: too many points");
+  if (dtype == SPX_F32)
+    k_kmeans_assign<float><<<(unsigned)g, 256, 0, S(stream)>>>(N, D, K, (const float*)points, ldp, centers, labels,
+                                                                mindist);
+  else
+    k_kmeans_assign<double><<<(unsigned)g, 256, 0, S(stream)>>>(N, D, K, (const double*)points, ldp, centers, labels,
+                                                                 mindist);
+  LAUNCH_CHECK("spx_kmeans_assign");
+  return SPX_OK;
+}
+
+extern "C" int64_t spx_kmeans_accumulate_workspace(int dtype, int64_t N, int64_t D, int64_t K) {
+  if ((dtype != SPX_F32 && dtype != SPX_F64) || N < 0 || D < 1 || K < 1) return -1;
+  i64 G, ndb, ncb;
+  ka_grid(dtype, N, D, K, &G, &ndb, &ncb);
+  return G * K * D * (int64_t)sizeof(double) + G * K * (int64_t)sizeof(uint64_t);
+}
+
+extern "C" int spx_kmeans_accumulate(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
+                                     const int64_t* labels, double* sums, uint64_t* counts, int zero_first,
+                                     void* workspace, size_t workspace_bytes, void* stream) {
+  if (dtype != SPX_F32 && dtype != SPX_F64)
+    return set_err(SPX_ENOTSUP, "spx_kmeans_accumulate: points must be F32/F64");
+  if (N < 0 || D < 1 || K < 1 || ldp < D) return set_err(SPX_EINVAL, "spx_kmeans_accumulate: bad N/D/K/ldp");
+  if (!sums || !counts) return set_err(SPX_EINVAL, "spx_kmeans_accumulate: null pointer");
+  if (N == 0) {
+    if (zero_first) {
+      HIP_TRY(hipMemsetAsync(sums, 0, (size_t)K * D * sizeof(double), S(stream)));
+      HIP_TRY(hipMemsetAsync(counts, 0, (size_t)K * sizeof(uint64_t), S(stream)));
+    }
+    return SPX_OK;
+  }
+  if (!points || !labels || !workspace) return set_err(SPX_EINVAL, "spx_kmeans_accumulate: null pointer");
+  const int64_t need = spx_kmeans_accumulate_workspace(dtype, N, D, K);
+  if ((int64_t)workspace_bytes < need)
+    return set_err(SPX_EINVAL, "spx_kmeans_accumulate: workspace %zu < %lld bytes", workspace_bytes, (long long)need);
+  i64 G, ndb, ncb;
+  ka_grid(dtype, N, D, K, &G, &ndb, &ncb);
+  if (ndb * ncb > 65535) return set_err(SPX_ENOTSUP, "spx_kmeans_accumulate: K*D too large");
+  double* psum = (double*)workspace;
+  unsigned long long* pcnt = (unsigned long long*)(psum + G * K * D);
+  dim3 grid((unsigned)G, (unsigned)(ndb * ncb));
+  const int db = ka_db(D);
+#define KA_LAUNCH(TP, DBV)                                                                               \
+  k_kmeans_accum<TP, DBV><<<grid, KA_THREADS, 0, S(stream)>>>(N, D, K, (const TP*)points, ldp, labels, psum, \
+                                                              pcnt, (int)ndb)
+  if (dtype == SPX_F32) {
+    if (db == 128) KA_LAUNCH(float, 128);
+    else if (db == 64) KA_LAUNCH(float, 64);
+    else KA_LAUNCH(float, 32);
+  } else {
+    if (db == 128) KA_LAUNCH(double, 128);
+    else if (db == 64) KA_LAUNCH(double, 64);
+    else KA_LAUNCH(double, 32);
+  }
+#undef KA_LAUNCH
+  LAUNCH_CHECK("spx_kmeans_accumulate");
+  const int add = zero_first ? 0 : 1;
+  i64 n = K * D;
+  unsigned gb = (unsigned)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
+  k_kmeans_reduce<double><<<gb, 256, 0, S(stream)>>>(n, G, psum, sums, add);
+  LAUNCH_CHECK("spx_kmeans_accumulate(reduce sums)");
+  gb = (unsigned)((K + 255) / 256 < 2048 ? (K + 255) / 256 : 2048);
+  k_kmeans_reduce<unsigned long long><<<gb, 256, 0, S(stream)>>>(K, G, pcnt, (unsigned long long*)counts, add);
+  LAUNCH_CHECK("spx_kmeans_accumulate(reduce counts)");
+  return SPX_OK;
+}
+
 // ============================================================ JIT modules
 extern "C" int spx_module_load(const void* image, size_t nbytes, void** module_out) {
   if (!image || nbytes == 0 || !module_out) return set_err(SPX_EINVAL, "spx_module_load: bad args");

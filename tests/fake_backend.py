@@ -164,3 +164,19 @@ class FakeBackend:
     if beta != 0.0:
       r = r + beta * _np(C)
     C.copy_(torch.as_tensor(np.ascontiguousarray(r.astype(_np(C).dtype))))
+
+  def kmeans_assign(self, points, centers, labels, mindist=None):
+    from scipy.spatial.distance import cdist
+    d = cdist(_np(points).astype(np.float64), _np(centers))
+    labels.copy_(torch.as_tensor(d.argmin(1).astype(np.int64)))
+
+  def kmeans_accumulate(self, points, labels, sums, counts, zero_first=True):
+    p = _np(points).astype(np.float64)
+    lab = _np(labels)
+    K = sums.shape[0]
+    s = np.zeros((K, p.shape[1])) if zero_first else _np(sums).copy()
+    c = np.zeros(K, np.int64) if zero_first else _np(counts).copy()
+    np.add.at(s, lab, p)
+    np.add.at(c, lab, 1)
+    sums.copy_(torch.as_tensor(s))
+    counts.copy_(torch.as_tensor(c))

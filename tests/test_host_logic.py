@@ -137,3 +137,15 @@ def test_lreg_update_matches_oracle(host_ctx):
     got = workloads.linear_regression_update(x, y, w, 1e-3)
     want = OW.linear_regression_update(X, Yv, w, 1e-3, W)
     np.testing.assert_allclose(got, want, rtol=1e-5)
+
+
+def test_kmeans_driver_host(host_ctx):
+  from oracle import workloads as OW
+  for W in (1, 3):
+    host_ctx(W)
+    from spartan_amd import expr, workloads
+    pts = rng.rand((600, 8), 21, np.float32)
+    c, labels = workloads.kmeans_fit(expr.from_numpy(pts), 5, 3)
+    c2, l2 = OW.kmeans_fit(pts, 5, 3, W)
+    np.testing.assert_allclose(c, c2, rtol=1e-6)
+    np.testing.assert_array_equal(labels.glom(), l2)
