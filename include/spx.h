@@ -152,10 +152,18 @@ int spx_argreduce_combine(int op, int dtype, const void* vals, const int64_t* id
  * 126-128): labels[p] = first argmin over c of cdist(P[p], C[c]) computed
  * exactly as scipy's fp64 euclidean cdist (sequential sum of squared
  * differences, separately rounded, then sqrt) -> bit-exact labels.  points
- * F32/F64 (N, D) with row stride ldp; centers fp64 (K, D); mindist optional.
+ * F32/F64 (N, D) with row stride ldp; centers fp64 (K, D).
+ * With a workspace (>= spx_kmeans_assign_workspace(dtype, N, D, K) bytes) and
+ * mindist == NULL, an fp32 MFMA GEMM first certifies the points whose nearest
+ * centre is separated from the runner-up by more than a rigorous error bound;
+ * only the remaining points run the exact-order kernel.  The labels are the
+ * same bits either way.  With mindist != NULL (receives the fp64 distance)
+ * or workspace == NULL every point takes the exact-order kernel.
  */
+int64_t spx_kmeans_assign_workspace(int dtype, int64_t N, int64_t D, int64_t K);
 int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
-                      const double* centers, int64_t* labels, double* mindist, void* stream);
+                      const double* centers, int64_t* labels, double* mindist, void* workspace,
+                      size_t workspace_bytes, void* stream);
 /* Per-centre sums (fp64, K x D) and counts (K) of the points carrying each
  * label (labels outside [0, K) are skipped), ADDED into sums/counts (which are
  * overwritten instead when zero_first != 0): replaces kmeans_center_mapper /

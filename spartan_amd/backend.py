@@ -84,9 +84,11 @@ _SIGS = {
                   ctypes.c_double, ctypes.c_double, ctypes.c_void_p], ctypes.c_int),
     'spx_argreduce_combine': ([ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    'spx_kmeans_assign_workspace': ([ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64],
+                                     ctypes.c_int64),
     'spx_kmeans_assign': ([ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
-                           ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
-                          ctypes.c_int),
+                           ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                           ctypes.c_size_t, ctypes.c_void_p], ctypes.c_int),
     'spx_kmeans_accumulate_workspace': ([ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64],
                                          ctypes.c_int64),
     'spx_kmeans_accumulate': ([ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
@@ -456,15 +458,25 @@ class HipBackend:
 
 
   # --------------------------------------------------------------- k-means
-  def kmeans_assign(self, points, centers, labels, mindist=None):
-    """labels[p] = first argmin_c cdist(points[p], centers[c]) (exact fp64 order)."""
+  def kmeans_assign(self, points, centers, labels, mindist=None, exact_only=False):
+    """labels[p] = first argmin_c cdist(points[p], centers[c]) (exact fp64 order).
+    Default: MFMA-certified fast path + exact-order kernel for the undecided
+    points; exact_only=True (or mindist) runs every point exactly."""
     N, D = points.shape
     K = centers.shape[0]
     assert centers.dtype == self._f64() and tuple(centers.shape) == (K, D) and labels.shape[0] == N
-    _check(self.lib.spx_kmeans_assign(spx_dtype(np_dtype(points.dtype)), N, D, K,
-                                      ctypes.c_void_p(points.data_ptr()), points.stride(0),
+    dt = spx_dtype(np_dtype(points.dtype))
+    ws, nws = None, 0
+    if mindist is None and not exact_only and N > 0:
+      need = self.lib.spx_kmeans_assign_workspace(dt, N, D, K)
+      if need < 0:
+        raise RuntimeError('spx_kmeans_assign_workspace: bad arguments')
+      ws = self._workspace(int(need), points.device)
+      nws = ws.numel()
+    _check(self.lib.spx_kmeans_assign(dt, N, D, K, ctypes.c_void_p(points.data_ptr()), points.stride(0),
                                       ctypes.c_void_p(centers.data_ptr()), ctypes.c_void_p(labels.data_ptr()),
                                       ctypes.c_void_p(mindist.data_ptr() if mindist is not None else 0),
+                                      ctypes.c_void_p(ws.data_ptr() if ws is not None else 0), nws,
                                       self.stream()), 'spx_kmeans_assign')
 
   def kmeans_accumulate(self, points, labels, sums, counts, zero_first=True):

@@ -577,10 +577,16 @@ extern "C" int spx_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* 
 template <typename TP>
 __global__ __launch_bounds__(256) void k_kmeans_assign(i64 N, i64 D, i64 K, const TP* __restrict__ P, i64 ldp,
                                                        const double* __restrict__ C, i64* __restrict__ labels,
-                                                       double* __restrict__ mind) {
+                                                       double* __restrict__ mind, const i64* __restrict__ rows,
+                                                       const unsigned int* __restrict__ nrows) {
+  // rows != NULL: only the *nrows points rows[0..*nrows) (the filter's
+  // undecided points); the grid is sized for the worst case.
   __shared__ double Cs[KM_CC][KM_DC];
-  const i64 p = (i64)blockIdx.x * 256 + threadIdx.x;
-  const bool valid = p < N;
+  const i64 n = rows ? (i64)*nrows : N;
+  if ((i64)blockIdx.x * 256 >= n) return;  // block-uniform
+  const i64 q = (i64)blockIdx.x * 256 + threadIdx.x;
+  const bool valid = q < n;
+  const i64 p = valid ? (rows ? rows[q] : q) : 0;
   double best = 0.0;
   i64 bi = -1;
   for (i64 c0 = 0; c0 < K; c0 += KM_CC) {
@@ -626,171 +632,408 @@ __global__ __launch_bounds__(256) void k_kmeans_assign(i64 N, i64 D, i64 K, cons
   }
 }
 
+// Certified fast assignment.  Exact-order fp64 distances cost 3 fp64 VALU
+// ops per (point, centre, dim); instead an fp32 MFMA GEMM gives
+//   a'(p, c) = |c|^2 - 2 p.c   (= d^2(p, c) - |p|^2 up to rounding)
+// for every centre, and a point is labelled here only when its best and
+// second-best a' are separated by more than a rigorous bound on the error:
+//   |a' - a| <= 2 (D + 3) u32 |p| |c|  (fp32 fma-chain dot over D terms of
+//   fp32-rounded operands, u32 = 2^-24) + an absolute term for fp32
+//   underflow, and a relative slack 1e-8 (|p|^2 + max|c|^2) that dwarfs the
+//   fp64 rounding of scipy's sum and of the sqrt, so the certified winner is
+//   the strict, hence first-index, argmin of the exact-order distances.
+// Every other point (near-ties, non-finite values) is appended to a list and
+// labelled by k_kmeans_assign in exactly scipy's order.  The labels are thus
+// bit-identical to the all-exact kernel's.
+// Layout: block = 256 points x all centres (256-centre tiles), 16 waves of
+// v_mfma_f32_32x32x2_f32 (4 x 4, 64 x 64 each), BK = 16 with register-staged
+// double buffering as in gemm_kernels.h.  The epilogue transposes each
+// 128-row half of the S tile through LDS (stride 264: conflict-free both
+// ways) and 8 lanes per row scan 32 centres each for the top two, merged by
+// xor-shuffles.  |p| comes from the A tiles already in LDS.
+constexpr int KF_BM = 256, KF_BN = 256, KF_BK = 16, KF_THREADS = 1024;
+constexpr int KF_EP = 264;  // epilogue row stride (floats)
+
+__device__ __forceinline__ void kf_merge(double& b1, i64& i1, double& b2, double o1, i64 oi, double o2) {
+  if (o1 < b1 || (o1 == b1 && oi < i1)) {
+    b2 = b1 < o2 ? b1 : o2;
+    b1 = o1;
+    i1 = oi;
+  } else {
+    b2 = b2 < o1 ? b2 : o1;
+  }
+}
+
+template <typename TP, bool ALIGNED>
+__global__ __launch_bounds__(KF_THREADS) void k_kmeans_filter(i64 N, i64 D, i64 K, i64 Kp, const TP* __restrict__ P,
+                                                              i64 ldp, const float* __restrict__ CT,
+                                                              const double* __restrict__ cn, const double* cmax_p,
+                                                              i64* __restrict__ labels, unsigned int* __restrict__ nflag,
+                                                              i64* __restrict__ flagged) {
+  typedef spx_mfma::Mfma<float> F;
+  typedef float V __attribute__((ext_vector_type(4)));
+  constexpr int BM = KF_BM, BN = KF_BN, BK = KF_BK, NT = KF_THREADS, WN = 4;
+  constexpr int WTM = 64, WTN = 64, TM = 2, TN = 2;
+  constexpr int LA = BM * BK / 4 / NT, LB = BK * BN / 4 / NT;  // 1, 1
+  constexpr int MAIN_BYTES = (2 * BK * (BM + 2) + 2 * BK * BN) * 4;
+  constexpr int EPI_BYTES = 128 * KF_EP * 4;
+  static_assert(LA == 1 && LB == 1, "tiling");
+  __shared__ __attribute__((aligned(16))) unsigned char lds[MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES];
+  __shared__ float pnp[4][BM];
+  float(*As)[BK][BM + 2] = (float(*)[BK][BM + 2])lds;
+  float(*Bs)[BK][BN] = (float(*)[BK][BN])(lds + 2 * BK * (BM + 2) * 4);
+  float* E = (float*)lds;
+  const i64 row0 = (i64)blockIdx.x * BM;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w / WN, wn = w % WN;
+  const int rl = t >> 3, sub = t & 7;      // epilogue: row (of 128) and column phase
+  const int nm = t & (BM - 1), nq = t >> 8;  // row-norm: row and k quarter
+  float pn = 0.f;
+  double s1[TM], s2[TM];
+  i64 si[TM];
+  bool bad[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    s1[i] = INFINITY;
+    s2[i] = INFINITY;
+    si[i] = -1;
+    bad[i] = false;
+  }
+  V ra, rb;
+  for (i64 c0 = 0; c0 < Kp; c0 += BN) {
+    F::acc_t acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = F::zero();
+    auto load = [&](i64 k0) {
+      {
+        const int r = t / (BK / 4), kq = t % (BK / 4);
+        const i64 gr = row0 + r, gk = k0 + kq * 4;
+        if (ALIGNED && gr < N) {
+          ra = *(const V*)(P + gr * ldp + gk);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) ra[j] = (gr < N && gk + j < D) ? (float)P[gr * ldp + gk + j] : 0.f;
+        }
+      }
+      {
+        const int kr = t / (BN / 4), cq = t % (BN / 4);
+        const i64 bk = k0 + kr;
+        if (bk < D) rb = *(const V*)(CT + bk * Kp + c0 + cq * 4);
+        else rb = (V){0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    auto store = [&](int buf) {
+      const int r = t / (BK / 4), kq = t % (BK / 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) As[buf][kq * 4 + j][r] = ra[j];
+      const int kr = t / (BN / 4), cq = t % (BN / 4);
+      *(V*)(&Bs[buf][kr][cq * 4]) = rb;
+    };
+    const int nk = (int)((D + BK - 1) / BK);
+    __syncthreads();  // previous epilogue done with the shared buffer
+    load(0);
+    store(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) load((i64)(kt + 1) * BK);
+      if (c0 == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float v = As[cur][nq * 4 + k][nm];
+          pn += v * v;
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < BK / F::KS; ++kk) {
+        const int k = kk * F::KS + F::opk(lane);
+        float a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = As[cur][k][wm * WTM + i * F::TILE + F::opi(lane)];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = Bs[cur][k][wn * WTN + j * F::TILE + F::opi(lane)];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
+      }
+      if (kt + 1 < nk) store(cur ^ 1);
+      __syncthreads();
+    }
+    // epilogue: half i holds rows wm*64 + i*32 + [0, 32) of every wm
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      if (i) __syncthreads();
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < F::NREG; ++r)
+          E[(wm * 32 + F::crow(lane, r)) * KF_EP + wn * WTN + j * F::TILE + F::ccol(lane)] = acc[i][j][r];
+      __syncthreads();
+      double b1 = INFINITY, b2 = INFINITY;
+      i64 i1 = -1;
+      bool nf = false;
+#pragma unroll 8
+      for (int k = 0; k < BN / 8; ++k) {
+        const int col = sub + 8 * k;
+        const double a = cn[c0 + col] - 2.0 * (double)E[rl * KF_EP + col];
+        nf |= a != a;
+        if (a < b1) {
+          b2 = b1;
+          b1 = a;
+          i1 = c0 + col;
+        } else if (a < b2) {
+          b2 = a;
+        }
+      }
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) {
+        const double o1 = __shfl_xor(b1, o, 64), o2 = __shfl_xor(b2, o, 64);
+        const i64 oi = __shfl_xor(i1, o, 64);
+        nf |= __shfl_xor((int)nf, o, 64) != 0;
+        kf_merge(b1, i1, b2, o1, oi, o2);
+      }
+      kf_merge(s1[i], si[i], s2[i], b1, i1, b2);
+      bad[i] |= nf;
+    }
+    if (c0 == 0) pnp[nq][nm] = pn;
+  }
+  __syncthreads();
+  if (sub != 0) return;
+  const double cmax = *cmax_p;
+  const double u32 = 5.9604644775390625e-08;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int lr = (rl / 32) * WTM + i * 32 + (rl % 32);  // row within the block
+    const i64 row = row0 + lr;
+    if (row >= N) continue;
+    const double p2 = (double)pnp[0][lr] + (double)pnp[1][lr] + (double)pnp[2][lr] + (double)pnp[3][lr];
+    const double pnorm = sqrt(p2) * 1.001;
+    const double e = 2.0 * (double)(D + 3) * u32 * 1.01 * pnorm * cmax + 4.0 * (double)D * 1.2e-38 * (1.0 + cmax) +
+                     1e-8 * (p2 + cmax * cmax) + 1e-300;
+    const bool ok = !bad[i] && isfinite(s1[i]) && isfinite(pnorm) && isfinite(e) && s1[i] == s1[i] &&
+                    (s2[i] - s1[i] > 2.0 * e);
+    if (ok) {
+      labels[row] = si[i];
+    } else {
+      const unsigned int slot = atomicAdd(nflag, 1u);
+      flagged[slot] = row;
+    }
+  }
+}
+
+// CT[d][c] = (float)C[c][d] (zero-padded to Kp centres), cn[c] = |C[c]|^2 in
+// fp64 (+inf for padding), *cmax = max_c |C[c]| (one block).
+__global__ __launch_bounds__(256) void k_kmeans_prep(i64 D, i64 K, i64 Kp, const double* __restrict__ C,
+                                                     float* __restrict__ CT, double* __restrict__ cn,
+                                                     double* __restrict__ cmax) {
+  __shared__ double red[256];
+  double mx = 0.0;
+  for (i64 c = threadIdx.x; c < Kp; c += 256) {
+    double s = 0.0;
+    for (i64 d = 0; d < D; ++d) {
+      const double v = c < K ? C[c * D + d] : 0.0;
+      CT[d * Kp + c] = (float)v;
+      s += v * v;
+    }
+    cn[c] = c < K ? s : INFINITY;
+    if (c < K) mx = (s > mx || s != s) ? s : mx;
+  }
+  red[threadIdx.x] = mx;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      const double a = red[threadIdx.x], b = red[threadIdx.x + o];
+      red[threadIdx.x] = (b > a || b != b) ? b : a;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *cmax = sqrt(red[0]) * 1.001;
+}
+
 // Accumulation: sums[c][:] += P[p][:] and counts[c] += 1 for labels[p] == c,
 // replacing kmeans_center_mapper / kmeans_count_mapper (k_means_.py:61-89,
 // which sum in fp32; fp64 here is at least as exact).  No float atomics and a
 // fixed summation order, so the result is deterministic:
-//   k_kmeans_accum    persistent 1024-lane blocks; block (x, y) owns the
-//                     accumulator tile of CB centres x DB columns picked by y
-//                     and the point chunks x, x+G, x+2G, ...  Lane (cg, col)
-//                     keeps 32 fp64 accumulators in registers, for centres
-//                     cg, cg+NCG, ... of the tile.  Per chunk of CH points the
-//                     rows are prefetched into registers one chunk ahead,
-//                     staged in LDS, the labels are stable counting-sorted in
-//                     LDS, and each lane adds its centres' rows in point order.
-//                     The block's tile is written once to its partial slot.
-//   k_kmeans_reduce   out[i] (+)= sum over g = 0..G-1 of part[g][i], in order.
+//   k_kmeans_accum    persistent 1024-lane blocks; block (x, y) owns the fp64
+//                     accumulator tile of KA_CB centres x 64 columns picked by
+//                     y (128 KB of LDS) and the point chunks x, x+G, ...  Wave
+//                     w owns the centres c == w (mod 16) of the tile, lane =
+//                     column.  Each chunk of rows is prefetched into registers
+//                     one chunk ahead and staged in LDS; every wave ballots the
+//                     chunk's labels and adds its own points' rows, in point
+//                     order, with plain LDS read-modify-writes (one owner per
+//                     accumulator: no atomics).  The tile is written once to
+//                     the block's partial slot.
+//   k_kmeans_reduce   out[i] (+)= sum over g of part[g][i]: four fixed g
+//                     slices per output, combined in a fixed order.
 constexpr int KA_THREADS = 1024;
-constexpr int KA_SLOTS = 32;
-constexpr int KA_CHUNK_BYTES = 32768;  // rows staged in LDS per chunk
+constexpr int KA_DB = 64;                  // columns per tile = lanes per wave
+constexpr int KA_CB = 16384 / KA_DB;       // centres per tile (128 KB of fp64)
+constexpr int KA_WAVES = KA_THREADS / 64;  // centre owners per tile
 
-template <int DB>
-struct KaShape {
-  static constexpr int NCG = KA_THREADS / DB;  // centre groups per block
-  static constexpr int CB = KA_SLOTS * NCG;    // centres per accumulator tile
-};
-
-template <typename TP, int DB>
+template <typename TP>
 __global__ __launch_bounds__(KA_THREADS) void k_kmeans_accum(i64 N, i64 D, i64 K, const TP* __restrict__ P, i64 ldp,
                                                              const i64* __restrict__ labels, double* __restrict__ psum,
                                                              unsigned long long* __restrict__ pcnt, int ndb) {
-  constexpr int NCG = KaShape<DB>::NCG, CB = KaShape<DB>::CB;
-  constexpr int CH = KA_CHUNK_BYTES / (DB * (int)sizeof(TP));  // points per chunk
-  constexpr int PF = CH * DB / KA_THREADS;            // prefetched elements per lane
-  static_assert(CH <= KA_THREADS && CB <= KA_THREADS, "chunk / tile larger than the block");
-  __shared__ TP xs[CH * DB];
+  constexpr int CH = 16384 / (KA_DB * (int)sizeof(TP)) < 64 ? 16384 / (KA_DB * (int)sizeof(TP)) : 64;
+  constexpr int PF = CH * KA_DB / KA_THREADS;  // prefetched elements per lane
+  __shared__ double acc[KA_CB * KA_DB];
+  __shared__ TP xs[CH * KA_DB];
   __shared__ int lab_s[CH];
-  __shared__ unsigned short order[CH];
-  __shared__ unsigned int hist[CB], start[CB], cnt[CB];
-  __shared__ unsigned int wsum[KA_THREADS / 64];
-  const int t = threadIdx.x, lane = t & 63, col = t % DB, cg = t / DB;
+  __shared__ unsigned int cnt[KA_CB];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int cb = blockIdx.y / ndb, db = blockIdx.y % ndb;
-  const i64 c0 = (i64)cb * CB, d0 = (i64)db * DB;
+  const i64 c0 = (i64)cb * KA_CB, d0 = (i64)db * KA_DB;
   const i64 nch = (N + CH - 1) / CH;
-  double acc[KA_SLOTS];
-#pragma unroll
-  for (int j = 0; j < KA_SLOTS; ++j) acc[j] = 0.0;
-  if (t < CB) cnt[t] = 0;
+  for (int i = t; i < KA_CB * KA_DB; i += KA_THREADS) acc[i] = 0.0;
+  for (int i = t; i < KA_CB; i += KA_THREADS) cnt[i] = 0;
   TP pf[PF];
   int plab = -1;
   auto load = [&](i64 ch) {
     const i64 p0 = ch * CH;
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
-      const int e = t + KA_THREADS * k, p = e / DB, d = e % DB;
+      const int e = t + KA_THREADS * k, p = e / KA_DB, d = e % KA_DB;
       pf[k] = (p0 + p < N && d0 + d < D) ? P[(p0 + p) * ldp + d0 + d] : TP(0);
     }
     if (t < CH) {
       const i64 l = p0 + t < N ? labels[p0 + t] : -1;
-      plab = (l >= c0 && l < K && l - c0 < CB) ? (int)(l - c0) : -1;
+      plab = (l >= c0 && l < K && l - c0 < KA_CB) ? (int)(l - c0) : -1;
     }
   };
   i64 ch = blockIdx.x;
   if (ch < nch) load(ch);
   for (; ch < nch; ch += gridDim.x) {
+    __syncthreads();  // previous chunk fully consumed (and the zeroing done)
 #pragma unroll
     for (int k = 0; k < PF; ++k) xs[t + KA_THREADS * k] = pf[k];
     if (t < CH) lab_s[t] = plab;
-    if (t < CB) hist[t] = 0;
     __syncthreads();
-    if (ch + gridDim.x < nch) load(ch + gridDim.x);  // next chunk in flight during sort + sums
-    // stable rank of each point among the chunk's points with its label
-    int r = -1, rank = 0;
-    if (t < CH) {
-      r = lab_s[t];
-      if (r >= 0) {
-        for (int j = 0; j < t; ++j) rank += lab_s[j] == r;
-        atomicAdd(&hist[r], 1u);
-      }
+    if (ch + gridDim.x < nch) load(ch + gridDim.x);  // next chunk in flight
+    const int r = lane < CH ? lab_s[lane] : -1;
+    unsigned long long m = __ballot(r >= 0 && (r % KA_WAVES) == w);
+    while (m) {
+      const int p = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const int rr = __shfl(r, p, 64);
+      acc[rr * KA_DB + lane] += (double)xs[p * KA_DB + lane];
+      if (lane == 0) cnt[rr] += 1u;
     }
-    __syncthreads();
-    // exclusive scan of hist -> start (wave scans + one scan of wave totals)
-    const unsigned int h = t < CB ? hist[t] : 0u;
-    unsigned int v = h;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned int u = __shfl_up(v, o, 64);
-      if (lane >= o) v += u;
-    }
-    if (lane == 63) wsum[t >> 6] = v;
-    __syncthreads();
-    if (t < 64) {
-      const unsigned int w = t < KA_THREADS / 64 ? wsum[t] : 0u;
-      unsigned int s2 = w;
-#pragma unroll
-      for (int o = 1; o < KA_THREADS / 64; o <<= 1) {
-        const unsigned int u = __shfl_up(s2, o, 64);
-        if (lane >= o) s2 += u;
-      }
-      if (t < KA_THREADS / 64) wsum[t] = s2 - w;
-    }
-    __syncthreads();
-    if (t < CB) {
-      start[t] = v - h + wsum[t >> 6];
-      cnt[t] += h;
-    }
-    __syncthreads();
-    if (r >= 0) order[start[r] + rank] = (unsigned short)t;
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < KA_SLOTS; ++j) {
-      const int rel = cg + NCG * j;
-      const unsigned int b = start[rel], e = b + hist[rel];
-      double a = acc[j];
-      for (unsigned int q = b; q < e; ++q) a += (double)xs[order[q] * DB + col];
-      acc[j] = a;
-    }
-    __syncthreads();
   }
+  __syncthreads();
   const i64 g = blockIdx.x;
-#pragma unroll
-  for (int j = 0; j < KA_SLOTS; ++j) {
-    const i64 c = c0 + cg + NCG * j;
-    if (c < K && d0 + col < D) psum[(g * K + c) * D + d0 + col] = acc[j];
+  for (int i = t; i < KA_CB * KA_DB; i += KA_THREADS) {
+    const i64 c = c0 + i / KA_DB, d = d0 + i % KA_DB;
+    if (c < K && d < D) psum[(g * K + c) * D + d] = acc[i];
   }
-  if (db == 0 && t < CB && c0 + t < K) pcnt[g * K + c0 + t] = cnt[t];
+  if (db == 0)
+    for (int i = t; i < KA_CB; i += KA_THREADS)
+      if (c0 + i < K) pcnt[g * K + c0 + i] = cnt[i];
 }
 
+// 256 lanes = 64 outputs x 4 g-slices; slice s sums g = s, s+4, ... in order,
+// then the four slice sums are added in order 0..3 (deterministic).
 template <typename T>
-__global__ void k_kmeans_reduce(i64 n, i64 G, const T* __restrict__ part, T* __restrict__ out, int add) {
-  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
-    T s = add ? out[i] : T(0);
-    for (i64 g = 0; g < G; ++g) s += part[g * n + i];
-    out[i] = s;
+__global__ __launch_bounds__(256) void k_kmeans_reduce(i64 n, i64 G, const T* __restrict__ part, T* __restrict__ out,
+                                                       int add) {
+  __shared__ T red[4][64];
+  const int j = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const i64 i = (i64)blockIdx.x * 64 + j;
+  T s = T(0);
+  if (i < n)
+    for (i64 g = sl; g < G; g += 4) s += part[g * n + i];
+  red[sl][j] = s;
+  __syncthreads();
+  if (sl == 0 && i < n) {
+    T v = add ? out[i] : T(0);
+    v += red[0][j];
+    v += red[1][j];
+    v += red[2][j];
+    v += red[3][j];
+    out[i] = v;
   }
 }
-
-static int ka_db(i64 D) { return D > 64 ? 128 : (D > 32 ? 64 : 32); }
-static int ka_cb(int db) { return KA_SLOTS * (KA_THREADS / db); }
 
 // Grid of the accumulation for (N, D, K): x = G point-chunk streams, y = tiles.
 static void ka_grid(int dtype, i64 N, i64 D, i64 K, i64* G, i64* ndb, i64* ncb) {
-  const int db = ka_db(D);
-  const i64 ch = KA_CHUNK_BYTES / (db * (dtype == SPX_F32 ? 4 : 8));
-  *ndb = (D + db - 1) / db;
-  *ncb = (K + ka_cb(db) - 1) / ka_cb(db);
+  const i64 ch = dtype == SPX_F32 ? 64 : 32;
+  *ndb = (D + KA_DB - 1) / KA_DB;
+  *ncb = (K + KA_CB - 1) / KA_CB;
   const i64 nch = (N + ch - 1) / ch;
-  i64 g = 512 / (*ndb * *ncb);  // ~2 blocks per CU over all tiles
+  i64 g = 256 / (*ndb * *ncb);  // one block per CU over all tiles
   if (g < 1) g = 1;
   if (g > nch) g = nch;
   *G = g < 1 ? 1 : g;
 }
 
+static i64 kf_kp(i64 K) { return (K + KF_BN - 1) / KF_BN * KF_BN; }
+
+extern "C" int64_t spx_kmeans_assign_workspace(int dtype, int64_t N, int64_t D, int64_t K) {
+  if ((dtype != SPX_F32 && dtype != SPX_F64) || N < 0 || D < 1 || K < 1) return -1;
+  const i64 Kp = kf_kp(K);
+  // CT (D x Kp f32) | cn (Kp f64) | cmax | counter | flagged (N i64)
+  return (D * Kp * 4 + 15) / 16 * 16 + Kp * 8 + 16 + 16 + N * 8;
+}
+
 extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
-                                 const double* centers, int64_t* labels, double* mindist, void* stream) {
+                                 const double* centers, int64_t* labels, double* mindist, void* workspace,
+                                 size_t workspace_bytes, void* stream) {
   if (dtype != SPX_F32 && dtype != SPX_F64) return set_err(SPX_ENOTSUP, "spx_kmeans_assign: points must be F32/F64");
-  if (N < 0 || D < 1 || K < 1 || ldp < D) return set_err(SPX_EINVAL, "spx_kmeans_assign: bad N/D/K/ldp");
+  if (N < 0 || D < 1 || K < 1 || (N > 0 && ldp < D)) return set_err(SPX_EINVAL, "spx_kmeans_assign: bad N/D/K/ldp");
   if (N == 0) return SPX_OK;
   if (!points || !centers || !labels) return set_err(SPX_EINVAL, "spx_kmeans_assign: null pointer");
-  i64 g = (N + 255) / 256;
+  const i64 g = (N + 255) / 256;
   if (g > 0x7fffffffLL) return set_err(SPX_EINVAL, "spx_kmeans_assign: too many points");
+  if (mindist || !workspace) {  // all points through the exact-order kernel
+    if (dtype == SPX_F32)
+      k_kmeans_assign<float><<<(unsigned)g, 256, 0, S(stream)>>>(N, D, K, (const float*)points, ldp, centers, labels,
+                                                                  mindist, nullptr, nullptr);
+    else
+      k_kmeans_assign<double><<<(unsigned)g, 256, 0, S(stream)>>>(N, D, K, (const double*)points, ldp, centers,
+                                                                   labels, mindist, nullptr, nullptr);
+    LAUNCH_CHECK("spx_kmeans_assign");
+    return SPX_OK;
+  }
+  const int64_t need = spx_kmeans_assign_workspace(dtype, N, D, K);
+  if ((int64_t)workspace_bytes < need)
+    return set_err(SPX_EINVAL, "spx_kmeans_assign: workspace %zu < %lld bytes", workspace_bytes, (long long)need);
+  const i64 Kp = kf_kp(K);
+  unsigned char* ws = (unsigned char*)workspace;
+  float* CT = (float*)ws;
+  ws += (D * Kp * 4 + 15) / 16 * 16;
+  double* cn = (double*)ws;
+  ws += Kp * 8;
+  double* cmax = (double*)ws;
+  ws += 16;
+  unsigned int* nflag = (unsigned int*)ws;
+  ws += 16;
+  i64* flagged = (i64*)ws;
+  HIP_TRY(hipMemsetAsync(nflag, 0, sizeof(unsigned int), S(stream)));
+  k_kmeans_prep<<<1, 256, 0, S(stream)>>>(D, K, Kp, centers, CT, cn, cmax);
+  LAUNCH_CHECK("spx_kmeans_assign(prep)");
+  const i64 gf = (N + KF_BM - 1) / KF_BM;
+  const bool al = D % KF_BK == 0 && ldp % 4 == 0 && ((uintptr_t)points % 16) == 0;
+  if (dtype == SPX_F32) {
+    if (al)
+      k_kmeans_filter<float, true><<<(unsigned)gf, KF_THREADS, 0, S(stream)>>>(
+          N, D, K, Kp, (const float*)points, ldp, CT, cn, cmax, labels, nflag, flagged);
+    else
+      k_kmeans_filter<float, false><<<(unsigned)gf, KF_THREADS, 0, S(stream)>>>(
+          N, D, K, Kp, (const float*)points, ldp, CT, cn, cmax, labels, nflag, flagged);
+  } else {
+    k_kmeans_filter<double, false><<<(unsigned)gf, KF_THREADS, 0, S(stream)>>>(
+        N, D, K, Kp, (const double*)points, ldp, CT, cn, cmax, labels, nflag, flagged);
+  }
+  LAUNCH_CHECK("spx_kmeans_assign(filter)");
   if (dtype == SPX_F32)
     k_kmeans_assign<float><<<(unsigned)g, 256, 0, S(stream)>>>(N, D, K, (const float*)points, ldp, centers, labels,
-                                                                mindist);
+                                                                nullptr, flagged, nflag);
   else
     k_kmeans_assign<double><<<(unsigned)g, 256, 0, S(stream)>>>(N, D, K, (const double*)points, ldp, centers, labels,
-                                                                 mindist);
-  LAUNCH_CHECK("spx_kmeans_assign");
+                                                                 nullptr, flagged, nflag);
+  LAUNCH_CHECK("spx_kmeans_assign(exact)");
   return SPX_OK;
 }
 
@@ -806,7 +1049,7 @@ extern "C" int spx_kmeans_accumulate(int dtype, int64_t N, int64_t D, int64_t K,
                                      void* workspace, size_t workspace_bytes, void* stream) {
   if (dtype != SPX_F32 && dtype != SPX_F64)
     return set_err(SPX_ENOTSUP, "spx_kmeans_accumulate: points must be F32/F64");
-  if (N < 0 || D < 1 || K < 1 || ldp < D) return set_err(SPX_EINVAL, "spx_kmeans_accumulate: bad N/D/K/ldp");
+  if (N < 0 || D < 1 || K < 1 || (N > 0 && ldp < D)) return set_err(SPX_EINVAL, "spx_kmeans_accumulate: bad N/D/K/ldp");
   if (!sums || !counts) return set_err(SPX_EINVAL, "spx_kmeans_accumulate: null pointer");
   if (N == 0) {
     if (zero_first) {
@@ -825,28 +1068,19 @@ extern "C" int spx_kmeans_accumulate(int dtype, int64_t N, int64_t D, int64_t K,
   double* psum = (double*)workspace;
   unsigned long long* pcnt = (unsigned long long*)(psum + G * K * D);
   dim3 grid((unsigned)G, (unsigned)(ndb * ncb));
-  const int db = ka_db(D);
-#define KA_LAUNCH(TP, DBV)                                                                               \
-  k_kmeans_accum<TP, DBV><<<grid, KA_THREADS, 0, S(stream)>>>(N, D, K, (const TP*)points, ldp, labels, psum, \
-                                                              pcnt, (int)ndb)
-  if (dtype == SPX_F32) {
-    if (db == 128) KA_LAUNCH(float, 128);
-    else if (db == 64) KA_LAUNCH(float, 64);
-    else KA_LAUNCH(float, 32);
-  } else {
-    if (db == 128) KA_LAUNCH(double, 128);
-    else if (db == 64) KA_LAUNCH(double, 64);
-    else KA_LAUNCH(double, 32);
-  }
-#undef KA_LAUNCH
+  if (dtype == SPX_F32)
+    k_kmeans_accum<float><<<grid, KA_THREADS, 0, S(stream)>>>(N, D, K, (const float*)points, ldp, labels, psum, pcnt,
+                                                              (int)ndb);
+  else
+    k_kmeans_accum<double><<<grid, KA_THREADS, 0, S(stream)>>>(N, D, K, (const double*)points, ldp, labels, psum,
+                                                               pcnt, (int)ndb);
   LAUNCH_CHECK("spx_kmeans_accumulate");
   const int add = zero_first ? 0 : 1;
-  i64 n = K * D;
-  unsigned gb = (unsigned)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
-  k_kmeans_reduce<double><<<gb, 256, 0, S(stream)>>>(n, G, psum, sums, add);
+  const i64 n = K * D;
+  k_kmeans_reduce<double><<<(unsigned)((n + 63) / 64), 256, 0, S(stream)>>>(n, G, psum, sums, add);
   LAUNCH_CHECK("spx_kmeans_accumulate(reduce sums)");
-  gb = (unsigned)((K + 255) / 256 < 2048 ? (K + 255) / 256 : 2048);
-  k_kmeans_reduce<unsigned long long><<<gb, 256, 0, S(stream)>>>(K, G, pcnt, (unsigned long long*)counts, add);
+  k_kmeans_reduce<unsigned long long><<<(unsigned)((K + 63) / 64), 256, 0, S(stream)>>>(
+      K, G, pcnt, (unsigned long long*)counts, add);
   LAUNCH_CHECK("spx_kmeans_accumulate(reduce counts)");
   return SPX_OK;
 }

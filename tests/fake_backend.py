@@ -165,7 +165,7 @@ class FakeBackend:
       r = r + beta * _np(C)
     C.copy_(torch.as_tensor(np.ascontiguousarray(r.astype(_np(C).dtype))))
 
-  def kmeans_assign(self, points, centers, labels, mindist=None):
+  def kmeans_assign(self, points, centers, labels, mindist=None, exact_only=False):
     from scipy.spatial.distance import cdist
     d = cdist(_np(points).astype(np.float64), _np(centers))
     labels.copy_(torch.as_tensor(d.argmin(1).astype(np.int64)))

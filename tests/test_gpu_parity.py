@@ -453,4 +453,51 @@ def test_kmeans_accumulate_direct(ex, dt, N, D, K):
   np.testing.assert_array_equal(sums.cpu().numpy(), s1)        # deterministic
   be.kmeans_accumulate(P, L, sums, cnts, zero_first=False)
   np.testing.assert_array_equal(cnts.cpu().numpy(), 2 * want_c)
-  np.testing.assert_allclose(sums.cpu().numpy(), 2 * s1, rtol=1e-14, atol=1e-300)
+  assert np.all(np.abs(sums.cpu().numpy() - 2 * s1) <= 1e-13 * scale * max(1, N) ** 0.5 + 1e-300)
+
+
+def _assign_case(kind, dt):
+  g = np.random.default_rng(hash(kind) % 2**32)
+  if kind == 'uniform':
+    pts = g.random((20000, 128)).astype(dt); C = pts[:256].astype(np.float64)
+  elif kind == 'ties':                      # duplicate centres + exact midpoints
+    C = g.random((64, 24)); C[40] = C[3]; C[41] = C[3]
+    pts = g.random((6000, 24)).astype(dt)
+    for i in range(0, 6000, 7):
+      a, b = g.integers(0, 64, 2)
+      pts[i] = ((C[a] + C[b]) / 2).astype(dt)
+    pts[1::11] = C[g.integers(0, 64, len(pts[1::11]))].astype(dt)
+  elif kind == 'offset':                    # |p|^2 >> d^2: stresses the bound
+    C = 1e4 + g.random((300, 40)); pts = (1e4 + g.random((5000, 40))).astype(dt)
+  elif kind == 'clusters':                  # tight clusters, many near-equidistant
+    ctr = g.random((20, 33)) * 10
+    pts = (ctr[g.integers(0, 20, 8000)] + 1e-3 * g.standard_normal((8000, 33))).astype(dt)
+    C = ctr[g.integers(0, 20, 517)] + 1e-3 * g.standard_normal((517, 33))
+  elif kind == 'k1':
+    C = g.random((1, 7)); pts = g.random((1000, 7)).astype(dt)
+  elif kind == 'nonfinite':
+    C = g.random((30, 16)); pts = g.random((3000, 16)).astype(dt)
+    pts[5, 3] = np.nan; pts[9, 0] = np.inf; pts[13, :] = -np.inf
+  return np.ascontiguousarray(pts), np.ascontiguousarray(C)
+
+
+@pytest.mark.parametrize('dt', [np.float32, np.float64])
+@pytest.mark.parametrize('kind', ['uniform', 'ties', 'offset', 'clusters', 'k1', 'nonfinite'])
+def test_kmeans_assign_certified_bit_exact(ex, kind, dt):
+  """The MFMA-certified fast path must give argmin(scipy cdist) bit for bit
+  (first index on ties, NaN rows -> first NaN = 0), identical to the
+  all-exact kernel."""
+  import torch
+  from oracle import workloads as OW
+  from spartan_amd import backend
+  be = backend.get()
+  pts, C = _assign_case(kind, dt)
+  want = OW.kmeans_assign(pts, C)
+  P = torch.as_tensor(pts).cuda()
+  Cd = torch.as_tensor(C).cuda()
+  fast = torch.empty(len(pts), dtype=torch.int64, device='cuda')
+  slow = torch.empty_like(fast)
+  be.kmeans_assign(P, Cd, fast)
+  be.kmeans_assign(P, Cd, slow, exact_only=True)
+  np.testing.assert_array_equal(slow.cpu().numpy(), want)
+  np.testing.assert_array_equal(fast.cpu().numpy(), want)
