@@ -583,8 +583,8 @@ __global__ __launch_bounds__(256) void k_kmeans_assign(i64 N, i64 D, i64 K, cons
   // undecided points); the grid is sized for the worst case.
   __shared__ double Cs[KM_CC][KM_DC];
   const i64 n = rows ? (i64)*nrows : N;
-  if ((i64)blockIdx.x * 256 >= n) return;  // block-uniform
-  const i64 q = (i64)blockIdx.x * 256 + threadIdx.x;
+  for (i64 base = (i64)blockIdx.x * 256; base < n; base += (i64)gridDim.x * 256) {  // block-uniform
+  const i64 q = base + threadIdx.x;
   const bool valid = q < n;
   const i64 p = valid ? (rows ? rows[q] : q) : 0;
   double best = 0.0;
@@ -630,31 +630,46 @@ __global__ __launch_bounds__(256) void k_kmeans_assign(i64 N, i64 D, i64 K, cons
     labels[p] = bi;
     if (mind) mind[p] = best;
   }
+  }
 }
 
 // Certified fast assignment.  Exact-order fp64 distances cost 3 fp64 VALU
 // ops per (point, centre, dim); instead an fp32 MFMA GEMM gives
-//   a'(p, c) = |c|^2 - 2 p.c   (= d^2(p, c) - |p|^2 up to rounding)
+//   a'(p, c) = fl(|c|^2 - 2 p.c)   (= d^2(p, c) - |p|^2 up to rounding)
 // for every centre, and a point is labelled here only when its best and
-// second-best a' are separated by more than a rigorous bound on the error:
-//   |a' - a| <= 2 (D + 3) u32 |p| |c|  (fp32 fma-chain dot over D terms of
-//   fp32-rounded operands, u32 = 2^-24) + an absolute term for fp32
-//   underflow, and a relative slack 1e-8 (|p|^2 + max|c|^2) that dwarfs the
-//   fp64 rounding of scipy's sum and of the sqrt, so the certified winner is
-//   the strict, hence first-index, argmin of the exact-order distances.
-// Every other point (near-ties, non-finite values) is appended to a list and
-// labelled by k_kmeans_assign in exactly scipy's order.  The labels are thus
-// bit-identical to the all-exact kernel's.
-// Layout: block = 256 points x all centres (256-centre tiles), 16 waves of
-// v_mfma_f32_32x32x2_f32 (4 x 4, 64 x 64 each), BK = 16 with register-staged
-// double buffering as in gemm_kernels.h.  The epilogue transposes each
-// 128-row half of the S tile through LDS (stride 264: conflict-free both
-// ways) and 8 lanes per row scan 32 centres each for the top two, merged by
-// xor-shuffles.  |p| comes from the A tiles already in LDS.
-constexpr int KF_BM = 256, KF_BN = 256, KF_BK = 16, KF_THREADS = 1024;
+// second-best a' are separated by more than twice a rigorous bound e on
+// |a' - a|:
+//   2 (D + 3) u |p| |c|     fp32 fma-chain dot over D terms of fp32-rounded
+//                           operands (v_mfma_f32_32x32x2_f32 is exactly such
+//                           a chain), u = 2^-24;
+//   2 u (|c|^2 + |p| |c|)   fp32 |c|^2 and the final fma;
+//   4 D 1.2e-38 (1 + |c|)   fp32 underflow;
+//   1e-8 (|p|^2 + |c|^2)    slack that dwarfs the fp64 rounding of scipy's
+//                           sum and of the sqrt, so the certified winner is
+//                           the strict, hence first-index, exact argmin;
+// with |p|, |c| upper bounds (max over centres for |c|).  Undecided points
+// (near-ties, non-finite values) are labelled in exactly scipy's order: for
+// K <= 256 only the candidate centres (a' <= best + 2e, a 256-bit mask per
+// point) are recomputed (k_kmeans_cand), otherwise every centre
+// (k_kmeans_assign in list mode).  The labels are bit-identical to the
+// all-exact kernel's.
+// Layout: block = BM points x all centres in 256-centre tiles, waves of
+// v_mfma_f32_32x32x2_f32 (BM/64 x 4 waves, 64 x 64 each), BK = 16,
+// register-staged double buffering as in gemm_kernels.h; several blocks per
+// CU so one block's epilogue overlaps another's MFMAs (KfProd, tuned with
+// tools/kf_tune.hip).  The epilogue transposes each 64-row
+// half of the S tile through LDS (row stride 264 floats: conflict-free both
+// ways) and 8 lanes per row scan 32 centres each for the top two (fp32),
+// merged by xor-shuffles.  |p| comes from the A tiles already in LDS.
+constexpr int KF_BN = 256, KF_BK = 16;
 constexpr int KF_EP = 264;  // epilogue row stride (floats)
 
-__device__ __forceinline__ void kf_merge(double& b1, i64& i1, double& b2, double o1, i64 oi, double o2) {
+struct KfCand {
+  i64 row;
+  unsigned int mask[8];  // bit k of word w <-> centre w + 8 k
+};
+
+__device__ __forceinline__ void kf_merge(float& b1, int& i1, float& b2, float o1, int oi, float o2) {
   if (o1 < b1 || (o1 == b1 && oi < i1)) {
     b2 = b1 < o2 ? b1 : o2;
     b1 = o1;
@@ -664,32 +679,39 @@ __device__ __forceinline__ void kf_merge(double& b1, i64& i1, double& b2, double
   }
 }
 
-template <typename TP, bool ALIGNED>
-__global__ __launch_bounds__(KF_THREADS) void k_kmeans_filter(i64 N, i64 D, i64 K, i64 Kp, const TP* __restrict__ P,
-                                                              i64 ldp, const float* __restrict__ CT,
-                                                              const double* __restrict__ cn, const double* cmax_p,
-                                                              i64* __restrict__ labels, unsigned int* __restrict__ nflag,
-                                                              i64* __restrict__ flagged) {
+// BM points per block (BM / 64 x 4 waves), LDS row padding PA (A) / PB (B),
+// MINW = min waves per SIMD for the register budget.
+template <typename TP, bool ALIGNED, int BM, int PA, int PB, int MINW>
+__global__ __launch_bounds__(BM * 4, MINW) void k_kmeans_filter(i64 N, i64 D, i64 K, i64 Kp,
+                                                                const TP* __restrict__ P, i64 ldp,
+                                                                const float* __restrict__ CT,
+                                                                const double* __restrict__ cn, const double* cmax_p,
+                                                                i64* __restrict__ labels,
+                                                                unsigned int* __restrict__ counters,
+                                                                i64* __restrict__ full_list,
+                                                                KfCand* __restrict__ cand_list) {
   typedef spx_mfma::Mfma<float> F;
   typedef float V __attribute__((ext_vector_type(4)));
-  constexpr int BM = KF_BM, BN = KF_BN, BK = KF_BK, NT = KF_THREADS, WN = 4;
-  constexpr int WTM = 64, WTN = 64, TM = 2, TN = 2;
-  constexpr int LA = BM * BK / 4 / NT, LB = BK * BN / 4 / NT;  // 1, 1
-  constexpr int MAIN_BYTES = (2 * BK * (BM + 2) + 2 * BK * BN) * 4;
-  constexpr int EPI_BYTES = 128 * KF_EP * 4;
-  static_assert(LA == 1 && LB == 1, "tiling");
+  constexpr int BN = KF_BN, BK = KF_BK, NT = BM * 4, WN = 4;
+  constexpr int WTM = 64, WTN = 64, TM = 2, TN = 2, HR = BM / 2;  // HR: rows per epilogue half
+  constexpr int LB = BK * BN / 4 / NT;  // B loads per lane (A: 1)
+  constexpr int MAIN_BYTES = (2 * BK * (BM + PA) + 2 * BK * (BN + PB)) * 4;
+  constexpr int EPI_BYTES = HR * KF_EP * 4;
+  static_assert(BM * BK / 4 == NT && LB * NT * 4 == BK * BN && HR * 8 == NT && PB % 4 == 0, "tiling");
   __shared__ __attribute__((aligned(16))) unsigned char lds[MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES];
   __shared__ float pnp[4][BM];
-  float(*As)[BK][BM + 2] = (float(*)[BK][BM + 2])lds;
-  float(*Bs)[BK][BN] = (float(*)[BK][BN])(lds + 2 * BK * (BM + 2) * 4);
+  __shared__ float cns[BN];
+  float(*As)[BK][BM + PA] = (float(*)[BK][BM + PA])lds;
+  float(*Bs)[BK][BN + PB] = (float(*)[BK][BN + PB])(lds + 2 * BK * (BM + PA) * 4);
   float* E = (float*)lds;
   const i64 row0 = (i64)blockIdx.x * BM;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w / WN, wn = w % WN;
-  const int rl = t >> 3, sub = t & 7;      // epilogue: row (of 128) and column phase
-  const int nm = t & (BM - 1), nq = t >> 8;  // row-norm: row and k quarter
+  const int rl = t >> 3, sub = t & 7;                   // epilogue: row (of HR) and column phase
+  const int nm = t & (BM - 1), nq = t / BM;             // row norm: row and k quarter
+  const bool single = Kp == BN;
   float pn = 0.f;
-  double s1[TM], s2[TM];
-  i64 si[TM];
+  float s1[TM], s2[TM];
+  int si[TM];
   bool bad[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -698,8 +720,11 @@ __global__ __launch_bounds__(KF_THREADS) void k_kmeans_filter(i64 N, i64 D, i64 
     si[i] = -1;
     bad[i] = false;
   }
-  V ra, rb;
+  const double cmax = *cmax_p;
+  const double u32 = 5.9604644775390625e-08;
+  V ra, rb[LB];
   for (i64 c0 = 0; c0 < Kp; c0 += BN) {
+    const bool last = c0 + BN >= Kp;
     F::acc_t acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -716,22 +741,26 @@ __global__ __launch_bounds__(KF_THREADS) void k_kmeans_filter(i64 N, i64 D, i64 
           for (int j = 0; j < 4; ++j) ra[j] = (gr < N && gk + j < D) ? (float)P[gr * ldp + gk + j] : 0.f;
         }
       }
-      {
-        const int kr = t / (BN / 4), cq = t % (BN / 4);
+#pragma unroll
+      for (int l = 0; l < LB; ++l) {
+        const int idx = t + l * NT, kr = idx / (BN / 4), cq = idx % (BN / 4);
         const i64 bk = k0 + kr;
-        if (bk < D) rb = *(const V*)(CT + bk * Kp + c0 + cq * 4);
-        else rb = (V){0.f, 0.f, 0.f, 0.f};
+        rb[l] = bk < D ? *(const V*)(CT + bk * Kp + c0 + cq * 4) : (V){0.f, 0.f, 0.f, 0.f};
       }
     };
     auto store = [&](int buf) {
       const int r = t / (BK / 4), kq = t % (BK / 4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) As[buf][kq * 4 + j][r] = ra[j];
-      const int kr = t / (BN / 4), cq = t % (BN / 4);
-      *(V*)(&Bs[buf][kr][cq * 4]) = rb;
+#pragma unroll
+      for (int l = 0; l < LB; ++l) {
+        const int idx = t + l * NT, kr = idx / (BN / 4), cq = idx % (BN / 4);
+        *(V*)(&Bs[buf][kr][cq * 4]) = rb[l];
+      }
     };
     const int nk = (int)((D + BK - 1) / BK);
-    __syncthreads();  // previous epilogue done with the shared buffer
+    __syncthreads();  // previous epilogue done with the shared buffers
+    if (t < BN) cns[t] = (float)cn[c0 + t];
     load(0);
     store(0);
     __syncthreads();
@@ -761,7 +790,8 @@ __global__ __launch_bounds__(KF_THREADS) void k_kmeans_filter(i64 N, i64 D, i64 
       if (kt + 1 < nk) store(cur ^ 1);
       __syncthreads();
     }
-    // epilogue: half i holds rows wm*64 + i*32 + [0, 32) of every wm
+    if (c0 == 0) pnp[nq][nm] = pn;
+    // epilogue: half i holds rows wm*64 + i*32 + [0, 32) of both wm
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       if (i) __syncthreads();
@@ -771,55 +801,117 @@ __global__ __launch_bounds__(KF_THREADS) void k_kmeans_filter(i64 N, i64 D, i64 
         for (int r = 0; r < F::NREG; ++r)
           E[(wm * 32 + F::crow(lane, r)) * KF_EP + wn * WTN + j * F::TILE + F::ccol(lane)] = acc[i][j][r];
       __syncthreads();
-      double b1 = INFINITY, b2 = INFINITY;
-      i64 i1 = -1;
+      float b1 = INFINITY, b2 = INFINITY;
+      int i1 = -1;
       bool nf = false;
 #pragma unroll 8
       for (int k = 0; k < BN / 8; ++k) {
         const int col = sub + 8 * k;
-        const double a = cn[c0 + col] - 2.0 * (double)E[rl * KF_EP + col];
+        const float a = __builtin_fmaf(-2.f, E[rl * KF_EP + col], cns[col]);
         nf |= a != a;
         if (a < b1) {
           b2 = b1;
           b1 = a;
-          i1 = c0 + col;
+          i1 = (int)c0 + col;
         } else if (a < b2) {
           b2 = a;
         }
       }
 #pragma unroll
       for (int o = 1; o < 8; o <<= 1) {
-        const double o1 = __shfl_xor(b1, o, 64), o2 = __shfl_xor(b2, o, 64);
-        const i64 oi = __shfl_xor(i1, o, 64);
+        const float o1 = __shfl_xor(b1, o, 64), o2 = __shfl_xor(b2, o, 64);
+        const int oi = __shfl_xor(i1, o, 64);
         nf |= __shfl_xor((int)nf, o, 64) != 0;
         kf_merge(b1, i1, b2, o1, oi, o2);
       }
       kf_merge(s1[i], si[i], s2[i], b1, i1, b2);
       bad[i] |= nf;
+      if (!last) continue;
+      // decision for this half's rows (the 8 lanes of a row agree)
+      const int lr = (rl / 32) * WTM + i * 32 + (rl % 32);  // row within the block
+      const i64 row = row0 + lr;
+      if (row >= N) continue;
+      static_assert(BM / 64 * 32 == HR, "halves");
+      const float p2f = pnp[0][lr] + pnp[1][lr] + pnp[2][lr] + pnp[3][lr];
+      const double p2 = (double)p2f * 1.001 + (double)D * 2e-45;
+      const double pnorm = sqrt(p2) * 1.0001;
+      const double e = 2.0 * (double)(D + 3) * 1.01 * u32 * pnorm * cmax +
+                       2.02 * u32 * (cmax * cmax + pnorm * cmax) + 4.0 * (double)D * 1.2e-38 * (1.0 + cmax) +
+                       1e-8 * (p2 + cmax * cmax) + 1e-300;
+      const bool fin = !bad[i] && isfinite(s1[i]) && isfinite(e);
+      if (fin && (double)s2[i] - (double)s1[i] > 2.0 * e) {
+        if (sub == 0) labels[row] = si[i];
+      } else if (fin && single) {
+        const double thr = (double)s1[i] + 2.0 * e;
+        unsigned int m = 0;
+#pragma unroll 8
+        for (int k = 0; k < BN / 8; ++k) {
+          const int col = sub + 8 * k;
+          const float a = __builtin_fmaf(-2.f, E[rl * KF_EP + col], cns[col]);
+          if ((double)a <= thr) m |= 1u << k;
+        }
+        unsigned int slot = 0;
+        if (sub == 0) slot = atomicAdd(&counters[1], 1u);
+        slot = __shfl(slot, lane & ~7, 64);
+        cand_list[slot].mask[sub] = m;
+        if (sub == 0) cand_list[slot].row = row;
+      } else if (sub == 0) {
+        full_list[atomicAdd(&counters[0], 1u)] = row;
+      }
     }
-    if (c0 == 0) pnp[nq][nm] = pn;
   }
-  __syncthreads();
-  if (sub != 0) return;
-  const double cmax = *cmax_p;
-  const double u32 = 5.9604644775390625e-08;
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int lr = (rl / 32) * WTM + i * 32 + (rl % 32);  // row within the block
-    const i64 row = row0 + lr;
-    if (row >= N) continue;
-    const double p2 = (double)pnp[0][lr] + (double)pnp[1][lr] + (double)pnp[2][lr] + (double)pnp[3][lr];
-    const double pnorm = sqrt(p2) * 1.001;
-    const double e = 2.0 * (double)(D + 3) * u32 * 1.01 * pnorm * cmax + 4.0 * (double)D * 1.2e-38 * (1.0 + cmax) +
-                     1e-8 * (p2 + cmax * cmax) + 1e-300;
-    const bool ok = !bad[i] && isfinite(s1[i]) && isfinite(pnorm) && isfinite(e) && s1[i] == s1[i] &&
-                    (s2[i] - s1[i] > 2.0 * e);
-    if (ok) {
-      labels[row] = si[i];
-    } else {
-      const unsigned int slot = atomicAdd(nflag, 1u);
-      flagged[slot] = row;
+}
+
+template <int BM_, int PA, int PB, int MINW>
+struct KfConf {
+  static constexpr int BM = BM_;
+  template <typename TP, bool AL>
+  static void launch(i64 grid, hipStream_t s, i64 N, i64 D, i64 K, i64 Kp, const void* P, i64 ldp, const float* CT,
+                     const double* cn, const double* cmax, i64* labels, unsigned int* counters, i64* full_list,
+                     KfCand* cand_list) {
+    k_kmeans_filter<TP, AL, BM, PA, PB, MINW><<<(unsigned)grid, BM * 4, 0, s>>>(
+        N, D, K, Kp, (const TP*)P, ldp, CT, cn, cmax, labels, counters, full_list, cand_list);
+  }
+};
+#ifndef KF_PROD
+#define KF_PROD KfConf<64, 2, 0, 3>
+#endif
+typedef KF_PROD KfProd;
+
+// Exact-order labels of the undecided points from their candidate masks
+// (K <= 256); equal distances go to the lower index (= first occurrence).
+template <typename TP>
+__global__ __launch_bounds__(256) void k_kmeans_cand(i64 D, const TP* __restrict__ P, i64 ldp,
+                                                     const double* __restrict__ C, i64* __restrict__ labels,
+                                                     const unsigned int* __restrict__ counters,
+                                                     const KfCand* __restrict__ cand_list) {
+  const i64 n = counters[1];
+  for (i64 q = (i64)blockIdx.x * 256 + threadIdx.x; q < n; q += (i64)gridDim.x * 256) {
+    const i64 row = cand_list[q].row;
+    const TP* x = P + row * ldp;
+    double best = 0.0;
+    int bi = -1;
+    for (int wd = 0; wd < 8; ++wd) {
+      unsigned int m = cand_list[q].mask[wd];
+      while (m) {
+        const int k = __ffs(m) - 1;
+        m &= m - 1;
+        const int c = wd + 8 * k;
+        const double* cc = C + (i64)c * D;
+        double acc = 0.0;
+        for (i64 d = 0; d < D; ++d) {
+          const double df = (double)x[d] - cc[d];
+          const double sq = df * df;
+          acc = acc + sq;
+        }
+        const double dist = sqrt(acc);
+        if (bi < 0 || dist < best || (dist == best && c < bi)) {
+          best = dist;
+          bi = c;
+        }
+      }
     }
+    labels[row] = bi;
   }
 }
 
@@ -860,8 +952,8 @@ __global__ __launch_bounds__(256) void k_kmeans_prep(i64 D, i64 K, i64 Kp, const
 //                     accumulator tile of KA_CB centres x 64 columns picked by
 //                     y (128 KB of LDS) and the point chunks x, x+G, ...  Wave
 //                     w owns the centres c == w (mod 16) of the tile, lane =
-//                     column.  Each chunk of rows is prefetched into registers
-//                     one chunk ahead and staged in LDS; every wave ballots the
+//                     column.  Chunks of rows are prefetched into a register
+//                     ring KA_STAGES chunks deep and staged in LDS; every wave ballots the
 //                     chunk's labels and adds its own points' rows, in point
 //                     order, with plain LDS read-modify-writes (one owner per
 //                     accumulator: no atomics).  The tile is written once to
@@ -872,13 +964,15 @@ constexpr int KA_THREADS = 1024;
 constexpr int KA_DB = 64;                  // columns per tile = lanes per wave
 constexpr int KA_CB = 16384 / KA_DB;       // centres per tile (128 KB of fp64)
 constexpr int KA_WAVES = KA_THREADS / 64;  // centre owners per tile
+constexpr int KA_STAGES = 4;               // register prefetch ring depth
 
 template <typename TP>
 __global__ __launch_bounds__(KA_THREADS) void k_kmeans_accum(i64 N, i64 D, i64 K, const TP* __restrict__ P, i64 ldp,
                                                              const i64* __restrict__ labels, double* __restrict__ psum,
                                                              unsigned long long* __restrict__ pcnt, int ndb) {
   constexpr int CH = 16384 / (KA_DB * (int)sizeof(TP)) < 64 ? 16384 / (KA_DB * (int)sizeof(TP)) : 64;
-  constexpr int PF = CH * KA_DB / KA_THREADS;  // prefetched elements per lane
+  constexpr int PF = CH * KA_DB / KA_THREADS;  // prefetched elements per lane per chunk
+  constexpr int ST = KA_STAGES;                // chunks in flight per block
   __shared__ double acc[KA_CB * KA_DB];
   __shared__ TP xs[CH * KA_DB];
   __shared__ int lab_s[CH];
@@ -889,37 +983,45 @@ __global__ __launch_bounds__(KA_THREADS) void k_kmeans_accum(i64 N, i64 D, i64 K
   const i64 nch = (N + CH - 1) / CH;
   for (int i = t; i < KA_CB * KA_DB; i += KA_THREADS) acc[i] = 0.0;
   for (int i = t; i < KA_CB; i += KA_THREADS) cnt[i] = 0;
-  TP pf[PF];
-  int plab = -1;
-  auto load = [&](i64 ch) {
+  TP pf[ST][PF];
+  int plab[ST];
+  auto load = [&](int s, i64 ch) {
+    if (ch >= nch) return;
     const i64 p0 = ch * CH;
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
       const int e = t + KA_THREADS * k, p = e / KA_DB, d = e % KA_DB;
-      pf[k] = (p0 + p < N && d0 + d < D) ? P[(p0 + p) * ldp + d0 + d] : TP(0);
+      pf[s][k] = (p0 + p < N && d0 + d < D) ? P[(p0 + p) * ldp + d0 + d] : TP(0);
     }
+    plab[s] = -1;
     if (t < CH) {
       const i64 l = p0 + t < N ? labels[p0 + t] : -1;
-      plab = (l >= c0 && l < K && l - c0 < KA_CB) ? (int)(l - c0) : -1;
+      plab[s] = (l >= c0 && l < K && l - c0 < KA_CB) ? (int)(l - c0) : -1;
     }
   };
-  i64 ch = blockIdx.x;
-  if (ch < nch) load(ch);
-  for (; ch < nch; ch += gridDim.x) {
-    __syncthreads();  // previous chunk fully consumed (and the zeroing done)
+  const i64 G = gridDim.x;
 #pragma unroll
-    for (int k = 0; k < PF; ++k) xs[t + KA_THREADS * k] = pf[k];
-    if (t < CH) lab_s[t] = plab;
-    __syncthreads();
-    if (ch + gridDim.x < nch) load(ch + gridDim.x);  // next chunk in flight
-    const int r = lane < CH ? lab_s[lane] : -1;
-    unsigned long long m = __ballot(r >= 0 && (r % KA_WAVES) == w);
-    while (m) {
-      const int p = __ffsll((long long)m) - 1;
-      m &= m - 1;
-      const int rr = __shfl(r, p, 64);
-      acc[rr * KA_DB + lane] += (double)xs[p * KA_DB + lane];
-      if (lane == 0) cnt[rr] += 1u;
+  for (int s = 0; s < ST; ++s) load(s, blockIdx.x + s * G);
+  for (i64 base = blockIdx.x; base < nch; base += ST * G) {
+#pragma unroll
+    for (int s = 0; s < ST; ++s) {
+      const i64 ch = base + s * G;
+      if (ch >= nch) break;  // block-uniform
+      __syncthreads();       // previous chunk consumed (and the zeroing done)
+#pragma unroll
+      for (int k = 0; k < PF; ++k) xs[t + KA_THREADS * k] = pf[s][k];
+      if (t < CH) lab_s[t] = plab[s];
+      __syncthreads();
+      load(s, ch + ST * G);  // refill this stage: ST chunks stay in flight
+      const int r = lane < CH ? lab_s[lane] : -1;
+      unsigned long long m = __ballot(r >= 0 && (r % KA_WAVES) == w);
+      while (m) {
+        const int p = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const int rr = __shfl(r, p, 64);
+        acc[rr * KA_DB + lane] += (double)xs[p * KA_DB + lane];
+        if (lane == 0) cnt[rr] += 1u;
+      }
     }
   }
   __syncthreads();
@@ -970,11 +1072,16 @@ static void ka_grid(int dtype, i64 N, i64 D, i64 K, i64* G, i64* ndb, i64* ncb) 
 
 static i64 kf_kp(i64 K) { return (K + KF_BN - 1) / KF_BN * KF_BN; }
 
+static int kf_persistent_grid(i64 N) {
+  const i64 g = (N + 255) / 256;
+  return (int)(g < 2048 ? (g < 1 ? 1 : g) : 2048);
+}
+
 extern "C" int64_t spx_kmeans_assign_workspace(int dtype, int64_t N, int64_t D, int64_t K) {
   if ((dtype != SPX_F32 && dtype != SPX_F64) || N < 0 || D < 1 || K < 1) return -1;
   const i64 Kp = kf_kp(K);
-  // CT (D x Kp f32) | cn (Kp f64) | cmax | counter | flagged (N i64)
-  return (D * Kp * 4 + 15) / 16 * 16 + Kp * 8 + 16 + 16 + N * 8;
+  // CT (D x Kp f32) | cn (Kp f64) | cmax | counters | full list (N i64) | candidate list (N KfCand, K <= 256)
+  return (D * Kp * 4 + 15) / 16 * 16 + Kp * 8 + 16 + 16 + N * 8 + (Kp == KF_BN ? N * (i64)sizeof(KfCand) : 0);
 }
 
 extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
@@ -1007,32 +1114,42 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
   ws += Kp * 8;
   double* cmax = (double*)ws;
   ws += 16;
-  unsigned int* nflag = (unsigned int*)ws;
+  unsigned int* counters = (unsigned int*)ws;
   ws += 16;
-  i64* flagged = (i64*)ws;
-  HIP_TRY(hipMemsetAsync(nflag, 0, sizeof(unsigned int), S(stream)));
+  i64* full_list = (i64*)ws;
+  ws += N * 8;
+  KfCand* cand_list = (KfCand*)ws;
+  HIP_TRY(hipMemsetAsync(counters, 0, 2 * sizeof(unsigned int), S(stream)));
   k_kmeans_prep<<<1, 256, 0, S(stream)>>>(D, K, Kp, centers, CT, cn, cmax);
   LAUNCH_CHECK("spx_kmeans_assign(prep)");
-  const i64 gf = (N + KF_BM - 1) / KF_BM;
+  const i64 gf = (N + KfProd::BM - 1) / KfProd::BM;
   const bool al = D % KF_BK == 0 && ldp % 4 == 0 && ((uintptr_t)points % 16) == 0;
   if (dtype == SPX_F32) {
-    if (al)
-      k_kmeans_filter<float, true><<<(unsigned)gf, KF_THREADS, 0, S(stream)>>>(
-          N, D, K, Kp, (const float*)points, ldp, CT, cn, cmax, labels, nflag, flagged);
-    else
-      k_kmeans_filter<float, false><<<(unsigned)gf, KF_THREADS, 0, S(stream)>>>(
-          N, D, K, Kp, (const float*)points, ldp, CT, cn, cmax, labels, nflag, flagged);
+    if (al) KfProd::launch<float, true>(gf, S(stream), N, D, K, Kp, points, ldp, CT, cn, cmax, labels, counters,
+                                        full_list, cand_list);
+    else KfProd::launch<float, false>(gf, S(stream), N, D, K, Kp, points, ldp, CT, cn, cmax, labels, counters,
+                                      full_list, cand_list);
   } else {
-    k_kmeans_filter<double, false><<<(unsigned)gf, KF_THREADS, 0, S(stream)>>>(
-        N, D, K, Kp, (const double*)points, ldp, CT, cn, cmax, labels, nflag, flagged);
+    KfProd::launch<double, false>(gf, S(stream), N, D, K, Kp, points, ldp, CT, cn, cmax, labels, counters, full_list,
+                                  cand_list);
   }
   LAUNCH_CHECK("spx_kmeans_assign(filter)");
+  const int gp = kf_persistent_grid(N);
+  if (Kp == KF_BN) {
+    if (dtype == SPX_F32)
+      k_kmeans_cand<float><<<gp, 256, 0, S(stream)>>>(D, (const float*)points, ldp, centers, labels, counters,
+                                                       cand_list);
+    else
+      k_kmeans_cand<double><<<gp, 256, 0, S(stream)>>>(D, (const double*)points, ldp, centers, labels, counters,
+                                                        cand_list);
+    LAUNCH_CHECK("spx_kmeans_assign(candidates)");
+  }
   if (dtype == SPX_F32)
-    k_kmeans_assign<float><<<(unsigned)g, 256, 0, S(stream)>>>(N, D, K, (const float*)points, ldp, centers, labels,
-                                                                nullptr, flagged, nflag);
+    k_kmeans_assign<float><<<gp, 256, 0, S(stream)>>>(N, D, K, (const float*)points, ldp, centers, labels, nullptr,
+                                                       full_list, counters);
   else
-    k_kmeans_assign<double><<<(unsigned)g, 256, 0, S(stream)>>>(N, D, K, (const double*)points, ldp, centers, labels,
-                                                                 nullptr, flagged, nflag);
+    k_kmeans_assign<double><<<gp, 256, 0, S(stream)>>>(N, D, K, (const double*)points, ldp, centers, labels,
+                                                        nullptr, full_list, counters);
   LAUNCH_CHECK("spx_kmeans_assign(exact)");
   return SPX_OK;
 }
