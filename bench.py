@@ -225,11 +225,12 @@ def bench_lreg(npts, ctx, expr, comm, sync, D=64, iters=5):
   comm.barrier()
   el = comm.max_over_ranks(time.perf_counter() - t0) / iters
   n = npts * ctx.world_size
-  nbytes = 2 * (4.0 * n * D) + 3 * 4.0 * n   # GEMV reads X, fused reduce reads X + yp + y; yp written
+  nbytes = 4.0 * n * D + 4.0 * n   # one pass: X and y read once (DotReduceFusion)
   out = {'ms_per_iter': round(el * 1e3, 3), 'algorithmic_GBps': round(nbytes / el / 1e9, 1),
-         'single_pass_bytes_GBps': round((4.0 * n * D + 4.0 * n) / el / 1e9, 1),
-         'config': 'cfg5: X %d x %d fp32, y %d x 1, w 64 x 1 host; dot (GEMV) + fused x*(yp-y) sum axis 0 '
-                   '+ all-reduce; two passes over X' % (n, D, n)}
+         'hbm_frac_per_gpu': round(nbytes / el / 1e9 / (HBM_PEAK_GBS * ctx.world_size), 4),
+         'config': 'cfg5: X %d x %d fp32, y %d x 1, w 64 x 1 host; grad = sum(x * (dot(x, w) - y), axis=0): '
+                   'dot folded into the fused axis-0 reduction (one pass over X) + all-reduce of 64 fp32'
+                   % (n, D, n)}
   del X, Y, Xe, Ye
   torch.cuda.empty_cache()
   return out

@@ -380,6 +380,8 @@ class HipBackend:
       P = -(-R // chunk)
       nblk = base * P
       args.aux[0], args.aux[1], args.aux[2], args.aux[3] = P, chunk, lpr.bit_length() - 1, CT
+    if codegen.rowdots(root) and (kind != 'cols' or CT != 1):
+      raise NotImplementedError('fused row dot needs each row in one lane group (K <= 64 * vector width)')
     if nblk > 0x7fffffff:
       raise NotImplementedError('reduction grid too large')
     args.flags = 1 if vec_ok else 0
@@ -402,10 +404,15 @@ class HipBackend:
       part_i = None
     args.out0 = part_v.data_ptr()
     args.out1 = part_i.data_ptr() if arg else 0
-    sig = ('reduce', root.sig(), tuple(ins), tuple(classes), kind, op, V)
+    U, rowinv = None, ()
+    if kind == 'cols':
+      U = codegen.cols_unroll(ins, classes, V, [vstr[k][1] for k in range(len(slots))])
+      rowinv = tuple(s for k, s in enumerate(slots) if vstr[k][1] == 0)
+    sig = ('reduce', root.sig(), tuple(ins), tuple(classes), kind, op, V, U, rowinv)
     fn = self._sig_fns.get(sig)
     if fn is None:
-      fn = self._sig_fns[sig] = self.kernel(codegen.gen_reduce(root, ins, classes, kind, op, V), 'spx_reduce')
+      fn = self._sig_fns[sig] = self.kernel(codegen.gen_reduce(root, ins, classes, kind, op, V, U, rowinv),
+                                            'spx_reduce')
     self.launch(fn, nblk, args)
     if not direct:
       _check(self.lib.spx_reduce_finalize(

@@ -101,6 +101,24 @@ class Cast:
     return 'cast<%s>(%s)' % (self.dtype.str, self.arg.sig())
 
 
+class RowDot:
+  """Per-row dot product ``a[i, :] . w`` of a fused ``dot(x, w)`` whose right
+  operand is a small host (K, 1) vector (DotReduceFusion): the value of
+  ``dot_map2_np_mapper`` (spartan/expr/dot.py:172-187) for row i, broadcast
+  along the row.  ``a`` is the (N, K) input itself, ``w`` a (1, K) broadcast
+  input; the row's K products are summed inside the lane group that holds the
+  row (only the 'cols' reduce skeleton with one column tile supports it)."""
+  __slots__ = ('a', 'w', 'dtype', 'rid')
+
+  def __init__(self, a, w):
+    self.a, self.w = a, w
+    self.dtype = np.result_type(a.dtype, w.dtype)
+    self.rid = 0
+
+  def sig(self):
+    return 'rowdot(%s,%s)' % (self.a.sig(), self.w.sig())
+
+
 def walk(node):
   yield node
   if isinstance(node, Op):
@@ -108,6 +126,19 @@ def walk(node):
       yield from walk(a)
   elif isinstance(node, Cast):
     yield from walk(node.arg)
+  elif isinstance(node, RowDot):
+    yield from walk(node.a)
+    yield from walk(node.w)
+
+
+def rowdots(root):
+  """Unique RowDot nodes of a tree, numbered (rid) in first-visit order."""
+  out = []
+  for n in walk(root):
+    if isinstance(n, RowDot) and not any(n is m for m in out):
+      n.rid = len(out)
+      out.append(n)
+  return out
 
 
 # ------------------------------------------------------------ C emission
@@ -174,7 +205,7 @@ class Emitter:
     """Return a C expression (usually a temporary) of node.dtype."""
     if isinstance(node, In):
       return leaf(node)
-    if isinstance(node, Sc):
+    if isinstance(node, (Sc, RowDot)):
       return leaf(node)
     if isinstance(node, Const):
       if is_float(node.dtype):
@@ -357,19 +388,41 @@ def _expr_fn(root, n_in, name='fexpr'):
   def leaf(node):
     if isinstance(node, In):
       return 'x%d' % node.slot
+    if isinstance(node, RowDot):
+      return 'rd%d' % node.rid
     if node.pytype is float:
       return 'a.fsc[%d]' % node.slot
     return 'a.isc[%d]' % node.slot
 
   val = em.emit(root, leaf)
-  params = ', '.join(['const KArgs& a'] + ['%s x%d' % (ctype(dt), s) for s, dt in n_in])
+  params = ', '.join(['const KArgs& a'] + ['%s x%d' % (ctype(dt), s) for s, dt in n_in] +
+                     ['%s rd%d' % (ctype(r.dtype), r.rid) for r in rowdots(root)])
   body = '\n  '.join(em.lines + ['return %s;' % val])
   fn = 'DEV %s %s(%s) {\n  %s\n}' % (ctype(root.dtype), name, params, body)
   return fn, em.ocml
 
 
-def _call_expr(inputs, j, name='fexpr'):
-  return '%s(a%s)' % (name, ''.join(', x%d_%d' % (s, j) for s, _ in inputs))
+def _call_expr(inputs, j, name='fexpr', n_rd=0, sfx=''):
+  return '%s(a%s%s)' % (name, ''.join(', x%d_%d%s' % (s, j, sfx) for s, _ in inputs),
+                        ''.join(', rd%d%s' % (k, sfx) for k in range(n_rd)))
+
+
+def cols_unroll(inputs, classes, vec, row_strides=None):
+  """Rows per lane group per iteration of the column-reduce loop: enough that
+  each wave keeps >= ~3 KiB of streamed loads in flight (Little's law at
+  ~8 TB/s over 256 CUs needs ~32-64 KiB per CU).  Inputs broadcast along the
+  columns ('b') or along the reduced rows (row stride 0, e.g. the (1, K) row
+  vector of a fused row dot) cost no HBM stream; one row of 3 contiguous
+  fp32x4 inputs is 3 KiB per wave."""
+  streamed = 0
+  for k, ((s, dt), cls) in enumerate(zip(inputs, classes)):
+    if cls != 'b' and not (row_strides is not None and row_strides[k] == 0):
+      streamed += np.dtype(dt).itemsize * vec
+  if streamed >= 48:
+    return 1
+  if streamed >= 24:
+    return 2
+  return 4
 
 
 # ---------------------------------------------------------------- map
@@ -379,6 +432,8 @@ def gen_map(root, inputs, classes, ndim, vec, dense):
   dense=True: every input is contiguous with the output's shape (flat index).
   Otherwise the N-d path: offsets from the iteration index via dim[] / str[][].
   """
+  if rowdots(root):
+    raise NotImplementedError('a fused row dot needs the column-reduce skeleton')
   fn, ocml = _expr_fn(root, inputs)
   out_ct = ctype(root.dtype)
   L = []
@@ -491,7 +546,7 @@ def _acc_update(op, j, val, idx_expr):
   return 'acc%d = comb(acc%d, %s);' % (j, j, val)
 
 
-def gen_reduce(root, inputs, classes, kind, op, vec):
+def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
   """Fused map+reduce.  kind 'rows' (reduce over contiguous R of (O, R), one
   or more blocks per segment), 'rowsp' (the same for short R: several
   segments per wave, LPR lanes each, butterfly combine) or 'cols' (reduce over
@@ -501,14 +556,20 @@ def gen_reduce(root, inputs, classes, kind, op, vec):
   I for cols): 'c', 'b' or 'g'.
   """
   assert op in REDOPS and kind in ('rows', 'rowsp', 'cols')
+  rds = rowdots(root)
+  if rds and kind != 'cols':
+    raise NotImplementedError('a fused row dot needs the column-reduce skeleton')
   fn, ocml = _expr_fn(root, inputs)
   adt = acc_dtype(op, root.dtype)
   act = ctype(adt)
   arg = op in ('argmin', 'argmax')
   L = [PRELUDE, _ocml_decls(ocml), fn, _comb_fns(op, adt)]
+  if rds:
+    L.append(SHFL)
+    L.append(ROW_ALLSUM)
 
   def val_j(j):
-    return '(%s)%s' % (act, _call_expr(inputs, j))
+    return '(%s)%s' % (act, _call_expr(inputs, j, n_rd=len(rds)))
 
   def loads(V, base_expr, vdim):
     b = []
@@ -640,17 +701,97 @@ def gen_reduce(root, inputs, classes, kind, op, vec):
     L.append('  }')
     L.append('}')
   else:
-    def body(V):
-      b = []
-      b.append('if (col < I) {')
-      b.append('  for (i64 r = r0 + w * RPW + sub; r < r1; r += 4 * RPW) {')
-      b += ['    ' + x for x in loads(
-          V, lambda s: 'o * a.str[%d][0] + r * a.str[%d][1] + col * a.str[%d][2]' % (s, s, s), 2)]
+    U = unroll or cols_unroll(inputs, classes, vec)
+
+    def one_row(V, rv, sfx, masked):
+      """Loads + (row dots) + accumulator updates of row ``rv`` into names
+      suffixed ``sfx``; split in (load lines, compute lines) so an unrolled
+      body issues every row's loads before the first use."""
+      ld, cp = [], []
+      base = lambda s, c: 'o * a.str[%d][0] + %s * a.str[%d][1] + %s * a.str[%d][2]' % (s, rv, s, c, s)
+      for (s, dt), cls in zip(inputs, classes):
+        ct = ctype(dt)
+        names = ['x%d_%d%s' % (s, j, sfx) for j in range(V)]
+        if s in rowinv:
+          ld += ['%s %s = x%d_%d_ri;' % (ct, n, s, j) for j, n in enumerate(names)]
+          continue
+        srcs, pre = load_srcs(s, dt, cls, V, base(s, 'cc' if masked else 'col'))
+        ld.append('%s %s;' % (ct, ' '.join(names).replace(' ', ', ')))
+        ld.append('{')
+        ld += ['  ' + x for x in pre]
+        # masked lanes load column 0 (always in bounds) and select zero at use
+        ld += ['  %s = %s;' % (n, ('colok ? %s : (%s)0' % (v, ct)) if masked else v) for n, v in zip(names, srcs)]
+        ld.append('}')
+      for rd in rds:
+        ct = ctype(rd.dtype)
+        n = 'rd%d%s' % (rd.rid, sfx)
+        cp.append('%s %s = (%s)0;' % (ct, n, ct))
+        for j in range(V):
+          cp.append('%s = %s + (%s)x%d_%d%s * (%s)x%d_%d%s;' % (n, n, ct, rd.a.slot, j, sfx, ct, rd.w.slot, j, sfx))
+        cp.append('%s = row_allsum(%s, LPR);' % (n, n))
+      upd = []
       for j in range(V):
-        if V > 1:
-          b.append('    ' + _acc_update(op, j, val_j(j), gidx('r')))
-        else:
-          b.append('    ' + _acc_update(op, 0, val_j(0), gidx('r')))
+        call = '(%s)%s' % (act, _call_expr(inputs, j, n_rd=len(rds), sfx=sfx))
+        upd.append(_acc_update(op, j, call, gidx(rv)))
+      if masked:
+        cp.append('if (colok) {')
+        cp += ['  ' + x for x in upd]
+        cp.append('}')
+      else:
+        cp += upd
+      return ld, cp
+
+    def load_srcs(s, dt, cls, V, off):
+      """(per-element source expressions, preamble lines) of one vector load."""
+      ct = ctype(dt)
+      p = '((const GLOBAL %s*)a.ptr[%d])' % (ct, s)
+      pre = ['const i64 off = %s;' % off]
+      if V > 1 and cls == 'c':
+        pre.append('typedef %s __attribute__((ext_vector_type(%d))) vt;' % (ct, V))
+        pre.append('const vt xv = *(const GLOBAL vt*)(%s + off);' % p)
+        return ['xv[%d]' % j for j in range(V)], pre
+      if V > 1 and cls == 'b':
+        pre.append('const %s xb = %s[off];' % (ct, p))
+        return ['xb'] * V, pre
+      if V > 1:
+        pre.append('const i64 s_in = a.str[%d][2];' % s)
+        return ['%s[off + %d * s_in]' % (p, j) for j in range(V)], pre
+      return ['%s[off]' % p], pre
+
+    def body(V):
+      masked = bool(rds)
+      b = []
+      # row-dot kernels: every lane of a row group takes part in the DPP row
+      # sum, so lanes past the last column read column 0 and use zeros
+      b.append('{' if masked else 'if (col < I) {')
+      b.append('  const bool colok = col < I; (void)colok;')
+      b.append('  const i64 cc = colok ? col : 0; (void)cc;')
+      for (s, dt), cls in zip(inputs, classes):
+        if s in rowinv:  # row stride 0: loaded once, outside the row loop
+          ct = ctype(dt)
+          srcs, pre = load_srcs(s, dt, cls, V, 'o * a.str[%d][0] + %s * a.str[%d][2]'
+                                % (s, 'cc' if masked else 'col', s))
+          b.append('  %s %s;' % (ct, ', '.join('x%d_%d_ri' % (s, j) for j in range(V))))
+          b.append('  {')
+          b += ['    ' + x for x in pre]
+          b += ['    x%d_%d_ri = %s;' % (s, j, (('colok ? %s : (%s)0' % (v, ct)) if masked else v))
+                for j, v in enumerate(srcs)]
+          b.append('  }')
+      b.append('  const i64 STEP = 4 * RPW;')
+      b.append('  i64 r = r0 + w * RPW + sub;')
+      if U > 1:
+        b.append('  for (; r + %d * STEP < r1; r += %d * STEP) {' % (U - 1, U))
+        lds, cps = [], []
+        for u in range(U):
+          b.append('    const i64 r_%d = r + %d * STEP;' % (u, u))
+          ld, cp = one_row(V, 'r_%d' % u, '_u%d' % u, masked)
+          lds += ld
+          cps += cp
+        b += ['    ' + x for x in lds + cps]
+        b.append('  }')
+      b.append('  for (; r < r1; r += STEP) {')
+      ld, cp = one_row(V, 'r', '', masked)
+      b += ['    ' + x for x in ld + cp]
       b.append('  }')
       b.append('}')
       return b
@@ -721,6 +862,36 @@ template <typename T> DEV T shfl_xor(T v, int m) {
     u32 lo = shfl_u32((u32)u, m), hi = shfl_u32((u32)(u >> 32), m);
     return __builtin_bit_cast(T, ((u64)hi << 32) | lo);
   }
+}
+'''
+
+
+ROW_ALLSUM = r'''
+// Sum over aligned groups of LPR lanes (LPR a power of two <= 64), result in
+// every lane of the group.  Within a 16-lane DPP row: quad_perm [1,0,3,2],
+// quad_perm [2,3,0,1], row_half_mirror, row_mirror (each step adds a partner
+// holding the mirror-group's equal partial, so all lanes of a group end with
+// the bit-identical sum); across rows: ds_bpermute xor 16 / 32.
+template <int CTRL> DEV u32 dpp_u32(u32 v) {
+  return (u32)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL, typename T> DEV T dpp_mov(T v) {
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, dpp_u32<CTRL>(__builtin_bit_cast(u32, v)));
+  } else {
+    u64 u = __builtin_bit_cast(u64, v);
+    u32 lo = dpp_u32<CTRL>((u32)u), hi = dpp_u32<CTRL>((u32)(u >> 32));
+    return __builtin_bit_cast(T, ((u64)hi << 32) | lo);
+  }
+}
+template <typename T> DEV T row_allsum(T v, i64 LPR) {
+  if (LPR > 1) v = v + dpp_mov<0xB1>(v);
+  if (LPR > 2) v = v + dpp_mov<0x4E>(v);
+  if (LPR > 4) v = v + dpp_mov<0x141>(v);
+  if (LPR > 8) v = v + dpp_mov<0x140>(v);
+  if (LPR > 16) v = v + shfl_xor(v, 16);
+  if (LPR > 32) v = v + shfl_xor(v, 32);
+  return v;
 }
 '''
 

@@ -287,6 +287,72 @@ __global__ __launch_bounds__(256) void k_finalize(int op, int acc_dt, int out_dt
   }
 }
 
+// Many partials per output (a tall column reduce splits R over P ~ 2048
+// blocks, e.g. cfg5's (1e8, 64) gradient): one block per output, threads
+// stride over P in order, then a fixed-shape LDS tree -- deterministic run to
+// run.  Float partials are combined in fp64.
+__global__ __launch_bounds__(256) void k_finalize_wide(int op, int acc_dt, int out_dt, const void* pv,
+                                                       const i64* pi, i64 P, i64 n, void* out,
+                                                       void* out_val) {
+  __shared__ double sv[256];
+  __shared__ i64 si[256];
+  const int t = threadIdx.x;
+  const bool arg = op == SPX_OP_ARGMIN || op == SPX_OP_ARGMAX;
+  const bool fl = is_float_dt(acc_dt);
+  for (i64 i = blockIdx.x; i < n; i += gridDim.x) {
+    double b = 0.0;
+    i64 bi = ARG_EMPTY;
+    bool have = false;
+    for (i64 p = t; p < P; p += 256) {
+      if (arg) {
+        double v = ld_f(pv, acc_dt, p * n + i);
+        i64 vi = pi[p * n + i];
+        if (vi != ARG_EMPTY && (bi == ARG_EMPTY || arg_better(op, v, vi, b, bi))) { b = v; bi = vi; }
+      } else if (fl) {
+        double v = ld_f(pv, acc_dt, p * n + i);
+        b = have ? comb_f(op, b, v) : v;
+      } else {
+        i64 v = ld_i(pv, acc_dt, p * n + i);
+        bi = have ? comb_i(op, bi, v) : v;
+      }
+      have = true;
+    }
+    sv[t] = b;
+    si[t] = bi;
+    __syncthreads();
+    // lanes with no partial (P < 256) hold have=false: they are skipped by
+    // letting the tree only combine slots < min(P, 256)
+    const int m = P < 256 ? (int)P : 256;
+    for (int h = 128; h > 0; h >>= 1) {
+      if (t < h && t + h < m) {
+        if (arg) {
+          if (si[t + h] != ARG_EMPTY && (si[t] == ARG_EMPTY || arg_better(op, sv[t + h], si[t + h], sv[t], si[t]))) {
+            sv[t] = sv[t + h];
+            si[t] = si[t + h];
+          }
+        } else if (fl) {
+          sv[t] = comb_f(op, sv[t], sv[t + h]);
+        } else {
+          si[t] = comb_i(op, si[t], si[t + h]);
+        }
+      }
+      __syncthreads();
+    }
+    if (t == 0) {
+      if (arg) {
+        ((i64*)out)[i] = si[0];
+        if (out_val) st_f(out_val, acc_dt, i, sv[0]);
+      } else if (fl) {
+        if (is_float_dt(out_dt)) st_f(out, out_dt, i, sv[0]);
+        else st_i(out, out_dt, i, (i64)sv[0]);
+      } else {
+        st_i(out, out_dt, i, si[0]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 extern "C" int spx_reduce_finalize(int op, int acc_dtype, int out_dtype, const void* part_val,
                                    const int64_t* part_idx, int64_t P, int64_t n, void* out,
                                    void* out_val, void* stream) {
@@ -297,8 +363,12 @@ extern "C" int spx_reduce_finalize(int op, int acc_dtype, int out_dtype, const v
   if (n == 0) return SPX_OK;
   if ((op == SPX_OP_ARGMIN || op == SPX_OP_ARGMAX) && !part_idx)
     return set_err(SPX_EINVAL, "spx_reduce_finalize: arg op needs part_idx");
-  k_finalize<<<grid_for(n), 256, 0, S(stream)>>>(op, acc_dtype, out_dtype, part_val, part_idx, P, n,
-                                                 out, out_val);
+  if (P >= 32 && n <= 16384)
+    k_finalize_wide<<<(unsigned)(n < 4096 ? n : 4096), 256, 0, S(stream)>>>(op, acc_dtype, out_dtype, part_val,
+                                                                            part_idx, P, n, out, out_val);
+  else
+    k_finalize<<<grid_for(n), 256, 0, S(stream)>>>(op, acc_dtype, out_dtype, part_val, part_idx, P, n,
+                                                   out, out_val);
   LAUNCH_CHECK("spx_reduce_finalize");
   return SPX_OK;
 }

@@ -98,6 +98,22 @@ class LocalReduceExpr(FnCallExpr):
   _op_type = 'reduce'
 
 
+def rowdot(a, w):
+  """Host meaning of a fused ``dot(x, w)`` leaf (dot_map2_np_mapper,
+  spartan/expr/dot.py:172-187): ``a`` an (n, K) tile, ``w`` the (1, K) row
+  vector of the host (K, 1) operand.  Only ever lowered, never called on the
+  product path."""
+  return a.dot(w.reshape(-1, 1))
+
+
+class LocalRowDot(LocalMapExpr):
+  """``dot(x, w)`` with a small host ``w`` folded into a fused tree
+  (DotReduceFusion): deps = [x input, (1, K) w input]."""
+
+  def __init__(self, deps=None):
+    super().__init__(fn=rowdot, deps=deps, pretty_fn='rowdot')
+
+
 # ---------------------------------------------------------------- lowering
 class Pre(codegen.In):
   """A generator leaf (rand / arange ...) materialised into a tile by spx_fill
@@ -146,6 +162,11 @@ def lower(op, env):
   if not isinstance(op, FnCallExpr):
     raise CodegenError('cannot lower %r' % (op,))
   fn = op.fn
+  if isinstance(op, LocalRowDot):
+    a, w = (lower(d, env) for d in op.deps)
+    if not isinstance(a, codegen.In) or not isinstance(w, codegen.In):
+      raise CodegenError('row dot operands must be tile inputs')
+    return codegen.RowDot(a, w)
   if fn in _BUILTIN_LOWERINGS:
     return _BUILTIN_LOWERINGS[fn](op, env)
   deps = [d for d in op.deps if not (isinstance(d, LocalInput) and d.idx == 'extent')]

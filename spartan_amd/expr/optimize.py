@@ -7,9 +7,11 @@ ReduceMapFusion (:185-222), in the reference's registration order
 kernel.  ParakeetGeneration is replaced by that codegen; AutomaticTiling and
 RotateSlice are later-round items.
 """
+import numpy as np
+
 from ..config import FLAGS
 from .base import AsArray, Expr, ListExpr, Val, expr_like, lazify
-from .local import LocalInput, LocalMapLocationExpr, LocalReduceExpr, make_var
+from .local import FnCallExpr, LocalInput, LocalMapLocationExpr, LocalReduceExpr, LocalRowDot, make_var
 from .map import MapExpr
 from .ndarray import NdArrayExpr
 from .reduce import ReduceExpr
@@ -103,6 +105,83 @@ class ReduceMapFusion(OptimizePass):
     return expr_like(expr, children=ListExpr(vals=new_children), child_to_var=new_vars, op=combined)
 
 
+ROWDOT_MAX_K = 64  # one lane group of the column-reduce kernel holds a whole row
+
+
+def _subst(op, var, repl):
+  """Copy of a LocalExpr tree with every LocalInput(var) replaced by ``repl``."""
+  if isinstance(op, LocalInput):
+    return repl if op.idx == var else op
+  new = op.__class__.__new__(op.__class__)
+  new.__dict__.update(op.__dict__)
+  new.deps = [_subst(d, var, repl) for d in op.deps]
+  return new
+
+
+class DotReduceFusion(OptimizePass):
+  """reduce(f(x, dot(x, w)), axis=0) with a small host (K, 1) operand ``w``
+  -> one fused kernel that reads ``x`` once.
+
+  The reference evaluates ``dot(x, w)`` as its own pass (dot_map2_np_mapper,
+  spartan/expr/dot.py:172-187), materialising yp, and the map+reduce that
+  consumes it reads ``x`` again (linear_regression.py:10-16: ``x * (yp - y)``
+  summed over axis 0).  When the DotExpr feeds a fused axis-0 reduction over
+  an (N, K) iteration space and its left operand is that same (N, K) array,
+  the dot is replaced by a ``rowdot(x, w)`` leaf evaluated row by row inside
+  the reduction kernel (codegen.RowDot).  Applied only when every row fits one
+  lane group (2 <= K <= 64) and x, w share a float dtype; otherwise the DAG is
+  left unchanged."""
+  name = 'dot_fusion'
+
+  def visit_ReduceExpr(self, expr):
+    from .dot import DotExpr
+    children = self.visit(expr.children)
+    expr = expr_like(expr, children=children)
+    if expr.axis not in (0, -2) or not isinstance(expr.op, LocalReduceExpr):
+      return expr
+    shapes = [tuple(c.shape) for c in children]
+    if any(len(s) > 2 for s in shapes) or max(len(s) for s in shapes) != 2:
+      return expr
+    it_shape = tuple(max(s[i - 2 + len(s)] if i - 2 + len(s) >= 0 else 1 for s in shapes) for i in range(2))
+    vals, vars_ = list(children), list(expr.child_to_var)
+    op = expr.op
+    changed = False
+    for i in range(len(vals)):
+      d = vals[i]
+      if not isinstance(d, DotExpr) or getattr(d, 'tile_hint', None) is not None:
+        continue
+      w, a = d.matrix_b, d.matrix_a
+      if not isinstance(w, np.ndarray) or w.ndim != 2 or w.shape[1] != 1:
+        continue
+      K = w.shape[0]
+      if not (2 <= K <= ROWDOT_MAX_K) or tuple(a.shape) != it_shape or it_shape[1] != K:
+        continue
+      if w.dtype.kind != 'f' or np.dtype(a.dtype) != w.dtype:
+        continue
+      var_a = None
+      for c, v in zip(vals, vars_):
+        if c is a or (isinstance(c, Expr) and c.expr_id == a.expr_id):
+          var_a = v
+          break
+      if var_a is None:
+        var_a = make_var()
+        vals.append(a)
+        vars_.append(var_a)
+      var_w = make_var()
+      vals.append(AsArray(val=np.ascontiguousarray(w.reshape(1, K))))
+      vars_.append(var_w)
+      op = _subst(op, vars_[i], LocalRowDot(deps=[LocalInput(var_a), LocalInput(var_w)]))
+      vals[i] = None
+      changed = True
+    if not changed:
+      return expr
+    keep = [(c, v) for c, v in zip(vals, vars_) if c is not None]
+    # the driving (N, K) input first: dtype_fn reads children[0]
+    keep.sort(key=lambda cv: tuple(cv[0].shape) != it_shape)
+    return expr_like(expr, children=ListExpr(vals=[c for c, _ in keep]),
+                     child_to_var=[v for _, v in keep], op=op)
+
+
 class CollapsedCachedExpressions(OptimizePass):
   """Replace already-evaluated nodes by their value."""
   name = 'collapse_cached'
@@ -114,7 +193,7 @@ class CollapsedCachedExpressions(OptimizePass):
     return expr.visit(self)
 
 
-PASSES = [CollapsedCachedExpressions, MapMapFusion, ReduceMapFusion]
+PASSES = [CollapsedCachedExpressions, MapMapFusion, ReduceMapFusion, DotReduceFusion]
 
 
 def optimize(dag):

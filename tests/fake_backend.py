@@ -34,6 +34,10 @@ def eval_ir(node, arrays, shape):
   if isinstance(node, codegen.Cast):
     v = eval_ir(node.arg, arrays, shape)
     return np.asarray(v).astype(node.dtype)
+  if isinstance(node, codegen.RowDot):
+    a = np.asarray(eval_ir(node.a, arrays, shape), dtype=node.dtype)
+    w = np.asarray(eval_ir(node.w, arrays, shape), dtype=node.dtype)
+    return np.broadcast_to(a.dot(w[0].reshape(-1, 1)), shape)
   args = []
   for a, dt in zip(node.args, node.in_dtypes):
     v = eval_ir(a, arrays, shape)

@@ -62,3 +62,21 @@ def test_generated_source_is_deterministic():
   a = codegen.gen_reduce(root, ins, ['c'] * 3, 'cols', 'sum', 4)
   b = codegen.gen_reduce(root, ins, ['c'] * 3, 'cols', 'sum', 4)
   assert a == b and backend.source_key(a) == backend.source_key(b)
+
+
+@pytest.mark.parametrize('dt', [F32, F64])
+def test_rowdot_cols_compile(dt):
+  """DotReduceFusion's row-dot leaf in the column-reduce skeleton (vector and
+  scalar paths), and its refusal in the other skeletons."""
+  from spartan_amd.codegen import RowDot
+  x, yv, w = In(0, dt), In(1, dt), In(2, dt)
+  root = Op('multiply', [x, Op('subtract', [RowDot(x, w), yv])])
+  ins = [(0, dt), (1, dt), (2, dt)]
+  for V in (codegen.vec_width([dt]), 1):
+    src = codegen.gen_reduce(root, ins, ['c', 'b', 'c'], 'cols', 'sum', V)
+    assert 'row_allsum(rd0' in src
+    _compile(src)
+  with pytest.raises(NotImplementedError):
+    codegen.gen_reduce(root, ins, ['c', 'b', 'c'], 'rows', 'sum', 1)
+  with pytest.raises(NotImplementedError):
+    codegen.gen_map(root, ins, ['c', 'b', 'c'], 2, 1, False)

@@ -365,6 +365,31 @@ def test_lreg_cfg5_small(ex, W):
   check_fp(g, cpu, exact, 1e-5)
 
 
+@pytest.mark.parametrize('K,dt', [(64, np.float32), (48, np.float32), (5, np.float32), (2, np.float32),
+                                  (64, np.float64), (33, np.float64)])
+@pytest.mark.parametrize('W', [1, 3])
+def test_dot_reduce_fusion(ex, K, dt, W):
+  """DotReduceFusion: sum(x * (dot(x, w) - y), axis=0) runs as ONE generated
+  column-reduce kernel with the row dot inside (DPP row sums); K not a power
+  of two exercises the zero-filled lanes, K=5 fp32 / K=33 fp64 the unaligned
+  scalar path.  Tolerances: as the CPU result (1e-5 fp32, 1e-12 fp64)."""
+  from spartan_amd.expr.dot import DotExpr
+  expr, setw = ex
+  setw(W)
+  n = 7001
+  X = rng.rand((n, K), 41, dt) - dt(0.5)
+  Yv = rng.rand((n, 1), 42, dt)
+  w = rng.rand((K, 1), 43, dt) - dt(0.25)
+  x, y = expr.from_numpy(X), expr.from_numpy(Yv)
+  e = expr.sum(x * (expr.dot(x, w) - y), axis=0).optimized()
+  assert not any(isinstance(c, DotExpr) for c in e.children)
+  got = e.glom()
+  exact = (X.astype(np.float64) * (X.astype(np.float64) @ w.astype(np.float64) - Yv)).sum(0)
+  yp = np.concatenate([X[ex[0][0]:ex[1][0]].dot(w) for ex, _ in O.compute_extents(X.shape, W)])
+  cpu = O.sum_tiles(X * (yp - Yv), 0, W)
+  check_fp(got, cpu, exact, 1e-5 if dt == np.float32 else 1e-12)
+
+
 # ---------------------------------------------- short rows (packed kernel)
 @pytest.mark.parametrize('R', [1, 3, 64, 77, 256, 1000, 4096, 5000])
 def test_short_rows(ex, R):

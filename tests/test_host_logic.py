@@ -149,3 +149,36 @@ def test_kmeans_driver_host(host_ctx):
     c2, l2 = OW.kmeans_fit(pts, 5, 3, W)
     np.testing.assert_allclose(c, c2, rtol=1e-6)
     np.testing.assert_array_equal(labels.glom(), l2)
+
+
+def test_dot_reduce_fusion_rewrites_lreg(host_ctx):
+  """DotReduceFusion folds dot(x, w_host) into the axis-0 reduction of
+  x * (dot(x, w) - y): one ReduceExpr, no DotExpr left, same gradient."""
+  host_ctx(2)
+  from spartan_amd import expr
+  from spartan_amd.config import FLAGS
+  from spartan_amd.expr.dot import DotExpr
+  from spartan_amd.expr.reduce import ReduceExpr
+  n, d = 300, 16
+  X = rng.rand((n, d), 41, np.float32)
+  Yv = rng.rand((n, 1), 42, np.float32)
+  w = rng.rand((d, 1), 43, np.float32)
+  x, y = expr.from_numpy(X), expr.from_numpy(Yv)
+  g = expr.sum(x * (expr.dot(x, w) - y), axis=0)
+  opt = g.optimized()
+  assert isinstance(opt, ReduceExpr)
+  assert not any(isinstance(c, DotExpr) for c in opt.children)
+  assert 'rowdot' in opt.op.pretty_str()
+  got = opt.glom()
+  want = (X * (X.dot(w) - Yv)).sum(0)
+  np.testing.assert_allclose(got, want, rtol=1e-5)
+  # not applied: axis 1, a wide w, or the flag off
+  for e in (expr.sum(x * (expr.dot(x, w) - y), axis=1),
+            expr.sum(x * expr.dot(x, np.ones((d, 1), np.float64)), axis=0)):
+    assert any(isinstance(c, DotExpr) for c in e.optimized().children)
+  FLAGS.opt_dot_fusion = False
+  try:
+    e = expr.sum(x * (expr.dot(x, w) - y), axis=0).optimized()
+    assert any(isinstance(c, DotExpr) for c in e.children)
+  finally:
+    FLAGS.opt_dot_fusion = True
