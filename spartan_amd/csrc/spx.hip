@@ -1018,91 +1018,141 @@ __global__ __launch_bounds__(256) void k_kmeans_prep(i64 D, i64 K, i64 Kp, const
 // replacing kmeans_center_mapper / kmeans_count_mapper (k_means_.py:61-89,
 // which sum in fp32; fp64 here is at least as exact).  No float atomics and a
 // fixed summation order, so the result is deterministic:
-//   k_kmeans_accum    persistent 1024-lane blocks; block (x, y) owns the fp64
-//                     accumulator tile of KA_CB centres x 64 columns picked by
-//                     y (128 KB of LDS) and the point chunks x, x+G, ...  Wave
-//                     w owns the centres c == w (mod 16) of the tile, lane =
-//                     column.  Chunks of rows are prefetched into a register
-//                     ring KA_STAGES chunks deep and staged in LDS; every wave ballots the
-//                     chunk's labels and adds its own points' rows, in point
-//                     order, with plain LDS read-modify-writes (one owner per
-//                     accumulator: no atomics).  The tile is written once to
-//                     the block's partial slot.
+//   k_kmeans_accum    persistent 1024-lane blocks; block (x, y) covers the
+//                     centre tile of KA_CB = 16 waves x KA_CPW centres and the
+//                     64 columns picked by y, over the point chunks x, x+G, ...
+//                     Wave w owns the centres c == w (mod 16) of the tile and
+//                     keeps their fp64 sums in registers (lane = column): the
+//                     centre of a point is wave-uniform, so adding a row is an
+//                     indexed-register add (s_set_gpr_idx), no LDS
+//                     read-modify-write (fp64 LDS RMW traffic bounded the
+//                     LDS-accumulator design at ~16 ms for cfg3,
+//                     tools/ka_tune.hip).  Chunks are prefetched with 16-byte
+//                     loads (one per lane: dword loads cap a 1-block-per-CU
+//                     stream at ~2.2 TB/s) into a register ring KA_STAGES deep
+//                     and staged in LDS, double-buffered (one barrier per
+//                     chunk).  Every wave adds its own points in point order:
+//                     the sums are deterministic, no atomics.  The tile is
+//                     written once to the block's partial slot.
 //   k_kmeans_reduce   out[i] (+)= sum over g of part[g][i]: four fixed g
 //                     slices per output, combined in a fixed order.
 constexpr int KA_THREADS = 1024;
 constexpr int KA_DB = 64;                  // columns per tile = lanes per wave
-constexpr int KA_CB = 16384 / KA_DB;       // centres per tile (128 KB of fp64)
 constexpr int KA_WAVES = KA_THREADS / 64;  // centre owners per tile
+constexpr int KA_CPW = 16;                 // centres per wave (register sums)
+constexpr int KA_CB = KA_WAVES * KA_CPW;   // centres per tile
 constexpr int KA_STAGES = 4;               // register prefetch ring depth
+constexpr int KA_UNROLL = 4;               // points whose LDS reads are issued together
 
 template <typename TP>
-__global__ __launch_bounds__(KA_THREADS) void k_kmeans_accum(i64 N, i64 D, i64 K, const TP* __restrict__ P, i64 ldp,
+__global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_kmeans_accum(i64 N, i64 D, i64 K, const TP* __restrict__ P, i64 ldp,
                                                              const i64* __restrict__ labels, double* __restrict__ psum,
                                                              unsigned long long* __restrict__ pcnt, int ndb) {
-  constexpr int CH = 16384 / (KA_DB * (int)sizeof(TP)) < 64 ? 16384 / (KA_DB * (int)sizeof(TP)) : 64;
-  constexpr int PF = CH * KA_DB / KA_THREADS;  // prefetched elements per lane per chunk
-  constexpr int ST = KA_STAGES;                // chunks in flight per block
-  __shared__ double acc[KA_CB * KA_DB];
-  __shared__ TP xs[CH * KA_DB];
-  __shared__ int lab_s[CH];
-  __shared__ unsigned int cnt[KA_CB];
+  constexpr int VE = 16 / (int)sizeof(TP);                // elements per 16-byte load
+  constexpr int CH = KA_THREADS * VE / KA_DB;             // points per chunk (64 f32 / 32 f64)
+  constexpr int LPR = KA_DB / VE;                         // lanes per row slice
+  constexpr int ST = KA_STAGES;
+  typedef TP V __attribute__((ext_vector_type(VE)));
+  __shared__ TP xs[2][ST][CH * KA_DB];
+  __shared__ int lab_s[2][ST][CH];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int cb = blockIdx.y / ndb, db = blockIdx.y % ndb;
   const i64 c0 = (i64)cb * KA_CB, d0 = (i64)db * KA_DB;
   const i64 nch = (N + CH - 1) / CH;
-  for (int i = t; i < KA_CB * KA_DB; i += KA_THREADS) acc[i] = 0.0;
-  for (int i = t; i < KA_CB; i += KA_THREADS) cnt[i] = 0;
-  TP pf[ST][PF];
-  int plab[ST];
-  auto load = [&](int s, i64 ch) {
-    if (ch >= nch) return;
-    const i64 p0 = ch * CH;
+  // this lane's slice of a chunk: point lp, columns d0 + lc .. + VE
+  const int lp = t / LPR, lc = (t % LPR) * VE;
+  // 16-byte loads need the slice inside the row and aligned; else per element
+  const bool vec = d0 + lc + VE <= D && (ldp % VE) == 0 && ((uintptr_t)P % 16) == 0;
+  // padding slots of a partial unrolled step add +0.0 (exact: a sum that
+  // starts at +0.0 never becomes -0.0) and no count to centre slot 0
+  double acc[KA_CPW];
 #pragma unroll
-    for (int k = 0; k < PF; ++k) {
-      const int e = t + KA_THREADS * k, p = e / KA_DB, d = e % KA_DB;
-      pf[s][k] = (p0 + p < N && d0 + d < D) ? P[(p0 + p) * ldp + d0 + d] : TP(0);
+  for (int j = 0; j < KA_CPW; ++j) acc[j] = 0.0;
+  // counts: integer LDS atomics at staging time (order-free, hence exact and
+  // deterministic), kept by the db == 0 blocks
+  __shared__ unsigned int cnt_s[KA_CB];
+  for (int i = t; i < KA_CB; i += KA_THREADS) cnt_s[i] = 0u;
+  // Prefetch ring: loads use clamped (always valid) addresses and nothing
+  // consumes them until the stage comes round again -- a use right after the
+  // issue would make the compiler wait for the whole ring (vmcnt(0)).
+  V pf[ST];
+  i64 plab[ST];
+  auto load = [&](int s, i64 ch) {
+    const i64 p0 = (ch < nch ? ch : nch - 1) * CH;
+    const i64 pr = p0 + lp < N ? p0 + lp : N - 1;
+    if (vec) {
+      pf[s] = *(const V*)(P + pr * ldp + d0 + lc);
+    } else {
+#pragma unroll
+      for (int j = 0; j < VE; ++j) {
+        const i64 d = d0 + lc + j < D ? d0 + lc + j : D - 1;
+        pf[s][j] = P[pr * ldp + d];
+      }
     }
-    plab[s] = -1;
-    if (t < CH) {
-      const i64 l = p0 + t < N ? labels[p0 + t] : -1;
-      plab[s] = (l >= c0 && l < K && l - c0 < KA_CB) ? (int)(l - c0) : -1;
-    }
+    if (t < CH) plab[s] = labels[p0 + t < N ? p0 + t : N - 1];
   };
   const i64 G = gridDim.x;
 #pragma unroll
   for (int s = 0; s < ST; ++s) load(s, blockIdx.x + s * G);
+  int buf = 0;
+  // one barrier per ST chunks: the waves' uneven shares of a chunk's points
+  // (labels mod 16) even out over ST chunks
   for (i64 base = blockIdx.x; base < nch; base += ST * G) {
+    // stage into xs[buf]: its last reads (ST chunks ago) happened before
+    // every wave passed the previous barrier
 #pragma unroll
     for (int s = 0; s < ST; ++s) {
-      const i64 ch = base + s * G;
-      if (ch >= nch) break;  // block-uniform
-      __syncthreads();       // previous chunk consumed (and the zeroing done)
+      const i64 p0 = (base + s * G) * CH;
+      const bool prow = p0 + lp < N;
 #pragma unroll
-      for (int k = 0; k < PF; ++k) xs[t + KA_THREADS * k] = pf[s][k];
-      if (t < CH) lab_s[t] = plab[s];
-      __syncthreads();
-      load(s, ch + ST * G);  // refill this stage: ST chunks stay in flight
-      const int r = lane < CH ? lab_s[lane] : -1;
-      unsigned long long m = __ballot(r >= 0 && (r % KA_WAVES) == w);
-      while (m) {
-        const int p = __ffsll((long long)m) - 1;
-        m &= m - 1;
-        const int rr = __shfl(r, p, 64);
-        acc[rr * KA_DB + lane] += (double)xs[p * KA_DB + lane];
-        if (lane == 0) cnt[rr] += 1u;
+      for (int j = 0; j < VE; ++j)
+        xs[buf][s][lp * KA_DB + lc + j] = (prow && d0 + lc + j < D) ? pf[s][j] : TP(0);
+      if (t < CH) {
+        const i64 l = plab[s];
+        const int lr = (p0 + t < N && l >= c0 && l < K && l - c0 < KA_CB) ? (int)(l - c0) : -1;
+        lab_s[buf][s][t] = lr;
+        if (db == 0 && lr >= 0) atomicAdd(&cnt_s[lr], 1u);
       }
     }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < ST; ++s) load(s, base + (s + ST) * G);  // the next ST chunks fly meanwhile
+#pragma unroll
+    for (int s = 0; s < ST; ++s) {
+      const int r = lane < CH ? lab_s[buf][s][lane] : -1;
+      unsigned long long m = __ballot(r >= 0 && (r % KA_WAVES) == w);
+      while (m) {  // wave-uniform
+        int jj[KA_UNROLL];
+        double xx[KA_UNROLL];
+#pragma unroll
+        for (int q = 0; q < KA_UNROLL; ++q) {
+          int p = 0;
+          bool ok = false;
+          jj[q] = 0;
+          if (m) {
+            p = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            jj[q] = __builtin_amdgcn_readlane(r, p) / KA_WAVES;
+            ok = true;
+          }
+          xx[q] = ok ? (double)xs[buf][s][p * KA_DB + lane] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < KA_UNROLL; ++q) acc[jj[q]] += xx[q];  // in point order
+      }
+    }
+    buf ^= 1;
+  }
+  const i64 g = blockIdx.x, d = d0 + lane;
+#pragma unroll
+  for (int j = 0; j < KA_CPW; ++j) {
+    const i64 c = c0 + (i64)j * KA_WAVES + w;
+    if (c < K && d < D) psum[(g * K + c) * D + d] = acc[j];
   }
   __syncthreads();
-  const i64 g = blockIdx.x;
-  for (int i = t; i < KA_CB * KA_DB; i += KA_THREADS) {
-    const i64 c = c0 + i / KA_DB, d = d0 + i % KA_DB;
-    if (c < K && d < D) psum[(g * K + c) * D + d] = acc[i];
-  }
   if (db == 0)
     for (int i = t; i < KA_CB; i += KA_THREADS)
-      if (c0 + i < K) pcnt[g * K + c0 + i] = cnt[i];
+      if (c0 + i < K) pcnt[g * K + c0 + i] = cnt_s[i];
 }
 
 // 256 lanes = 64 outputs x 4 g-slices; slice s sums g = s, s+4, ... in order,
@@ -1130,7 +1180,7 @@ __global__ __launch_bounds__(256) void k_kmeans_reduce(i64 n, i64 G, const T* __
 
 // Grid of the accumulation for (N, D, K): x = G point-chunk streams, y = tiles.
 static void ka_grid(int dtype, i64 N, i64 D, i64 K, i64* G, i64* ndb, i64* ncb) {
-  const i64 ch = dtype == SPX_F32 ? 64 : 32;
+  const i64 ch = dtype == SPX_F32 ? 64 : 32;  // points per chunk (k_kmeans_accum CH)
   *ndb = (D + KA_DB - 1) / KA_DB;
   *ncb = (K + KA_CB - 1) / KA_CB;
   const i64 nch = (N + ch - 1) / ch;
