@@ -948,40 +948,394 @@ struct KfConf {
 #endif
 typedef KF_PROD KfProd;
 
+// ---------------------------------------------------------------------------
+// bf16x3 certified filter (fp32 points, K <= 256, D % 64 == 0, D <= 128).
+// The fp32 filter above runs v_mfma_f32_32x32x2_f32 at the fp32 rate (1/16
+// of bf16).  Here every fp32 operand is split exactly-enough into two bf16
+// terms, x = xh + xl + rx with xh = bf16(x), xl = bf16(x - xh), |rx| <=
+// 2^-18 |x|, and p.c is taken as ph.ch + ph.cl + pl.ch: three
+// v_mfma_f32_32x32x16_bf16 per 32x32x16 block, 16/3 x the fp32 MFMA rate.
+// Rigorous bound on |S - p.c| (S the computed dot product):
+//   2^-24 |p||c|             centre fp64 -> fp32 rounding;
+//   3.1 * 2^-18 |p||c|       the neglected pl.cl, rp.c and ph.rc terms
+//                            (Cauchy-Schwarz over the elementwise bounds);
+//   2 (48 G + D/(16 G) + 3) 2^-24 |p||c|  fp32 accumulation: the 48 G
+//                            exact products per output of G = KB_GRP k-steps
+//                            are summed into a fresh accumulator (an fma chain
+//                            of 48 G) that is then added to the running sum
+//                            (D/(16 G) adds; VALU adds out of the MFMA result,
+//                            so G trades bound for issue slots); a factor 2
+//                            covers directed rounding inside the MFMA;
+//   1e-28 D (1 + |c|)^2      bf16 / fp32 underflow of the small terms;
+// and the decision is the fp32 filter's: a'(p, c) = fl(|c|^2 - 2 S), a point
+// is labelled here iff best and second-best a' differ by more than 2e.  The
+// rest (near-ties; non-finite values) get exactly scipy's order as before:
+// the candidate centres (a' <= best + 2e, natural mask layout: bit b of word
+// w <-> centre 32 w + b) through k_kmeans_cand, non-finite points through
+// the all-centre exact kernel.  Labels are bit-identical to the exact kernel.
+// Layout: persistent blocks of KB_WAVES waves, one per CU (the split
+// centres, 2 x 32 NCT x (D + 8) bf16, stay resident in LDS; rows padded by
+// 16 B so the 32 lanes' ds_read_b128 of a B fragment are conflict-free);
+// wave = 32 points x all 32 NCT centres (NCT accumulator tiles of 16
+// registers); A fragments are loaded straight from global memory (lane
+// (r, h) holds point r's dims 8h..8h+7 of the 16-dim k-step: row-major
+// points ARE the A operand layout) through a 4-deep register ring; the
+// epilogue reduces each point's top two across the 32 lanes of its half with
+// xor-shuffles.
+constexpr int KB_WAVES = 4;
+constexpr int KB_DMAX = 128;
+constexpr int KB_GRP = 4;  // k-steps per fresh accumulator (divides 4)
+typedef __bf16 kb_bf8 __attribute__((ext_vector_type(8)));
+typedef float kb_acc __attribute__((ext_vector_type(16)));
+typedef float kb_f4 __attribute__((ext_vector_type(4)));
+
+// CBh / CBl[c][d]: bf16 split of (float)C[c][d] (zero past K); cnf[c] =
+// (float)|C[c]|^2 (+inf past K); *cmax = max_c |C[c]| (one block).
+__global__ __launch_bounds__(256) void k_kmeans_prep_b3(i64 D, i64 K, i64 Kp, const double* __restrict__ C,
+                                                        __bf16* __restrict__ CBh, __bf16* __restrict__ CBl,
+                                                        float* __restrict__ cnf, double* __restrict__ cmax) {
+  __shared__ double red[256];
+  double mx = 0.0;
+  for (i64 c = threadIdx.x; c < Kp; c += 256) {
+    double s = 0.0;
+    for (i64 d = 0; d < D; ++d) {
+      const double v = c < K ? C[c * D + d] : 0.0;
+      const float v32 = (float)v;
+      const __bf16 hi = (__bf16)v32;
+      CBh[c * D + d] = hi;
+      CBl[c * D + d] = (__bf16)(v32 - (float)hi);
+      s += v * v;
+    }
+    // padding centres: a huge FINITE |c|^2 (the filter tags a' mantissa bits,
+    // which would turn +inf into NaN); they never win, and a lone real centre
+    // is certified against them
+    cnf[c] = c < K ? (float)s : 3.0e38f;
+    if (c < K) mx = (s > mx || s != s) ? s : mx;
+  }
+  red[threadIdx.x] = mx;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      const double a = red[threadIdx.x], b = red[threadIdx.x + o];
+      red[threadIdx.x] = (b > a || b != b) ? b : a;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *cmax = sqrt(red[0]) * 1.001;
+}
+
+static size_t kb_lds_bytes(i64 D, int nct) { return (size_t)2 * 32 * nct * (D + 8) * 2 + (size_t)32 * nct * 4; }
+
+template <int NCT>
+__global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D, const float* __restrict__ P, i64 ldp,
+                                                                    const __bf16* __restrict__ CBh,
+                                                                    const __bf16* __restrict__ CBl,
+                                                                    const float* __restrict__ cnf, const double* cmax_p,
+                                                                    i64* __restrict__ labels,
+                                                                    unsigned int* __restrict__ counters,
+                                                                    i64* __restrict__ full_list,
+                                                                    KfCand* __restrict__ cand_list) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char kb_lds[];
+  constexpr int NC = 32 * NCT;
+  const int Dp = (int)D + 8;
+  __bf16* Bh = (__bf16*)kb_lds;
+  __bf16* Bl = Bh + NC * Dp;
+  float* cns = (float*)(Bl + NC * Dp);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, h = lane >> 5;
+  {
+    const int D8 = (int)D / 8;
+    for (int i = t; i < NC * D8; i += KB_WAVES * 64) {
+      const int c = i / D8, d = (i % D8) * 8;
+      *(kb_bf8*)&Bh[c * Dp + d] = *(const kb_bf8*)&CBh[(i64)c * D + d];
+      *(kb_bf8*)&Bl[c * Dp + d] = *(const kb_bf8*)&CBl[(i64)c * D + d];
+    }
+    for (int i = t; i < NC; i += KB_WAVES * 64) cns[i] = cnf[i];
+  }
+  __syncthreads();
+  float cnr[NCT];  // |c|^2 of this lane's centre in every tile
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) cnr[ct] = cns[ct * 32 + r];
+  const double cmax = *cmax_p;
+  const double u32 = 5.9604644775390625e-08;
+  const int KS = (int)D / 16;
+  const double eS =
+      (u32 + 3.1 * 3.814697265625e-06 + 2.0 * (48.0 * KB_GRP + (double)(KS / KB_GRP) + 3.0) * u32) * 1.01 * cmax;
+  const i64 ntiles = (N + 31) / 32;
+  const i64 stride = (i64)gridDim.x * KB_WAVES;
+  i64 tile = (i64)blockIdx.x * KB_WAVES + w;
+  // A ring: 4 k-steps in flight, addresses clamped into the array
+  kb_f4 ra[4][2];
+  auto load = [&](int s, i64 tl, int ks) {
+    i64 row = tl * 32 + r;
+    row = row < N ? row : N - 1;
+    const float* p = P + row * ldp + ks * 16 + 8 * h;
+    ra[s][0] = *(const kb_f4*)p;
+    ra[s][1] = *(const kb_f4*)(p + 4);
+  };
+#pragma unroll
+  for (int s = 0; s < 4; ++s) load(s, tile, s);
+  for (; tile < ntiles; tile += stride) {
+    kb_acc acc[NCT];
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) acc[ct] = (kb_acc){};
+    float p2 = 0.f;
+    for (int ks0 = 0; ks0 < KS; ks0 += 4) {
+#pragma unroll
+      for (int g0 = 0; g0 < 4; g0 += KB_GRP) {
+        kb_bf8 ah[KB_GRP], al[KB_GRP];
+#pragma unroll
+        for (int g = 0; g < KB_GRP; ++g) {
+          const int s = g0 + g, ks = ks0 + s;
+          float x[8];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            x[j] = ra[s][0][j];
+            x[j + 4] = ra[s][1][j];
+          }
+          {
+            int nks = ks + 4;
+            i64 ntl = tile;
+            if (nks >= KS) {
+              nks -= KS;
+              ntl += stride;
+            }
+            load(s, ntl, nks);
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            p2 += x[j] * x[j];
+            ah[g][j] = (__bf16)x[j];
+            al[g][j] = (__bf16)(x[j] - (float)ah[g][j]);
+          }
+        }
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) {
+          // the 48 KB_GRP products per output of KB_GRP k-steps go into a
+          // fresh accumulator that is then added to the running sum: the
+          // rounding bound is that chain + D / (16 KB_GRP) adds instead of
+          // one 3D-long chain
+          kb_acc tk = (kb_acc){};
+#pragma unroll
+          for (int g = 0; g < KB_GRP; ++g) {
+            const int ko = (ks0 + g0 + g) * 16 + 8 * h;
+            const kb_bf8 bh = *(const kb_bf8*)&Bh[(ct * 32 + r) * Dp + ko];
+            const kb_bf8 bl = *(const kb_bf8*)&Bl[(ct * 32 + r) * Dp + ko];
+            tk = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[g], bh, tk, 0, 0, 0);
+            tk = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[g], bl, tk, 0, 0, 0);
+            tk = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[g], bh, tk, 0, 0, 0);
+          }
+          acc[ct] += tk;
+        }
+      }
+    }
+    p2 += __shfl_xor(p2, 32, 64);  // row r's |p|^2 in lanes r and r + 32
+    // ---- epilogue.  Register reg of tile ct holds S(row rt(reg, h), centre
+    // 32 ct + r), rt = (reg&3) + 8(reg>>2) + 4h.
+    // (A) per register: a' = fl(|c|^2 - 2S) with the tile index ct written
+    // into the 3 low mantissa bits (a <= 7-ulp perturbation, priced into the
+    // bound below; the exact winner only matters once the gap certifies it),
+    // then the two smallest over the NCT tiles by a min / med3 network.
+    float lo[16], sec[16];
+    int li[16];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      float v[NCT];
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        const float a = __builtin_fmaf(-2.f, acc[ct][reg], cnr[ct]);
+        v[ct] = __builtin_bit_cast(float, (__builtin_bit_cast(unsigned int, a) & ~7u) | (unsigned int)ct);
+      }
+      float l = v[0], s2 = INFINITY;
+      if constexpr (NCT >= 2) {
+        float pl[NCT / 2], ps[NCT / 2];
+#pragma unroll
+        for (int k = 0; k < NCT / 2; ++k) {
+          pl[k] = fminf(v[2 * k], v[2 * k + 1]);
+          ps[k] = fmaxf(v[2 * k], v[2 * k + 1]);
+        }
+#pragma unroll
+        for (int n = NCT / 2; n > 1; n >>= 1) {
+#pragma unroll
+          for (int k = 0; k < n / 2; ++k) {
+            const float a0 = pl[2 * k], a1 = pl[2 * k + 1];
+            ps[k] = __builtin_amdgcn_fmed3f(a0, a1, fminf(ps[2 * k], ps[2 * k + 1]));
+            pl[k] = fminf(a0, a1);
+          }
+        }
+        l = pl[0];
+        s2 = ps[0];
+      }
+      lo[reg] = l;
+      sec[reg] = s2;
+      li[reg] = r;
+    }
+    // (B) across the 32 lanes of each half, halving the registers per lane at
+    // every step (xor 16, 8, 4, 2: a lane keeps the half its lane bit picks and
+    // sends the other), then xor 1 between the two lanes holding one row.  Lane
+    // (h, r) ends with register q = r >> 1, i.e. row rt(q, h), over all centres.
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const int n = 8 >> st;  // pairs this step
+      const int o = 16 >> st;
+      const bool up = (lane & o) != 0;
+#pragma unroll
+      for (int k = 0; k < n; ++k) {
+        const float sl = up ? lo[k] : lo[k + n], ss = up ? sec[k] : sec[k + n];
+        const int si = up ? li[k] : li[k + n];
+        const float kl = up ? lo[k + n] : lo[k], ks2 = up ? sec[k + n] : sec[k];
+        const int ki = up ? li[k + n] : li[k];
+        const float ol = __shfl_xor(sl, o, 64), os = __shfl_xor(ss, o, 64);
+        const int oi = __shfl_xor(si, o, 64);
+        sec[k] = __builtin_amdgcn_fmed3f(kl, ol, fminf(ks2, os));
+        li[k] = ol < kl ? oi : ki;
+        lo[k] = fminf(kl, ol);
+      }
+    }
+    {
+      const float ol = __shfl_xor(lo[0], 1, 64), os = __shfl_xor(sec[0], 1, 64);
+      const int oi = __shfl_xor(li[0], 1, 64);
+      sec[0] = __builtin_amdgcn_fmed3f(lo[0], ol, fminf(sec[0], os));
+      li[0] = (ol < lo[0] || (ol == lo[0] && oi < li[0])) ? oi : li[0];
+      lo[0] = fminf(lo[0], ol);
+    }
+    // (C) one decision per row, by the even lane of its pair
+    const int q = r >> 1;
+    const int rt = (q & 3) + 8 * (q >> 2) + 4 * h;
+    const i64 grow = tile * 32 + rt;
+    const float b1 = lo[0], b2 = sec[0];
+    const int i1 = 32 * (int)(__builtin_bit_cast(unsigned int, b1) & 7u) + li[0];
+    const float p2f = __shfl(p2, rt, 64);
+    const double pp2 = (double)p2f * 1.001 + (double)D * 2e-45;
+    const double pn = sqrt(pp2) * 1.0001;
+    // a' magnitudes are at most cmax^2 + 2 |p| cmax: the 7-ulp index tag adds
+    // 2 * 8 * 2^-23 of that to the gap test
+    const double amax = cmax * cmax + 2.0 * pn * cmax;
+    const double e = 2.0 * eS * pn + 2.02 * u32 * (cmax * cmax + pn * cmax) +
+                     1e-28 * (double)D * (1.0 + cmax) * (1.0 + cmax) + 1e-8 * (pp2 + cmax * cmax) +
+                     8.0 * 1.1920928955078125e-07 * amax + 1e-300;
+    const bool live = grow < N && (r & 1) == 0;
+    // finite point, no overflow possible in S or a' (every a' then finite)
+    const bool fin = isfinite(p2f) && isfinite(e) && pn * cmax < 1e36 && cmax * cmax < 1e36 &&
+                     isfinite(b1) && isfinite(b2);
+    const bool dec = fin && (double)b2 - (double)b1 > 2.0 * e;
+    if (live && dec) labels[grow] = i1;
+    if (live && !fin) full_list[atomicAdd(&counters[0], 1u)] = grow;
+    // undecided rows: one slot each (one atomic per wave), then per register
+    // q holding such a row, the masks of the centres with a' <= b1 + 2e by
+    // ballots (e prices the index tags in: every centre that can be the
+    // exact argmin is kept)
+    const bool needc = live && fin && !dec;
+    const unsigned long long und = __ballot(needc);
+    if (und) {  // wave-uniform
+      unsigned int base = 0;
+      if (lane == 0) base = atomicAdd(&counters[1], (unsigned int)__popcll(und));
+      base = __builtin_amdgcn_readfirstlane(base);
+      const unsigned int myslot = base + (unsigned int)__popcll(und & ((1ull << lane) - 1ull));
+      if (needc) cand_list[myslot].row = grow;
+      const double thr = (double)b1 + 2.0 * e;
+#pragma unroll
+      for (int qq = 0; qq < 16; ++qq) {
+        const bool n0 = (und >> (2 * qq)) & 1ull, n1 = (und >> (32 + 2 * qq)) & 1ull;
+        if (n0 || n1) {  // wave-uniform
+          const double tq = __shfl(thr, 2 * qq + 32 * h, 64);
+          const unsigned int s0 = __builtin_amdgcn_readlane(myslot, 2 * qq);
+          const unsigned int s1 = __builtin_amdgcn_readlane(myslot, 32 + 2 * qq);
+#pragma unroll
+          for (int ct = 0; ct < 8; ++ct) {
+            unsigned long long m = 0;
+            if (ct < NCT) {
+              const float a = __builtin_fmaf(-2.f, acc[ct < NCT ? ct : 0][qq], cnr[ct < NCT ? ct : 0]);
+              m = __ballot((double)a <= tq);
+            }
+            if (n0 && lane == ct) cand_list[s0].mask[ct] = (unsigned int)m;
+            if (n1 && lane == 32 + ct) cand_list[s1].mask[ct] = (unsigned int)(m >> 32);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int NCT>
+static void kb_launch(hipStream_t s, i64 N, i64 D, const float* P, i64 ldp, const __bf16* CBh, const __bf16* CBl,
+                      const float* cnf, const double* cmax, i64* labels, unsigned int* counters, i64* full_list,
+                      KfCand* cand_list, int grid) {
+  const size_t lds = kb_lds_bytes(D, NCT);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_kmeans_filter_b3<NCT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kb_lds_bytes(KB_DMAX, 8));
+    attr = true;
+  }
+  k_kmeans_filter_b3<NCT><<<grid, KB_WAVES * 64, lds, s>>>(N, D, P, ldp, CBh, CBl, cnf, cmax, labels, counters,
+                                                           full_list, cand_list);
+}
+
 // Exact-order labels of the undecided points from their candidate masks
 // (K <= 256); equal distances go to the lower index (= first occurrence).
-template <typename TP>
+// Eight lanes per point: in round j lane s takes the (8 j + s)-th candidate,
+// so the sequential fp64 d-loops of up to 8 candidates run side by side
+// (one lane per point serialised them); then a (distance, index) min over
+// the 8 lanes.
+// NATURAL: bit k of word w <-> centre 32 w + k (bf16x3 filter); else centre
+// w + 8 k (fp32 filter).
+template <typename TP, bool NATURAL>
 __global__ __launch_bounds__(256) void k_kmeans_cand(i64 D, const TP* __restrict__ P, i64 ldp,
                                                      const double* __restrict__ C, i64* __restrict__ labels,
                                                      const unsigned int* __restrict__ counters,
                                                      const KfCand* __restrict__ cand_list) {
   const i64 n = counters[1];
-  for (i64 q = (i64)blockIdx.x * 256 + threadIdx.x; q < n; q += (i64)gridDim.x * 256) {
+  const int sub = threadIdx.x & 7;
+  const i64 step = ((i64)gridDim.x * 256) >> 3;
+  for (i64 q = ((i64)blockIdx.x * 256 + threadIdx.x) >> 3; q < n; q += step) {  // uniform per 8 lanes
     const i64 row = cand_list[q].row;
+    unsigned int mw[8];
+    int tot = 0;
+#pragma unroll
+    for (int wd = 0; wd < 8; ++wd) {
+      mw[wd] = cand_list[q].mask[wd];
+      tot += __popc(mw[wd]);
+    }
     const TP* x = P + row * ldp;
     double best = 0.0;
     int bi = -1;
-    for (int wd = 0; wd < 8; ++wd) {
-      unsigned int m = cand_list[q].mask[wd];
-      while (m) {
-        const int k = __ffs(m) - 1;
-        m &= m - 1;
-        const int c = wd + 8 * k;
-        const double* cc = C + (i64)c * D;
-        double acc = 0.0;
-        for (i64 d = 0; d < D; ++d) {
-          const double df = (double)x[d] - cc[d];
-          const double sq = df * df;
-          acc = acc + sq;
-        }
-        const double dist = sqrt(acc);
-        if (bi < 0 || dist < best || (dist == best && c < bi)) {
-          best = dist;
-          bi = c;
+    for (int j = 0; 8 * j < tot; ++j) {  // uniform per 8 lanes
+      int nth = 8 * j + sub, c = -1;
+#pragma unroll
+      for (int wd = 0; wd < 8; ++wd) {
+        const int pc = __popc(mw[wd]);
+        if (c < 0 && nth < pc) {
+          unsigned int m = mw[wd];
+          for (int k = 0; k < nth; ++k) m &= m - 1;
+          const int b = __ffs(m) - 1;
+          c = NATURAL ? 32 * wd + b : wd + 8 * b;
+        } else if (c < 0) {
+          nth -= pc;
         }
       }
+      const double* cc = C + (i64)(c < 0 ? 0 : c) * D;
+      double acc = 0.0;
+      for (i64 d = 0; d < D; ++d) {
+        const double df = (double)x[d] - cc[d];
+        const double sq = df * df;
+        acc = acc + sq;
+      }
+      const double dist = sqrt(acc);
+      if (c >= 0 && (bi < 0 || dist < best || (dist == best && c < bi))) {
+        best = dist;
+        bi = c;
+      }
     }
-    labels[row] = bi;
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+      const double ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (oi >= 0 && (bi < 0 || ob < best || (ob == best && oi < bi))) {
+        best = ob;
+        bi = oi;
+      }
+    }
+    if (sub == 0) labels[row] = bi;
   }
 }
 
@@ -1240,6 +1594,40 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
   ws += N * 8;
   KfCand* cand_list = (KfCand*)ws;
   HIP_TRY(hipMemsetAsync(counters, 0, 2 * sizeof(unsigned int), S(stream)));
+  const int gp = kf_persistent_grid(N);
+  if (dtype == SPX_F32 && Kp == KF_BN && D % 64 == 0 && D <= KB_DMAX && ldp % 4 == 0 &&
+      ((uintptr_t)points % 16) == 0) {
+    // bf16x3 filter; the split centres reuse the CT area (2 x 2 B <= 4 B per element)
+    const int nct = K <= 32 ? 1 : K <= 64 ? 2 : K <= 128 ? 4 : 8;
+    __bf16* CBh = (__bf16*)CT;
+    __bf16* CBl = CBh + (i64)32 * nct * D;
+    float* cnf = (float*)cn;
+    k_kmeans_prep_b3<<<1, 256, 0, S(stream)>>>(D, K, 32 * nct, centers, CBh, CBl, cnf, cmax);
+    LAUNCH_CHECK("spx_kmeans_assign(prep)");
+    static int ncu = 0;
+    if (!ncu) {
+      int dev = 0;
+      HIP_TRY(hipGetDevice(&dev));
+      HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const i64 ntiles = (N + 31) / 32;
+    const i64 need_blocks = (ntiles + KB_WAVES - 1) / KB_WAVES;
+    const int grid = (int)(need_blocks < ncu ? need_blocks : ncu);
+    const float* Pf = (const float*)points;
+    switch (nct) {
+      case 1: kb_launch<1>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, grid); break;
+      case 2: kb_launch<2>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, grid); break;
+      case 4: kb_launch<4>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, grid); break;
+      default: kb_launch<8>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, grid); break;
+    }
+    LAUNCH_CHECK("spx_kmeans_assign(filter bf16x3)");
+    k_kmeans_cand<float, true><<<gp, 256, 0, S(stream)>>>(D, Pf, ldp, centers, labels, counters, cand_list);
+    LAUNCH_CHECK("spx_kmeans_assign(candidates)");
+    k_kmeans_assign<float><<<gp, 256, 0, S(stream)>>>(N, D, K, Pf, ldp, centers, labels, nullptr, full_list,
+                                                       counters);
+    LAUNCH_CHECK("spx_kmeans_assign(exact)");
+    return SPX_OK;
+  }
   k_kmeans_prep<<<1, 256, 0, S(stream)>>>(D, K, Kp, centers, CT, cn, cmax);
   LAUNCH_CHECK("spx_kmeans_assign(prep)");
   const i64 gf = (N + KfProd::BM - 1) / KfProd::BM;
@@ -1254,13 +1642,12 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
                                   cand_list);
   }
   LAUNCH_CHECK("spx_kmeans_assign(filter)");
-  const int gp = kf_persistent_grid(N);
   if (Kp == KF_BN) {
     if (dtype == SPX_F32)
-      k_kmeans_cand<float><<<gp, 256, 0, S(stream)>>>(D, (const float*)points, ldp, centers, labels, counters,
+      k_kmeans_cand<float, false><<<gp, 256, 0, S(stream)>>>(D, (const float*)points, ldp, centers, labels, counters,
                                                        cand_list);
     else
-      k_kmeans_cand<double><<<gp, 256, 0, S(stream)>>>(D, (const double*)points, ldp, centers, labels, counters,
+      k_kmeans_cand<double, false><<<gp, 256, 0, S(stream)>>>(D, (const double*)points, ldp, centers, labels, counters,
                                                         cand_list);
     LAUNCH_CHECK("spx_kmeans_assign(candidates)");
   }

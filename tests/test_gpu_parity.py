@@ -526,3 +526,38 @@ def test_kmeans_assign_certified_bit_exact(ex, kind, dt):
   be.kmeans_assign(P, Cd, slow, exact_only=True)
   np.testing.assert_array_equal(slow.cpu().numpy(), want)
   np.testing.assert_array_equal(fast.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize('D', [64, 128])
+@pytest.mark.parametrize('K', [1, 7, 32, 33, 100, 256])
+def test_kmeans_bf16x3_filter_bit_exact(ex, D, K):
+  """The bf16x3-MFMA certified filter (fp32 points, K <= 256, D % 64 == 0):
+  labels bit-identical to the all-exact fp64 kernel (scipy cdist order, ties
+  -> first index) on uniform data, exact duplicate centres, equidistant
+  points, a ragged last tile, and rows that must take the non-finite path
+  (NaN, 1e30)."""
+  import torch
+  from oracle import workloads as OW
+  from spartan_amd import backend
+  be = backend.get()
+  g = np.random.default_rng(D * 1000 + K)
+  n = 20011
+  pts = g.random((n, D)).astype(np.float32)
+  centers = pts[g.choice(n, K, replace=False)].astype(np.float64)
+  if K >= 4:
+    centers[K - 1] = centers[0]                                   # duplicate centre
+    pts[5] = ((centers[1] + centers[2]) / 2).astype(np.float32)   # near-equidistant
+    pts[6] = centers[3].astype(np.float32)                        # on a centre
+  pts[7] = np.nan
+  pts[8, 3] = 1e30
+  pts[9] = -pts[10]
+  P = torch.as_tensor(pts).cuda()
+  C = torch.as_tensor(centers).cuda()
+  fast = torch.empty(n, dtype=torch.int64, device='cuda')
+  exact = torch.empty(n, dtype=torch.int64, device='cuda')
+  be.kmeans_assign(P, C, fast)
+  be.kmeans_assign(P, C, exact, exact_only=True)
+  f, e = fast.cpu().numpy(), exact.cpu().numpy()
+  np.testing.assert_array_equal(f, e)
+  ok = np.isfinite(pts).all(1)
+  np.testing.assert_array_equal(f[ok][:3000], OW.kmeans_assign(pts[ok][:3000], centers))
