@@ -201,7 +201,7 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
          'gemm_form_tflops': round(2.0 * n * K * D / el / 1e12, 2),
          'gemm_form_mfma_f32_frac_per_gpu': round(2.0 * n * K * D / el / 1e12 / (157.3 * ctx.world_size), 4),
          'config': 'cfg3: %d x %d fp32 points (U[0,1), seed 21) per GPU, k=%d, centres = first %d points; '
-                   'assign = fp32-MFMA certified filter + exact-order fp64 recompute of undecided points '
+                   'assign = bf16x3-MFMA certified filter + exact-order fp64 recompute of undecided points '
                    '(bit-exact labels), fp64 centroid sums' % (npts, D, K, K)}
   del X, labels
   torch.cuda.empty_cache()

@@ -80,6 +80,21 @@ def _body(rank, world, port, W, q):
     np.testing.assert_allclose(expr.dot(expr.from_numpy(a), b).glom(), a @ b, rtol=1e-12)
     v = rng.rand((36,), 3, np.float64)
     np.testing.assert_allclose(expr.dot(expr.from_numpy(a), expr.from_numpy(v)).glom(), a @ v, rtol=1e-12)
+
+    # drivers over ranks: lreg (DotReduceFusion + all-reduce of the gradient)
+    # and k-means (row-strip assign + all-reduced sums / counts)
+    from spartan_amd import workloads
+    from oracle import workloads as OW
+    Xl = rng.rand((300, 16), 41, np.float32)
+    Yl = rng.rand((300, 1), 42, np.float32)
+    wl = rng.rand((16, 1), 43, np.float32)
+    got = workloads.linear_regression_update(expr.from_numpy(Xl), expr.from_numpy(Yl), wl, 1e-3)
+    np.testing.assert_allclose(got, OW.linear_regression_update(Xl, Yl, wl, 1e-3, W), rtol=1e-5)
+    pts = rng.rand((600, 8), 21, np.float32)
+    c, lab = workloads.kmeans_fit(expr.from_numpy(pts), 5, 2)
+    c2, l2 = OW.kmeans_fit(pts, 5, 2, W)
+    np.testing.assert_allclose(c, c2, rtol=1e-6)
+    np.testing.assert_array_equal(lab.glom(), l2)
     q.put((rank, 'ok'))
   except Exception as e:  # pragma: no cover - reported to the parent
     import traceback
