@@ -176,6 +176,19 @@ int spx_kmeans_accumulate(int dtype, int64_t N, int64_t D, int64_t K, const void
                           const int64_t* labels, double* sums, uint64_t* counts, int zero_first,
                           void* workspace, size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------------ automatic tiling */
+/* Host-only (no device work, callable without a GPU): the node choice on the
+ * AutomaticTiling cost graph (spartan/expr/optimize.py:454-890), replacing
+ * the reference's native `tiling.mincost_tiling` (spartan/expr/tiling.cc:
+ * 94-132, choice procedure :31-92).  Nodes 0..t, 0 = source, t = sink;
+ * edge i is eu[i] -> ev[i] with cost ecost[i] (elements moved), in insertion
+ * order; split pair k = {su[k], sv[k]} (the row / column alternatives of one
+ * expression).  On return chosen[u] (u < t) is 1 for the chosen nodes and
+ * *total_cost (may be NULL) holds the cost.  -1 on a malformed graph. */
+int spx_mincost_tiling(int32_t t, int64_t n_edges, const int32_t* eu, const int32_t* ev, const int64_t* ecost,
+                       int64_t n_split, const int32_t* su, const int32_t* sv, uint8_t* chosen,
+                       int64_t* total_cost);
+
 #ifdef __cplusplus
 }
 #endif

@@ -94,6 +94,9 @@ _SIGS = {
     'spx_kmeans_accumulate': ([ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                                ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p], ctypes.c_int),
+    'spx_mincost_tiling': ([ctypes.c_int32, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
+                            ctypes.POINTER(ctypes.c_int32), _I64P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
+                            ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_uint8), _I64P], ctypes.c_int),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -115,6 +118,28 @@ def load_library(path=LIB_PATH):
       fn.restype = res
     _lib = lib
     return lib
+
+
+def mincost_tiling(t, edges, split_pairs):
+  """spx_mincost_tiling (host code in libspx.so, no GPU needed): the node
+  choice of the AutomaticTiling cost graph.  edges: [(u, v, cost)] in
+  insertion order; split_pairs: [(a, b)].  Returns (chosen node ids < t,
+  total cost)."""
+  lib = load_library()
+  n = len(edges)
+  I32 = ctypes.c_int32
+  eu = (I32 * max(n, 1))(*[int(e[0]) for e in edges])
+  ev = (I32 * max(n, 1))(*[int(e[1]) for e in edges])
+  ec = (ctypes.c_int64 * max(n, 1))(*[int(e[2]) for e in edges])
+  m = len(split_pairs)
+  su = (I32 * max(m, 1))(*[int(p[0]) for p in split_pairs])
+  sv = (I32 * max(m, 1))(*[int(p[1]) for p in split_pairs])
+  chosen = (ctypes.c_uint8 * max(int(t), 1))()
+  total = ctypes.c_int64(0)
+  rc = lib.spx_mincost_tiling(int(t), n, eu, ev, ec, m, su, sv, chosen, ctypes.byref(total))
+  if rc != 0:
+    raise ValueError('spx_mincost_tiling: malformed tiling graph')
+  return [u for u in range(int(t)) if chosen[u]], int(total.value)
 
 
 def _arr(vals):
