@@ -333,6 +333,8 @@ def gather_regions(array, requests):
   """Collective: deliver ``region`` of ``array`` to rank ``dst`` for every
   (region, dst) in ``requests`` (identical list on every rank).  Returns
   {request index: device tensor} for the requests addressed to this rank."""
+  if hasattr(array, 'gather'):  # a view (array/views.py): the same exchange on its base
+    return array.gather(requests)
   import torch
   ctx = runtime.get()
   be = backend.get()

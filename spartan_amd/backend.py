@@ -283,8 +283,8 @@ class HipBackend:
       return
     slots = sorted(inputs)
     ins = [(s, np_dtype(inputs[s].dtype)) for s in slots]
-    strides = [broadcast_strides(tuple(inputs[s].shape), shape) for s in slots]
-    dense = all(tuple(inputs[s].shape) == shape for s in slots)
+    strides = [broadcast_strides(tuple(inputs[s].shape), shape, inputs[s].stride()) for s in slots]
+    dense = all(tuple(inputs[s].shape) == shape and inputs[s].is_contiguous() for s in slots)
     V = codegen.vec_width([dt for _, dt in ins] + [root.dtype])
     args = codegen.KArgs()
     _scalars_into(root, args)
@@ -325,8 +325,14 @@ class HipBackend:
     import torch
     slots = sorted(inputs)
     ins = [(s, np_dtype(inputs[s].dtype)) for s in slots]
-    strides = [broadcast_strides(tuple(inputs[s].shape), in_shape) for s in slots]
+    strides = [broadcast_strides(tuple(inputs[s].shape), in_shape, inputs[s].stride()) for s in slots]
     view = reduce_view(in_shape, strides, axis)
+    if view is None and any(not inputs[s].is_contiguous() for s in slots):
+      # a strided view whose dims do not collapse to (O, R, I): make the
+      # views dense (identity-map kernel) and take the plain path
+      inputs = {s: self.contiguous(t) for s, t in inputs.items()}
+      strides = [broadcast_strides(tuple(inputs[s].shape), in_shape) for s in slots]
+      view = reduce_view(in_shape, strides, axis)
     if view is None:
       raise NotImplementedError('reduction view not coalescible; materialise the map first')
     O, R, I, vstr = view
@@ -446,6 +452,23 @@ class HipBackend:
           ctypes.c_void_p(result.data_ptr()), ctypes.c_void_p(res_v.data_ptr() if arg else 0),
           self.stream()), 'spx_reduce_finalize')
     return (res_v, result) if arg else result
+
+  def contiguous(self, t, dtype=None):
+    """Dense copy of a strided view (and/or dtype conversion) by the generated
+    identity-map kernel; ``t`` itself when nothing is to be done."""
+    import torch
+    src_dt = np_dtype(t.dtype)
+    dst_dt = np.dtype(dtype) if dtype is not None else src_dt
+    if t.is_contiguous() and dst_dt == src_dt:
+      return t
+    out = torch.empty(tuple(t.shape), dtype=torch_dtype(dst_dt), device=t.device)
+    if t.numel() == 0:
+      return out
+    root = codegen.In(0, src_dt)
+    if dst_dt != src_dt:
+      root = codegen.Cast(root, dst_dt)
+    self.map(root, {0: t}, out)
+    return out
 
   # ------------------------------------------------------------ finalize
   def argcombine(self, op, vals, idx):

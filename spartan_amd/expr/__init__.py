@@ -9,6 +9,9 @@ from .dot import dot
 from .map import map
 from .ndarray import ndarray
 from .reduce import reduce
+from .reshape import reshape
+from .slice import slice_expr
+from .transpose import transpose
 from .write_array import from_numpy
 
 Expr.sum = sum

@@ -187,7 +187,13 @@ class Expr:
   def __xor__(self, o): return _map(self, o, fn=np.logical_xor)
 
   def __getitem__(self, idx):
-    raise NotImplementedError('slicing views are a later-round item (SURVEY.md 8(f) rank 2)')
+    from .slice import slice_expr
+    return slice_expr(self, idx)
+
+  @property
+  def T(self):
+    from .transpose import transpose
+    return transpose(self)
 
   def __setitem__(self, k, v):
     raise Exception('Expressions are read-only.')

@@ -107,13 +107,9 @@ class _As2D:
 
 
 def _as_dtype(t, dt):
-  import torch
-  tdt = backend.torch_dtype(dt)
-  if t.dtype == tdt:
-    return t.contiguous()
-  out = torch.empty(tuple(t.shape), dtype=tdt, device=t.device)
-  backend.get().copy_region(out, (0,) * t.dim(), t.contiguous(), (0,) * t.dim(), tuple(t.shape))
-  return out
+  """Dense ``dt`` tensor of ``t`` (a strided view, e.g. a transpose, is made
+  dense by the identity-map kernel; GEMM operands are row-major)."""
+  return backend.get().contiguous(t, dt)
 
 
 SKINNY_N = 4
@@ -132,7 +128,7 @@ def _skinny(at, bk, dtype):
   be = backend.get()
   cols = []
   for j in range(n):
-    bj = bk[:, j].contiguous().reshape(1, K)
+    bj = bk[:, j].reshape(1, K)  # a strided column: the kernel reads it in place
     cols.append(be.reduce(root, 'sum', {0: at, 1: bj}, (R, K), 1, (R,), dt))
   if n == 1:
     return cols[0].reshape(R, 1)
@@ -165,7 +161,7 @@ def run_dot(a, b, tile_hint=None):
         partials[ex2] = _skinny(at, bk, dtype)
       else:
         ct = torch.empty((ex2.shape[0], N), dtype=backend.torch_dtype(dtype), device=ctx.device)
-        be.gemm(at, bk.contiguous(), ct, 1.0, 0.0)
+        be.gemm(at, be.contiguous(bk), ct, 1.0, 0.0)
         partials[ex2] = ct
     return _combine_rows(partials, A, M, N, out_shape, dtype, tile_hint, k_split=any(
         ex.ul[1] != 0 or ex.lr[1] != K for ex in A.tiles2()))

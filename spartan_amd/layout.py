@@ -20,18 +20,22 @@ def contiguous_strides(shape):
   return st
 
 
-def broadcast_strides(in_shape, out_shape):
-  """Strides (elements) of a contiguous ``in_shape`` tensor viewed as ``out_shape``."""
+def broadcast_strides(in_shape, out_shape, in_strides=None):
+  """Strides (elements) of an ``in_shape`` tensor viewed as ``out_shape``.
+  ``in_strides``: the tensor's own element strides (a strided view such as a
+  transpose, consumed in place by the generated kernels); default contiguous."""
   in_shape = tuple(int(s) for s in in_shape)
   out_shape = tuple(int(s) for s in out_shape)
+  own = list(in_strides) if in_strides is not None else contiguous_strides(in_shape)
   if len(in_shape) > len(out_shape):
     # leading size-1 dims may be dropped
     extra = len(in_shape) - len(out_shape)
     assert all(s == 1 for s in in_shape[:extra]), (in_shape, out_shape)
     in_shape = in_shape[extra:]
+    own = own[extra:]
   pad = len(out_shape) - len(in_shape)
   full = (1,) * pad + in_shape
-  cst = [0] * pad + contiguous_strides(in_shape)
+  cst = [0] * pad + [int(x) for x in own]
   out = []
   for d, (si, so) in enumerate(zip(full, out_shape)):
     if si == so:

@@ -77,6 +77,10 @@ class FakeBackend:
     _put(out, v.reshape(shape))
     self.calls.append('fill')
 
+  def contiguous(self, t, dtype=None):
+    out = t.contiguous()
+    return out if dtype is None else out.to(B.torch_dtype(dtype))
+
   def map(self, root, inputs, out):
     shape = tuple(out.shape)
     arrays = {s: _np(t) for s, t in inputs.items()}

@@ -95,6 +95,11 @@ def _body(rank, world, port, W, q):
     c2, l2 = OW.kmeans_fit(pts, 5, 2, W)
     np.testing.assert_allclose(c, c2, rtol=1e-6)
     np.testing.assert_array_equal(lab.glom(), l2)
+    # views over ranks: slice / transpose / reshape pieces gathered across ranks
+    from test_views import _views_cases
+    for name, e, want in _views_cases(expr):
+      got = e.glom()
+      np.testing.assert_allclose(np.asarray(got).reshape(np.shape(want)), want, rtol=1e-12, err_msg=name)
     q.put((rank, 'ok'))
   except Exception as e:  # pragma: no cover - reported to the parent
     import traceback

@@ -561,3 +561,18 @@ def test_kmeans_bf16x3_filter_bit_exact(ex, D, K):
   np.testing.assert_array_equal(f, e)
   ok = np.isfinite(pts).all(1)
   np.testing.assert_array_equal(f[ok][:3000], OW.kmeans_assign(pts[ok][:3000], centers))
+
+
+# ---------------------------------------------- views: slice / transpose / reshape
+@pytest.mark.parametrize('W', [1, 3])
+def test_views_gpu(ex, W):
+  """The reference's test_slice / test_transpose / test_reshape cases through
+  the gfx950 kernels: slices and transposes are zero-copy views whose pieces
+  the generated kernels read in place (transposes as strided operands);
+  reshape is one gather + copy-region pass."""
+  from test_views import _views_cases
+  expr, setw = ex
+  setw(W)
+  for name, e, want in _views_cases(expr):
+    got = e.glom()
+    np.testing.assert_allclose(np.asarray(got).reshape(np.shape(want)), want, rtol=1e-12, err_msg=name)
