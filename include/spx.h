@@ -55,6 +55,7 @@ extern "C" {
 #define SPX_FILL_CONST 0   /* value a                                   */
 #define SPX_FILL_ARANGE 1  /* a + b * global_flat_index                 */
 #define SPX_FILL_UNIFORM 2 /* a + (b-a) * U[0,1) from splitmix64(seed,i) */
+#define SPX_FILL_NORMAL 3  /* a + b * N(0,1), Box-Muller of streams 2i, 2i+1 */
 
 /* ---------------------------------------------------------------- basics */
 int spx_abi_version(void);

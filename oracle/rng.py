@@ -39,6 +39,23 @@ def uniform_values(g, seed, low, high, dtype):
   return np.floor(low + (high - low) * u).astype(dtype)
 
 
+def normal_values(g, seed, loc, scale, dtype):
+  """loc + scale * N(0,1): Box-Muller over streams 2g (u1 in (0,1]) and
+  2g+1, in fp64 (libm log/cos: within a few ulp of the device's, not bit-exact)."""
+  g = np.asarray(g, dtype=np.uint64)
+  u1 = ((raw(np.uint64(2) * g, seed) >> np.uint64(11)) + np.uint64(1)).astype(np.float64) * (2.0 ** -53)
+  u2 = (raw(np.uint64(2) * g + np.uint64(1), seed) >> np.uint64(11)).astype(np.float64) * (2.0 ** -53)
+  z = np.sqrt(-2.0 * np.log(u1)) * np.cos(6.283185307179586 * u2)
+  v = loc + scale * z
+  dtype = np.dtype(dtype)
+  return v.astype(dtype) if dtype.kind == 'f' else np.floor(v).astype(dtype)
+
+
+def randn(shape, seed, dtype=np.float64):
+  n = int(np.prod(shape))
+  return normal_values(np.arange(n, dtype=np.uint64), seed, 0.0, 1.0, dtype).reshape(shape)
+
+
 def arange_values(g, start, step, dtype):
   dtype = np.dtype(dtype)
   g = np.asarray(g, dtype=np.int64)

@@ -18,6 +18,7 @@ import numpy as np
 from .. import backend, comm, runtime
 from ..util import prod
 from . import extent as ext
+from . import transfer
 from .tile import Tile, merge, reducer_name
 
 DEFAULT_TILE_SIZE = 100000
@@ -158,11 +159,19 @@ class DistArrayImpl(DistArray):
     (DistArrayImpl.update, distarray.py:370-421)."""
     import torch
     ctx = runtime.get()
+    op = reducer_name(reducer if reducer is not None else self.reducer_fn)
     if not isinstance(data, torch.Tensor):
-      data = torch.as_tensor(np.ascontiguousarray(np.asarray(data, dtype=self.dtype))).to(ctx.device)
+      # host data: only the pieces that land on this rank's tiles cross PCIe
+      host = np.asarray(data, dtype=self.dtype)
+      assert host.shape == tuple(region.shape) or host.size == region.size, (host.shape, region)
+      host = host.reshape(region.shape) if region.ndim else host.reshape(())
+      for ex, inter in ext.find_overlapping(self.tiles, region):
+        if ex in self.local:
+          piece = host[_rel_slice(inter, region)] if region.ndim else host
+          merge(self.local[ex], inter, transfer.upload(piece, ctx.device), op)
+      return
     assert tuple(data.shape) == tuple(region.shape) or data.numel() == region.size, (data.shape, region)
     data = data.reshape(region.shape) if region.ndim else data.reshape(())
-    op = reducer_name(reducer if reducer is not None else self.reducer_fn)
     be = backend.get()
     for ex, inter in ext.find_overlapping(self.tiles, region):
       if ex not in self.local:
@@ -214,7 +223,7 @@ class LocalWrapper(DistArray):
   def device_data(self):
     if self._dev is None:
       import torch
-      self._dev = torch.as_tensor(np.ascontiguousarray(self._data)).to(runtime.get().device)
+      self._dev = transfer.upload(self._data, runtime.get().device)
     return self._dev
 
   def fetch(self, region):
@@ -258,7 +267,7 @@ class ReplicatedArray(LocalWrapper):
     return self.glom()
 
   def glom(self):
-    return self._dev.cpu().numpy()
+    return transfer.download(self._dev)
 
 
 def as_array(data):
@@ -296,14 +305,13 @@ def from_tiles(shape, dtype, tiles, local_data, reducer=None):
 
 def from_numpy(arr, tile_hint=None):
   """Upload a host array; each rank copies its own tiles (write_array.py:411-433)."""
-  import torch
   arr = np.asarray(arr)
   backend.spx_dtype(arr.dtype)
   out = create(arr.shape, arr.dtype, tile_hint=tile_hint)
   dev = runtime.get().device
   for ex, tile in out.local.items():
     piece = arr[ex.to_slice()] if ex.ndim else arr
-    tile.data = torch.as_tensor(np.ascontiguousarray(piece)).to(dev)
+    tile.data = transfer.upload(piece, dev)
     tile.written = [ex]
   return out
 
@@ -311,6 +319,10 @@ def from_numpy(arr, tile_hint=None):
 # ---------------------------------------------------------------- movement
 def _rel(inner, outer):
   return tuple(a - b for a, b in zip(inner.ul, outer.ul))
+
+
+def _rel_slice(inner, outer):
+  return tuple(slice(u - o, l - o) for u, l, o in zip(inner.ul, inner.lr, outer.ul))
 
 
 def _sub_tensor(tile, region):
@@ -392,7 +404,7 @@ def glom(array):
     if ctx.distributed:
       t = t.contiguous()
       comm.broadcast(t, owner)
-    result[ex.to_slice()] = t.cpu().numpy()
+    transfer.download(t, result[ex.to_slice()])
   return result
 
 
@@ -404,4 +416,4 @@ def glom_region(array, region):
     return full[region.to_slice()] if region.ndim else full
   ctx = runtime.get()
   got = gather_regions(array, [(region, r) for r in range(ctx.world_size)])
-  return got[ctx.rank].cpu().numpy().reshape(region.shape)
+  return transfer.download(got[ctx.rank]).reshape(region.shape)

@@ -109,10 +109,10 @@ def merge(tile, region, update, reducer_op):
   else:
     if tile.mask is None:
       import torch
-      tile.mask = torch.zeros(tile.shape, dtype=torch.uint8, device=tile.data.device)
+      tile.mask = torch.zeros(tile.shape, dtype=torch.bool, device=tile.data.device)
       for w in tile.written:
         wl = tuple(a - b for a, b in zip(w.ul, t_ex.ul))
-        ones = torch.ones(w.shape, dtype=torch.uint8, device=tile.data.device)
+        ones = torch.ones(w.shape, dtype=torch.bool, device=tile.data.device)
         be.copy_region(tile.mask, wl, ones, (0,) * len(wl), w.shape)
     be.merge(tile.data, tile.mask, local_ul, update, reducer_op, fastpath=False)
   tile.written.append(region)

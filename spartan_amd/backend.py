@@ -29,7 +29,7 @@ SRC_PATH = os.path.join(_HERE, 'csrc', 'spx.hip')
 
 SPX_BOOL, SPX_I32, SPX_I64, SPX_F32, SPX_F64 = 0, 1, 2, 3, 4
 OP_CODE = {'sum': 0, 'min': 1, 'max': 2, 'argmin': 3, 'argmax': 4, 'replace': 5}
-FILL_CONST, FILL_ARANGE, FILL_UNIFORM = 0, 1, 2
+FILL_CONST, FILL_ARANGE, FILL_UNIFORM, FILL_NORMAL = 0, 1, 2, 3
 
 _DT = {np.dtype(np.bool_): SPX_BOOL, np.dtype(np.int32): SPX_I32, np.dtype(np.int64): SPX_I64,
        np.dtype(np.float32): SPX_F32, np.dtype(np.float64): SPX_F64}

@@ -123,6 +123,15 @@ __device__ __forceinline__ u64 rng_at(u64 seed, u64 g) {
   return mix64(seed * 0xD1B54A32D192ED03ULL + (g + 1ULL) * 0x9E3779B97F4A7C15ULL);
 }
 
+// standard normal at global flat index g: Box-Muller over the two counter
+// streams 2g (u1 in (0,1]) and 2g+1 (u2 in [0,1)), computed in fp64
+__device__ __forceinline__ double normal_at(u64 seed, i64 g) {
+  double u1 = (double)((rng_at(seed, 2ULL * (u64)g) >> 11) + 1ULL) * 1.1102230246251565e-16;
+  double u2 = (double)(rng_at(seed, 2ULL * (u64)g + 1ULL) >> 11) * 1.1102230246251565e-16;
+  double r = sqrt(-2.0 * log(u1));
+  return r * cos(6.283185307179586 * u2);
+}
+
 template <typename T>
 __device__ __forceinline__ T fill_value(int kind, int dt, double a, double b, u64 seed, i64 g);
 
@@ -130,6 +139,7 @@ template <>
 __device__ __forceinline__ float fill_value<float>(int kind, int, double a, double b, u64 seed, i64 g) {
   if (kind == SPX_FILL_CONST) return (float)a;
   if (kind == SPX_FILL_ARANGE) return (float)(a + b * (double)g);
+  if (kind == SPX_FILL_NORMAL) return (float)(a + b * normal_at(seed, g));
   float u = (float)(rng_at(seed, (u64)g) >> 40) * 5.9604644775390625e-08f;  // 2^-24
   float lo = (float)a, span = (float)(b - a);
   float t = span * u;  // separate rounding steps (fp-contract off) -- oracle does the same
@@ -139,6 +149,7 @@ template <>
 __device__ __forceinline__ double fill_value<double>(int kind, int, double a, double b, u64 seed, i64 g) {
   if (kind == SPX_FILL_CONST) return a;
   if (kind == SPX_FILL_ARANGE) return a + b * (double)g;
+  if (kind == SPX_FILL_NORMAL) return a + b * normal_at(seed, g);
   double u = (double)(rng_at(seed, (u64)g) >> 11) * 1.1102230246251565e-16;  // 2^-53
   double t = (b - a) * u;
   return a + t;
@@ -152,6 +163,7 @@ template <typename T>
 __device__ __forceinline__ T fill_value_int(int kind, double a, double b, u64 seed, i64 g) {
   if (kind == SPX_FILL_CONST) return (T)sat_i64(a);
   if (kind == SPX_FILL_ARANGE) return (T)((i64)a + (i64)b * g);
+  if (kind == SPX_FILL_NORMAL) return (T)(i64)floor(a + b * normal_at(seed, g));
   double u = (double)(rng_at(seed, (u64)g) >> 11) * 1.1102230246251565e-16;
   return (T)(i64)floor(a + (b - a) * u);
 }
@@ -187,7 +199,7 @@ extern "C" int spx_fill(int dtype, int kind, void* out, int ndim, const int64_t*
                         uint64_t seed, void* stream) {
   if (!valid_dtype(dtype)) return set_err(SPX_EINVAL, "spx_fill: bad dtype %d", dtype);
   if (ndim < 0 || ndim > 8) return set_err(SPX_EINVAL, "spx_fill: ndim %d > 8", ndim);
-  if (kind < SPX_FILL_CONST || kind > SPX_FILL_UNIFORM)
+  if (kind < SPX_FILL_CONST || kind > SPX_FILL_NORMAL)
     return set_err(SPX_EINVAL, "spx_fill: bad kind %d", kind);
   Geom geo{};
   geo.ndim = ndim;

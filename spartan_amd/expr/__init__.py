@@ -3,7 +3,7 @@ on the MI355X tile-execution backend."""
 from .base import (Expr, NotShapeable, as_array, eager, evaluate, force, glom, lazify,
                    optimized_dag)
 from .builtins import (abs, add, arange, argmax, argmin, astype, count_nonzero, count_zero, exp,
-                       ln, log, maximum, max, mean, min, minimum, multiply, ones, power, rand,
+                       ln, log, maximum, max, mean, min, minimum, multiply, ones, power, rand, randn,
                        size, sqrt, square, sub, sum, zeros)
 from .dot import dot
 from .map import map
@@ -12,7 +12,7 @@ from .reduce import reduce
 from .reshape import reshape
 from .slice import slice_expr
 from .transpose import transpose
-from .write_array import from_numpy
+from .write_array import from_file, from_numpy, write
 
 Expr.sum = sum
 Expr.mean = mean

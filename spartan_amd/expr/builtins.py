@@ -1,6 +1,6 @@
 """NumPy-style builtins (the hot-path subset of spartan/expr/builtins.py).
 
-Creation: ``ones`` / ``zeros`` (:378-401), ``rand`` (:72-88), ``arange``
+Creation: ``ones`` / ``zeros`` (:378-401), ``rand`` / ``randn`` (:72-104), ``arange``
 (:404-463) -- each a map over an ``ndarray`` placeholder whose mapper has a
 registered lowering (constants, or a generator leaf filled by spx_fill).
 Reductions: ``sum`` / ``max`` / ``min`` / ``mean`` (:466-539), ``argmin`` /
@@ -94,6 +94,29 @@ def rand(*shape, **kw):
     assert isinstance(s, (int, np.integer))
   return map(ndarray(shape, dtype=dtype, tile_hint=tile_hint), fn=_make_rand,
              fn_kw={'seed': seed, 'low': low, 'high': high})
+
+
+def _make_randn(input, seed=0):
+  raise CodegenError('_make_randn is lowered to spx_fill, never called')
+
+
+register_lowering(_make_randn, lambda op, env: Pre('normal', _leaf_of(op, env).dtype,
+                                                   (backend.FILL_NORMAL, 0.0, 1.0, int(op.kw['seed'])), None))
+
+
+@not_idempotent
+def randn(*shape, **kw):
+  """Standard normal array (float64; builtins.py:92-104).  Like ``rand``,
+  values come from the counter-based splitmix64 stream (Box-Muller of the
+  draws 2i and 2i+1), so they do not depend on tiling or device.  Extra
+  keywords of this build: ``dtype``, ``seed``."""
+  tile_hint = kw.pop('tile_hint', None)
+  dtype = kw.pop('dtype', np.float64)
+  seed = _new_seed(kw.pop('seed', None))
+  assert not kw, 'Unknown keywords %s' % kw
+  for s in shape:
+    assert isinstance(s, (int, np.integer))
+  return map(ndarray(shape, dtype=dtype, tile_hint=tile_hint), fn=_make_randn, fn_kw={'seed': seed})
 
 
 def _arange_mapper(tile, ex, start, stop, step, dtype=None):

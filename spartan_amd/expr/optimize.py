@@ -343,6 +343,24 @@ class AutomaticTiling:
         self.add_edge(cid, nid, _size(shape) if self.tiling(cid) != tiling else 0)
     return out
 
+  def visit_WriteArrayExpr(self, expr):  # :716-740
+    child_ids = self.visit_children([expr.array])
+    data_ids = self.visit_children([expr.data])
+    if not child_ids:
+      return []
+    if not data_ids:  # host data: the write keeps the target's nodes
+      for cid in child_ids:
+        self.nodes[cid][0].append(expr)
+      return child_ids
+    out = []
+    for i, tiling in enumerate(self._alternatives(child_ids)):
+      nid = self._node([expr], tiling)
+      out.append(nid)
+      self.add_edge(child_ids[i], nid, 0)
+      for cid in data_ids:
+        self.add_edge(cid, nid, _size(self.first_expr(cid).shape) if self.tiling(cid) != tiling else 0)
+    return out
+
   def visit_ReshapeExpr(self, expr):  # visit_aligned_nodes(reverse_cost=True), :742-763
     child_ids = self.visit_children([expr.array])
     if not child_ids:

@@ -72,6 +72,8 @@ class FakeBackend:
         v = np.full(n, a, dtype=dt)
     elif kind == B.FILL_ARANGE:
       v = rng.arange_values(g, a, b, dt)
+    elif kind == B.FILL_NORMAL:
+      v = rng.normal_values(g, seed, a, b, dt)
     else:
       v = rng.uniform_values(g, seed, a, b, dt)
     _put(out, v.reshape(shape))

@@ -100,6 +100,11 @@ def _body(rank, world, port, W, q):
     for name, e, want in _views_cases(expr):
       got = e.glom()
       np.testing.assert_allclose(np.asarray(got).reshape(np.shape(want)), want, rtol=1e-12, err_msg=name)
+    # writes over ranks: NumPy pieces land on the owners' tiles, array sources
+    # move by gather_regions, merges with reducers on sub-regions
+    import tempfile
+    from test_write import _run_write_cases
+    _run_write_cases(expr, tempfile.mkdtemp())
     q.put((rank, 'ok'))
   except Exception as e:  # pragma: no cover - reported to the parent
     import traceback

@@ -576,3 +576,52 @@ def test_views_gpu(ex, W):
   for name, e, want in _views_cases(expr):
     got = e.glom()
     np.testing.assert_allclose(np.asarray(got).reshape(np.shape(want)), want, rtol=1e-12, err_msg=name)
+
+
+# ---------------------------------------------- writes / ingest / egress (8(f) rank 3)
+@pytest.mark.parametrize('W', [1, 3])
+def test_write_gpu(ex, W, tmp_path):
+  """The reference's test_write cases, sub-region merges with reducers
+  (spx_merge masked and unmasked paths), self-aliasing writes and writes
+  from transposed views, on the GPU."""
+  from test_write import _run_write_cases
+  expr, setw = ex
+  setw(W)
+  _run_write_cases(expr, str(tmp_path))
+
+
+def test_transfer_pipeline_gpu(ex, tmp_path):
+  """Pinned double-buffered upload / download (array/transfer.py) at sizes
+  that take the pipeline: strided host pieces, a memmap, rows wider than a
+  staging block, bool and int dtypes, strided download targets."""
+  import torch
+  from spartan_amd.array import transfer
+  expr, setw = ex
+  setw(1)
+  dev = torch.device('cuda:0')
+  big = rng.rand((3000, 2000), 31, np.float32)            # 24 MB: two staging blocks
+  for piece in (big, big[:, 500:1700], big[1:2999:2, ::3], big.T):
+    t = transfer.upload(piece, dev)
+    np.testing.assert_array_equal(t.cpu().numpy(), piece)
+    np.testing.assert_array_equal(transfer.download(t), piece)
+    out = np.zeros((piece.shape[0], piece.shape[1] + 7), np.float32)
+    transfer.download(t, out[:, 3:3 + piece.shape[1]])
+    np.testing.assert_array_equal(out[:, 3:3 + piece.shape[1]], piece)
+    assert not out[:, :3].any() and not out[:, 3 + piece.shape[1]:].any()
+  wide = rng.rand((3, transfer.CHUNK // 8 + 5), 32, np.float64)  # rows wider than a block
+  t = transfer.upload(wide, dev)
+  np.testing.assert_array_equal(transfer.download(t), wide)
+  out = np.zeros((3, wide.shape[1] + 1))
+  transfer.download(t, out[:, 1:])
+  np.testing.assert_array_equal(out[:, 1:], wide)
+  flags = (rng.rand((5_000_000,), 33, np.float64) > 0.5)
+  np.testing.assert_array_equal(transfer.download(transfer.upload(flags, dev)), flags)
+  ints = np.arange(3_000_000, dtype=np.int64).reshape(1000, 3000)
+  np.testing.assert_array_equal(transfer.download(transfer.upload(ints, dev)), ints)
+  fn = str(tmp_path / 'm.npy')
+  np.save(fn, big)
+  mm = np.load(fn, mmap_mode='r')
+  x = expr.from_file(fn)
+  np.testing.assert_array_equal(x.glom(), big)
+  np.testing.assert_allclose(x.sum(0).glom(), big.astype(np.float64).sum(0), rtol=1e-5)
+  del mm
