@@ -177,6 +177,17 @@ int spx_kmeans_accumulate(int dtype, int64_t N, int64_t D, int64_t K, const void
                           const int64_t* labels, double* sums, uint64_t* counts, int zero_first,
                           void* workspace, size_t workspace_bytes, void* stream);
 
+/* Full distance matrix out[p * ldo + c] = cdist(points, centers)[p, c] in
+ * the exact order above, rounded once to out_dtype (F32/F64): the
+ * materialised outer((X, C), (0, 0), kmeans_dist_mapper) (k_means_.py:52-58,
+ * outer.py:14-61).  points F32/F64 (N, D) row stride ldp; centers fp64. */
+int spx_cdist(int dtype, int out_dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
+              const double* centers, void* out, int64_t ldo, void* stream);
+/* counts[k] (+)= number of labels equal to k (labels outside [0, K)
+ * skipped; overwritten when zero_first != 0): np.bincount(labels,
+ * minlength=K) of kmeans_count_mapper (k_means_.py:61-64).  Exact. */
+int spx_bincount(const int64_t* labels, int64_t N, int64_t K, uint64_t* counts, int zero_first, void* stream);
+
 /* ------------------------------------------------------ automatic tiling */
 /* Host-only (no device work, callable without a GPU): the node choice on the
  * AutomaticTiling cost graph (spartan/expr/optimize.py:454-890), replacing

@@ -94,6 +94,10 @@ _SIGS = {
     'spx_kmeans_accumulate': ([ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                                ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p], ctypes.c_int),
+    'spx_cdist': ([ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                   ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p], ctypes.c_int),
+    'spx_bincount': ([ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int,
+                      ctypes.c_void_p], ctypes.c_int),
     'spx_mincost_tiling': ([ctypes.c_int32, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
                             ctypes.POINTER(ctypes.c_int32), _I64P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
                             ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_uint8), _I64P], ctypes.c_int),
@@ -547,6 +551,24 @@ class HipBackend:
                                           ctypes.c_void_p(counts.data_ptr()), 1 if zero_first else 0,
                                           ctypes.c_void_p(ws.data_ptr()), ws.numel(), self.stream()),
            'spx_kmeans_accumulate')
+
+  def cdist(self, points, centers, out):
+    """out (N, K) = exact-order cdist(points, centers), rounded to out's dtype."""
+    N, D = points.shape
+    K = centers.shape[0]
+    assert centers.dtype == self._f64() and tuple(centers.shape) == (K, D) and tuple(out.shape) == (N, K)
+    assert centers.is_contiguous() and points.stride(1) == 1 and out.stride(1) == 1
+    _check(self.lib.spx_cdist(spx_dtype(np_dtype(points.dtype)), spx_dtype(np_dtype(out.dtype)), N, D, K,
+                              ctypes.c_void_p(points.data_ptr()), points.stride(0),
+                              ctypes.c_void_p(centers.data_ptr()), ctypes.c_void_p(out.data_ptr()), out.stride(0),
+                              self.stream()), 'spx_cdist')
+
+  def bincount(self, labels, counts, zero_first=True):
+    """counts (K,) int64 (+)= bincount of int64 ``labels`` (out-of-range skipped)."""
+    assert labels.dtype == counts.dtype and labels.is_contiguous() and counts.is_contiguous()
+    _check(self.lib.spx_bincount(ctypes.c_void_p(labels.data_ptr()), labels.numel(), counts.numel(),
+                                 ctypes.c_void_p(counts.data_ptr()), 1 if zero_first else 0, self.stream()),
+           'spx_bincount')
 
   def _workspace(self, nbytes, device):
     """Grow-only scratch buffer on ``device`` (reuse is stream-ordered)."""

@@ -131,6 +131,16 @@ def walk(node):
     yield from walk(node.w)
 
 
+def unique_nodes(root):
+  """Nodes of a tree (a DAG when leaves are shared), each object once."""
+  seen, out = set(), []
+  for n in walk(root):
+    if id(n) not in seen:
+      seen.add(id(n))
+      out.append(n)
+  return out
+
+
 def rowdots(root):
   """Unique RowDot nodes of a tree, numbered (rid) in first-visit order."""
   out = []

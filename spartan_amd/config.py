@@ -93,6 +93,8 @@ FLAGS.add('opt_map_fusion', True, bool)
 FLAGS.add('opt_reduce_fusion', True, bool)
 FLAGS.add('opt_dot_fusion', True, bool, 'fold dot(x, w_host) into a fused axis-0 reduction over x')
 FLAGS.add('opt_auto_tiling', True, bool, 'row / column partitioning chosen by the min-cost tiling solver')
+FLAGS.add('opt_outer_argmin_fusion', True, bool,
+          'argmin(outer(X, C, registered distance mapper), axis=1) -> one fused assignment kernel')
 FLAGS.add('opt_expression_cache', True, bool)
 FLAGS.add('rng_seed', 0x5EED, int, 'base seed of the counter-based rand()')
 FLAGS.add('kernel_cache_dir', '', str, 'override the JIT code-object cache directory')

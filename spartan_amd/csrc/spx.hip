@@ -1742,6 +1742,133 @@ extern "C" int spx_kmeans_accumulate(int dtype, int64_t N, int64_t D, int64_t K,
   return SPX_OK;
 }
 
+// ----------------------------------------------------- full distance matrix
+// out[p * ldo + c] = cdist(P, C)[p, c] (the materialised result of
+// outer((X, C), (0, 0), kmeans_dist_mapper), k_means_.py:52-58) in scipy's
+// exact order as in k_kmeans_assign (sequential fp64 over d, separately
+// rounded, then sqrt), rounded once to the output dtype as the reference's
+// target.update does.  A block owns a 64-point x 64-centre tile; each lane
+// 4 x 4 pairs, operands staged through LDS in 16-dim chunks (zero padding
+// past D adds exact +0.0 terms).  Only the unfused path uses it: argmin over
+// it is fused into spx_kmeans_assign (expr/optimize.py OuterArgminFusion).
+#define CD_T 64
+#define CD_DC 16
+template <typename TP, typename TO>
+__global__ __launch_bounds__(256) void k_cdist(i64 N, i64 D, i64 K, const TP* __restrict__ P, i64 ldp,
+                                               const double* __restrict__ C, TO* __restrict__ out, i64 ldo) {
+  __shared__ double Ps[CD_T][CD_DC + 1];
+  __shared__ double Cs[CD_T][CD_DC + 1];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const i64 c0 = (i64)blockIdx.x * CD_T;
+  for (i64 p0 = (i64)blockIdx.y * CD_T; p0 < N; p0 += (i64)gridDim.y * CD_T) {  // block-uniform
+    double s[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s[i][j] = 0.0;
+    for (i64 d0 = 0; d0 < D; d0 += CD_DC) {
+      __syncthreads();
+      for (int e = threadIdx.x; e < CD_T * CD_DC; e += 256) {
+        const int r = e / CD_DC, dd = e % CD_DC;
+        Ps[r][dd] = (p0 + r < N && d0 + dd < D) ? (double)P[(p0 + r) * ldp + d0 + dd] : 0.0;
+        Cs[r][dd] = (c0 + r < K && d0 + dd < D) ? C[(c0 + r) * D + d0 + dd] : 0.0;
+      }
+      __syncthreads();
+#pragma unroll 4
+      for (int dd = 0; dd < CD_DC; ++dd) {
+        double x[4], c[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          x[i] = Ps[ty + 16 * i][dd];
+          c[i] = Cs[tx + 16 * i][dd];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const double df = x[i] - c[j];
+            const double sq = df * df;
+            s[i][j] = s[i][j] + sq;
+          }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const i64 p = p0 + ty + 16 * i, c = c0 + tx + 16 * j;
+        if (p < N && c < K) out[p * ldo + c] = (TO)sqrt(s[i][j]);
+      }
+  }
+}
+
+extern "C" int spx_cdist(int dtype, int out_dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
+                         const double* centers, void* out, int64_t ldo, void* stream) {
+  if (dtype != SPX_F32 && dtype != SPX_F64) return set_err(SPX_ENOTSUP, "spx_cdist: points must be F32/F64");
+  if (out_dtype != SPX_F32 && out_dtype != SPX_F64) return set_err(SPX_ENOTSUP, "spx_cdist: out must be F32/F64");
+  if (N < 0 || D < 1 || K < 1 || (N > 0 && (ldp < D || ldo < K))) return set_err(SPX_EINVAL, "spx_cdist: bad sizes");
+  if (N == 0) return SPX_OK;
+  if (!points || !centers || !out) return set_err(SPX_EINVAL, "spx_cdist: null pointer");
+  const i64 cb = (K + CD_T - 1) / CD_T;
+  if (cb > 65535) return set_err(SPX_ENOTSUP, "spx_cdist: K too large");
+  i64 pb = (N + CD_T - 1) / CD_T;
+  if (pb > 65535) pb = 65535;
+  dim3 grid((unsigned)cb, (unsigned)pb);
+  if (dtype == SPX_F32 && out_dtype == SPX_F32)
+    k_cdist<float, float><<<grid, 256, 0, S(stream)>>>(N, D, K, (const float*)points, ldp, centers, (float*)out, ldo);
+  else if (dtype == SPX_F32)
+    k_cdist<float, double><<<grid, 256, 0, S(stream)>>>(N, D, K, (const float*)points, ldp, centers, (double*)out, ldo);
+  else if (out_dtype == SPX_F32)
+    k_cdist<double, float><<<grid, 256, 0, S(stream)>>>(N, D, K, (const double*)points, ldp, centers, (float*)out, ldo);
+  else
+    k_cdist<double, double><<<grid, 256, 0, S(stream)>>>(N, D, K, (const double*)points, ldp, centers, (double*)out,
+                                                         ldo);
+  LAUNCH_CHECK("spx_cdist");
+  return SPX_OK;
+}
+
+// ----------------------------------------------------------------- bincount
+// counts[k] (+)= #{i : labels[i] == k}, labels outside [0, K) skipped
+// (np.bincount(labels, minlength=K) of kmeans_count_mapper, k_means_.py:
+// 61-64).  Integer atomics, so the result is exact and order-free: per-block
+// LDS histograms when K fits (K <= BC_LDS), else global atomics.
+#define BC_LDS 16384
+__global__ __launch_bounds__(256) void k_bincount(i64 N, const i64* __restrict__ labels, i64 K,
+                                                  unsigned long long* __restrict__ counts, int use_lds) {
+  extern __shared__ unsigned int hist[];
+  if (use_lds) {
+    for (i64 k = threadIdx.x; k < K; k += 256) hist[k] = 0u;
+    __syncthreads();
+  }
+  for (i64 i = (i64)blockIdx.x * 256 + threadIdx.x; i < N; i += (i64)gridDim.x * 256) {
+    const i64 v = labels[i];
+    if (v >= 0 && v < K) {
+      if (use_lds) atomicAdd(&hist[v], 1u);
+      else atomicAdd(&counts[v], 1ull);
+    }
+  }
+  if (use_lds) {
+    __syncthreads();
+    for (i64 k = threadIdx.x; k < K; k += 256)
+      if (hist[k]) atomicAdd(&counts[k], (unsigned long long)hist[k]);
+  }
+}
+
+extern "C" int spx_bincount(const int64_t* labels, int64_t N, int64_t K, uint64_t* counts, int zero_first,
+                            void* stream) {
+  if (N < 0 || K < 1) return set_err(SPX_EINVAL, "spx_bincount: bad N/K");
+  if (!counts || (N > 0 && !labels)) return set_err(SPX_EINVAL, "spx_bincount: null pointer");
+  if (zero_first) HIP_TRY(hipMemsetAsync(counts, 0, (size_t)K * sizeof(uint64_t), S(stream)));
+  if (N == 0) return SPX_OK;
+  const int use_lds = K <= BC_LDS;
+  int g = grid_for(N, 16);
+  if (g > 4096) g = 4096;
+  k_bincount<<<g, 256, use_lds ? (size_t)K * sizeof(unsigned int) : 0, S(stream)>>>(
+      N, labels, K, (unsigned long long*)counts, use_lds);
+  LAUNCH_CHECK("spx_bincount");
+  return SPX_OK;
+}
+
 // ============================================================ JIT modules
 extern "C" int spx_module_load(const void* image, size_t nbytes, void** module_out) {
   if (!image || nbytes == 0 || !module_out) return set_err(SPX_EINVAL, "spx_module_load: bad args");

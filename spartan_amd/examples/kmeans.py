@@ -1,0 +1,226 @@
+"""The reference's k-means driver, runnable unmodified on the MI355X path
+(spartan/examples/sklearn/cluster/k_means_.py).
+
+``KMeans.fit(X, centers, implementation='outer')`` is the reference's loop
+(k_means_.py:108-152) written against ``expr.outer`` / ``expr.argmin`` /
+``expr.map2`` with the reference's three mapper functions.  Those mappers
+are registered joins (expr/join.py), so each runs as device work:
+
+  kmeans_dist_mapper    outer((X, C), (0, 0))  -> spx_cdist: exact-order fp64
+                        distances (N, K), rounded to the target dtype;
+  argmin(outer(...), axis=1)                   -> fused by OuterArgminFusion
+                        (expr/optimize.py) into spx_kmeans_assign when the
+                        distances are fp64: certified bf16x3-MFMA filter +
+                        exact recompute, no (N, K) matrix (204.8 GB at cfg3);
+  kmeans_count_mapper   map2(labels, 0)        -> spx_bincount per label tile
+                        + RCCL all-reduce;
+  kmeans_center_mapper  map2((X, labels), (0, 0)) -> spx_kmeans_accumulate
+                        per-centre fp64 sums + RCCL all-reduce.
+
+The mapper bodies below are the host meaning of each join (the reference's
+NumPy code, restated); they are never called on the product path.
+
+Divergence kept from workloads.kmeans_fit: counts and
+centre sums are SUMMED over tiles, where the reference's reducer-less map2
+keeps the last tile's; empty clusters are reseeded from a
+seeded generator instead of the global ``np.random``.
+"""
+import numpy as np
+
+from .. import backend, comm, expr, runtime
+from ..array import distarray, extent as ext
+from ..expr.join import register_argmin_fusion, register_join
+
+
+# ------------------------------------------------------ the three mappers
+def kmeans_dist_mapper(ex_a, tile_a, ex_b, tile_b):
+  """k_means_.py:52-58: cdist of a point tile against a centre tile."""
+  from scipy.spatial.distance import cdist
+  target_ex = ext.create((ex_a.ul[0], ex_b.ul[0]), (ex_a.lr[0], ex_b.lr[0]),
+                         (ex_a.array_shape[0], ex_b.array_shape[0]))
+  yield target_ex, cdist(tile_a, tile_b)
+
+
+def kmeans_count_mapper(extents, tiles, centers_count):
+  """k_means_.py:61-64: np.bincount of a label tile."""
+  target_ex = ext.create((0,), (centers_count,), (centers_count,))
+  yield target_ex, np.bincount(tiles[0].astype(np.int64), minlength=centers_count)
+
+
+def kmeans_center_mapper(extents, tiles, centers_count):
+  """k_means_.py:67-89: per-centre sums of the points carrying each label."""
+  points, labels = tiles
+  target_ex = ext.create((0, 0), (centers_count, points.shape[1]), (centers_count, points.shape[1]))
+  new_centers = np.zeros((centers_count, points.shape[1]))
+  for i in range(centers_count):
+    new_centers[i] = points[labels == i].sum(axis=0)
+  yield target_ex, new_centers
+
+
+# -------------------------------------------------------- device joins
+def _replicated_f64(array):
+  """The whole ``array`` as a contiguous fp64 tensor on every rank (collective)."""
+  ctx = runtime.get()
+  full = ext.from_shape(array.shape)
+  got = distarray.gather_regions(array, [(full, r) for r in range(ctx.world_size)])
+  return backend.get().contiguous(got[ctx.rank], np.float64)
+
+
+def _row_blocks(X, ncols):
+  """[(owner rank, row extent over all columns)] of X's row blocks, and
+  {index: device tensor} of the local ones (gathered when X is column-split)."""
+  ctx = runtime.get()
+  rows = sorted({(ex.ul[0], ex.lr[0]): w for ex, w in X.tiles.items()}.items())
+  blocks = [(ctx.owner(w) if w != -1 else ctx.rank,
+             ext.create((r0, 0), (r1, ncols), X.shape) if len(X.shape) == 2 else ext.create((r0,), (r1,), X.shape))
+            for (r0, r1), w in rows]
+  got = distarray.gather_regions(X, [(region, dst) for dst, region in blocks])
+  return blocks, got
+
+
+def _deliver_full(target, full):
+  """Copy a full-size tensor, identical on every rank, into target's local tiles."""
+  from ..expr.engine import _copy_out
+  be = backend.get()
+  for d, t in target.local.items():
+    _copy_out(be, t, full, d)
+
+
+def _dist_join(kind, arrays, axes, fn_kw, target):
+  import torch
+  from ..expr.join import _scatter_updates
+  if kind != 'outer' or tuple(axes) != (0, 0) or len(arrays[0].shape) != 2:
+    raise NotImplementedError('kmeans_dist_mapper: outer((X, C), (0, 0)) over a 2-d X only')
+  X, C = arrays
+  ctx = runtime.get()
+  be = backend.get()
+  c = _replicated_f64(C)
+  K, D = c.shape
+  blocks, got = _row_blocks(X, D)
+  updates = []
+  for qi, (src, region) in enumerate(blocks):
+    tex = ext.create((region.ul[0], 0), (region.lr[0], K), target.shape)
+    t = None
+    if src == ctx.rank:
+      pts = got[qi]
+      if pts.stride(-1) != 1:
+        pts = be.contiguous(pts)
+      t = torch.empty(tex.shape, dtype=backend.torch_dtype(target.dtype), device=ctx.device)
+      be.cdist(pts, c, t)
+    updates.append((qi, tex, src, t))
+  _scatter_updates(target, updates)
+
+
+def _count_join(kind, arrays, axes, fn_kw, target):
+  import torch
+  ctx = runtime.get()
+  be = backend.get()
+  K = int(fn_kw['centers_count'])
+  labels = arrays[0]
+  counts = torch.zeros((K,), dtype=torch.int64, device=ctx.device)
+  for ex, tile in labels.local.items():
+    lab = be.contiguous(tile.data, np.int64).reshape(-1)
+    be.bincount(lab, counts, zero_first=False)
+  comm.all_reduce(counts, 'sum')
+  _deliver_full(target, counts)
+
+
+def _center_join(kind, arrays, axes, fn_kw, target):
+  import torch
+  ctx = runtime.get()
+  be = backend.get()
+  K = int(fn_kw['centers_count'])
+  X, labels = arrays
+  D = X.shape[1]
+  sums = torch.zeros((K, D), dtype=torch.float64, device=ctx.device)
+  counts = torch.zeros((K,), dtype=torch.int64, device=ctx.device)
+  blocks, got = _row_blocks(X, D)
+  lab_blocks = distarray.gather_regions(labels, [(ext.create((r.ul[0],), (r.lr[0],), labels.shape)
+                                                  if len(labels.shape) == 1 else
+                                                  ext.create((r.ul[0], 0), (r.lr[0], labels.shape[1]), labels.shape),
+                                                  dst) for dst, r in blocks])
+  for qi, (src, region) in enumerate(blocks):
+    if src != ctx.rank:
+      continue
+    pts = got[qi]
+    if pts.stride(-1) != 1:
+      pts = be.contiguous(pts)
+    lab = be.contiguous(lab_blocks[qi], np.int64).reshape(-1)
+    be.kmeans_accumulate(pts, lab, sums, counts, zero_first=False)
+  comm.all_reduce(sums, 'sum')
+  _deliver_full(target, sums)
+
+
+def _assign_fused(arrays, fn_kw, target):
+  """argmin(outer((X, C), (0, 0), kmeans_dist_mapper), axis=1) for fp64
+  distances: spx_kmeans_assign per X row block (labels bit-exact with the
+  argmin of the materialised cdist, first index on ties, first NaN wins)."""
+  import torch
+  from ..expr.join import _scatter_updates
+  X, C = arrays
+  ctx = runtime.get()
+  be = backend.get()
+  c = _replicated_f64(C)
+  D = c.shape[1]
+  blocks, got = _row_blocks(X, D)
+  updates = []
+  for qi, (src, region) in enumerate(blocks):
+    tex = ext.create((region.ul[0],), (region.lr[0],), target.shape)
+    lab = None
+    if src == ctx.rank:
+      pts = got[qi]
+      if pts.stride(-1) != 1:
+        pts = be.contiguous(pts)
+      lab = torch.empty((tex.shape[0],), dtype=torch.int64, device=ctx.device)
+      be.kmeans_assign(pts, c, lab)
+    updates.append((qi, tex, src, lab))
+  _scatter_updates(target, updates)
+
+
+register_join(kmeans_dist_mapper, _dist_join)
+register_argmin_fusion(kmeans_dist_mapper, _assign_fused)
+register_join(kmeans_count_mapper, _count_join)
+register_join(kmeans_center_mapper, _center_join)
+
+
+# --------------------------------------------------------------- KMeans
+class KMeans(object):
+  """k_means_.py:90-152."""
+
+  def __init__(self, n_clusters=8, n_iter=100, seed=0):
+    self.n_clusters = n_clusters
+    self.n_iter = n_iter
+    self.seed = seed
+
+  def fit(self, X, centers=None, implementation='outer'):
+    """X: (N, D) array tiled by rows; centers: (K, D) host array / Expr, or
+    None (``expr.rand``).  Returns (centers (K, D) host fp64, labels)."""
+    if implementation != 'outer':
+      raise NotImplementedError('implementation %r: only the reference default "outer" is on the path'
+                                % implementation)
+    num_dim = X.shape[1]
+    rng = np.random.default_rng(self.seed)
+    labels = expr.zeros((X.shape[0], 1), dtype=np.int64)
+    if centers is None:
+      centers = expr.rand(self.n_clusters, num_dim)
+    elif isinstance(centers, np.ndarray):
+      centers = expr.from_numpy(centers)
+    for i in range(self.n_iter):
+      distances = expr.outer((X, centers), (0, 0), fn=kmeans_dist_mapper,
+                             shape=(X.shape[0], centers.shape[0]))
+      labels = expr.argmin(distances, axis=1)
+      counts = expr.map2(labels, 0, fn=kmeans_count_mapper, fn_kw={'centers_count': self.n_clusters},
+                         shape=(centers.shape[0],))
+      new_centers = expr.map2((X, labels), (0, 0), fn=kmeans_center_mapper,
+                              fn_kw={'centers_count': self.n_clusters},
+                              shape=(centers.shape[0], centers.shape[1]))
+      counts = counts.optimized().glom()
+      centers = new_centers.optimized().glom()
+      zcount_indices = (counts == 0).reshape(self.n_clusters)
+      if np.any(zcount_indices):
+        n_points = np.count_nonzero(zcount_indices)
+        counts[zcount_indices] = 1
+        centers[zcount_indices, :] = rng.standard_normal((n_points, num_dim))
+      centers = centers / counts.reshape(centers.shape[0], 1)
+      centers = expr.from_numpy(centers)
+    return centers.glom(), labels

@@ -2,10 +2,12 @@
 on the MI355X tile-execution backend."""
 from .base import (Expr, NotShapeable, as_array, eager, evaluate, force, glom, lazify,
                    optimized_dag)
-from .builtins import (abs, add, arange, argmax, argmin, astype, count_nonzero, count_zero, exp,
+from .builtins import (abs, add, arange, argmax, argmin, astype, bincount, concatenate, count_nonzero,
+                       count_zero, exp,
                        ln, log, maximum, max, mean, min, minimum, multiply, ones, power, rand, randn,
                        size, sqrt, square, sub, sum, zeros)
 from .dot import dot
+from .join import map2, outer
 from .map import map
 from .ndarray import ndarray
 from .reduce import reduce

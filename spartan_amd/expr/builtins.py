@@ -309,3 +309,117 @@ def sqrt(v):
 
 def abs(v):
   return map(v, fn=np.abs)
+
+
+# ------------------------------------------------------- join builtins
+def _bincount_mapper(ex, tiles, minlength=None):
+  """builtins.py:815-821: per-tile np.bincount (host meaning; lowered to
+  spx_bincount / spx_kmeans_accumulate by the registered join below)."""
+  if len(tiles) > 1:
+    result = np.bincount(tiles[0], weights=tiles[1], minlength=minlength)
+  else:
+    result = np.bincount(tiles[0], minlength=minlength)
+  from ..array import extent as ext
+  yield ext.from_shape(result.shape), result
+
+
+def _bincount_join(kind, arrays, axes, fn_kw, target):
+  import torch
+  from .. import comm, runtime
+  from ..examples.kmeans import _deliver_full
+  ctx = runtime.get()
+  be = backend.get()
+  K = target.shape[0]
+  v = arrays[0]
+  if len(arrays) == 1:
+    acc = torch.zeros((K,), dtype=torch.int64, device=ctx.device)
+    for ex, tile in v.local.items():
+      be.bincount(be.contiguous(tile.data, np.int64).reshape(-1), acc, zero_first=False)
+  else:
+    from ..array import distarray
+    w = arrays[1]
+    acc = torch.zeros((K, 1), dtype=torch.float64, device=ctx.device)
+    counts = torch.zeros((K,), dtype=torch.int64, device=ctx.device)
+    exs = sorted(v.tiles.items(), key=lambda kv: kv[0].ul)
+    got = distarray.gather_regions(w, [(ex, ctx.owner(o)) for ex, o in exs])
+    for qi, (ex, o) in enumerate(exs):
+      if ctx.owner(o) != ctx.rank:
+        continue
+      lab = be.contiguous(v.local[ex].data, np.int64).reshape(-1)
+      wt = got[qi]
+      if np.dtype(w.dtype).kind != 'f':
+        wt = be.contiguous(wt, np.float64)
+      be.kmeans_accumulate(be.contiguous(wt).reshape(-1, 1), lab, acc, counts, zero_first=False)
+  comm.all_reduce(acc, 'sum')
+  _deliver_full(target, acc.reshape(K))
+
+
+def bincount(v, weights=None, minlength=None):
+  """Count occurrences of each value in a 1-d non-negative int array
+  (builtins.py:824-846): per-tile counts (weighted sums with ``weights``)
+  summed across tiles.  As in the reference the result has the input's
+  dtype (int64), so weighted sums are truncated toward zero.  The reference
+  asserts min(v) > 0, which rejects the value 0 its own mapper counts; here
+  min(v) >= 0 is required."""
+  import builtins as _b
+  from .join import map2
+  minval = int(min(v).glom())
+  maxval = int(max(v).glom())
+  assert minval >= 0, 'bincount: negative values'
+  minlength = maxval + 1 if minlength is None else _b.max(maxval + 1, minlength)
+  arrays = (v, weights) if weights is not None else v
+  return map2(arrays, fn=_bincount_mapper, fn_kw={'minlength': minlength}, shape=(minlength,), reducer=np.add)
+
+
+def _concatenate_mapper(extents, tiles, shape=None, axis=0):
+  """builtins.py:871-884 (host meaning; data movement by the registered join)."""
+  raise CodegenError('_concatenate_mapper is lowered to a tile copy, never called')
+
+
+def _concatenate_join(kind, arrays, axes, fn_kw, target):
+  """Every tile of ``a`` lands at its own offset in the target, every tile of
+  ``b`` shifted by a.shape[axis] along ``axis``: one point-to-point batch."""
+  from .. import runtime
+  from ..array import extent as ext
+  from .join import _scatter_updates
+  ctx = runtime.get()
+  axis = fn_kw.get('axis', 0)
+  shape = tuple(target.shape)
+  updates = []
+  off = arrays[0].shape[axis]
+  for ai, arr in enumerate(arrays):
+    for ex, w in sorted(arr.tiles.items(), key=lambda kv: kv[0].ul):
+      ul, lr = list(ex.ul), list(ex.lr)
+      if ai == 1:
+        ul[axis] += off
+        lr[axis] += off
+      src = ctx.owner(w)
+      t = arr.local[ex].data if src == ctx.rank else None
+      updates.append(((ai, tuple(ex.ul)), ext.create(ul, lr, shape), src, t))
+  _scatter_updates(target, updates)
+
+
+def concatenate(a, b, axis=0):
+  """Join two arrays along ``axis`` (builtins.py:887-905)."""
+  from .join import map2
+  from ..array import extent as ext
+  new_shape = [0] * len(a.shape)
+  for index, (dim1, dim2) in enumerate(zip(a.shape, b.shape)):
+    if index == axis:
+      new_shape[index] = dim1 + dim2
+      continue
+    new_shape[index] = dim1
+    if dim1 != dim2:
+      raise ValueError('all the input array dimensions except for the concatenation axis must match exactly')
+  partition_axis = ext.largest_dim_axis(a.shape, exclude_axes=[axis]) if len(a.shape) > 1 else 0
+  return map2((a, b), (partition_axis, partition_axis), fn=_concatenate_mapper,
+              fn_kw={'axis': axis, 'shape': new_shape}, shape=new_shape)
+
+
+def _register_joins():
+  from .join import register_join
+  register_join(_bincount_mapper, _bincount_join)
+  register_join(_concatenate_mapper, _concatenate_join)
+
+
+_register_joins()

@@ -58,7 +58,7 @@ def bind(children, child_to_var, op):
   remap = {}
   for old in sorted(used):
     remap[old] = len(remap)
-  for n in codegen.walk(root):
+  for n in codegen.unique_nodes(root):
     if isinstance(n, codegen.In) and not isinstance(n, Pre):
       n.slot = remap[n.slot]
   seen = {}

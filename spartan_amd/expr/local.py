@@ -185,8 +185,13 @@ class Sym:
   """Symbolic tile value used to trace user mapper functions into IR."""
   __array_priority__ = 1000
 
-  def __init__(self, node, env):
+  def __init__(self, node, env, shape=None):
     self.node, self.env = node, env
+    self.shape = shape  # tile shape when known (join mappers read tiles[i].shape)
+
+  @property
+  def ndim(self):
+    return None if self.shape is None else len(self.shape)
 
   @property
   def dtype(self):
@@ -199,15 +204,26 @@ class Sym:
       return self.env.new_scalar(v.item() if isinstance(v, np.generic) else v)
     raise CodegenError('cannot trace operand of type %s' % type(v).__name__)
 
+  @staticmethod
+  def _shape_of(vals):
+    """Broadcast shape of the operands whose shapes are known (else None)."""
+    shapes = [v.shape for v in vals if isinstance(v, Sym) and v.shape is not None]
+    if not shapes:
+      return None
+    try:
+      return tuple(np.broadcast_shapes(*shapes))
+    except ValueError:
+      raise CodegenError('operands of shapes %s do not broadcast' % (shapes,))
+
   def __array_ufunc__(self, ufunc, method, *inputs, **kw):
     if method != '__call__' or kw:
       raise CodegenError('unsupported ufunc use %s.%s %s' % (ufunc.__name__, method, kw))
-    return Sym(codegen.Op(ufunc.__name__, [self._wrap(x) for x in inputs]), self.env)
+    return Sym(codegen.Op(ufunc.__name__, [self._wrap(x) for x in inputs]), self.env, self._shape_of(inputs))
 
   def _bin(name, rev=False):
     def f(self, other):
       a, b = (other, self) if rev else (self, other)
-      return Sym(codegen.Op(name, [self._wrap(a), self._wrap(b)]), self.env)
+      return Sym(codegen.Op(name, [self._wrap(a), self._wrap(b)]), self.env, self._shape_of((a, b)))
     return f
 
   __add__, __radd__ = _bin('add'), _bin('add', True)
@@ -224,13 +240,13 @@ class Sym:
   del _bin
 
   def __neg__(self):
-    return Sym(codegen.Op('negative', [self.node]), self.env)
+    return Sym(codegen.Op('negative', [self.node]), self.env, self.shape)
 
   def __abs__(self):
-    return Sym(codegen.Op('absolute', [self.node]), self.env)
+    return Sym(codegen.Op('absolute', [self.node]), self.env, self.shape)
 
   def astype(self, dtype):
-    return Sym(codegen.Cast(self.node, np.dtype(dtype)), self.env)
+    return Sym(codegen.Cast(self.node, np.dtype(dtype)), self.env, self.shape)
 
   def __bool__(self):
     raise CodegenError('data-dependent control flow cannot be traced')

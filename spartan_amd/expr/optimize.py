@@ -183,6 +183,38 @@ class DotReduceFusion(OptimizePass):
                      child_to_var=[v for _, v in keep], op=op)
 
 
+class OuterArgminFusion(OptimizePass):
+  """argmin(outer((X, C), (0, 0), mapper), axis=1) -> one fused kernel.
+
+  The reference materialises the (N, K) outer product (k_means_.py:126-128:
+  cdist per row strip into an N x K target, 204.8 GB fp64 at cfg3) and then
+  runs argmin over it.  When the outer's mapper has a registered argmin
+  fusion (examples/kmeans.py: kmeans_dist_mapper -> spx_kmeans_assign) and
+  the argmin reads the outer product directly, the pair becomes an
+  ArgminJoinExpr with the argmin's expr_id; its labels are the same bits."""
+  name = 'outer_argmin_fusion'
+
+  def visit_ReduceExpr(self, expr):
+    from .builtins import _argmin_local
+    from .join import ArgminJoinExpr, OuterProductExpr, argmin_fusion_for
+    children = self.visit(expr.children)
+    expr = expr_like(expr, children=children)
+    op = expr.op
+    if not isinstance(op, LocalReduceExpr) or op.fn is not _argmin_local or expr.axis not in (1, -1):
+      return expr
+    if len(children.vals) != 1 or not isinstance(children.vals[0], OuterProductExpr):
+      return expr
+    tree = op.deps[1]
+    if not (isinstance(tree, LocalInput) and tree.idx == expr.child_to_var[0]):
+      return expr
+    outer = children.vals[0]
+    impl = argmin_fusion_for(outer)
+    if impl is None:
+      return expr
+    return ArgminJoinExpr(expr_id=expr.expr_id, arrays=outer.arrays, outer=outer, impl=impl,
+                          tile_hint=expr.tile_hint)
+
+
 class CollapsedCachedExpressions(OptimizePass):
   """Replace already-evaluated nodes by their value."""
   name = 'collapse_cached'
@@ -482,7 +514,8 @@ def _world_workers():
   return ctx.num_workers if ctx is not None else 1
 
 
-PASSES = [CollapsedCachedExpressions, AutomaticTiling, MapMapFusion, ReduceMapFusion, DotReduceFusion]
+PASSES = [CollapsedCachedExpressions, AutomaticTiling, MapMapFusion, ReduceMapFusion, DotReduceFusion,
+          OuterArgminFusion]
 
 
 def optimize(dag):

@@ -180,6 +180,20 @@ class FakeBackend:
     d = cdist(_np(points).astype(np.float64), _np(centers))
     labels.copy_(torch.as_tensor(d.argmin(1).astype(np.int64)))
 
+  def cdist(self, points, centers, out):
+    from scipy.spatial.distance import cdist
+    d = cdist(_np(points).astype(np.float64), _np(centers))
+    out.copy_(torch.as_tensor(d.astype(B.np_dtype(out.dtype))))
+
+  def bincount(self, labels, counts, zero_first=True):
+    lab = _np(labels).reshape(-1)
+    K = counts.numel()
+    lab = lab[(lab >= 0) & (lab < K)]
+    c = np.bincount(lab, minlength=K).astype(np.int64)
+    if not zero_first:
+      c = c + _np(counts)
+    counts.copy_(torch.as_tensor(c))
+
   def kmeans_accumulate(self, points, labels, sums, counts, zero_first=True):
     p = _np(points).astype(np.float64)
     lab = _np(labels)

@@ -105,6 +105,11 @@ def _body(rank, world, port, W, q):
     import tempfile
     from test_write import _run_write_cases
     _run_write_cases(expr, tempfile.mkdtemp())
+    # joins over ranks: k-means mappers, fused argmin, bincount / concatenate,
+    # traced map2 / outer with pieces scattered to the target owners
+    from test_join import _run_join_cases
+    from spartan_amd.config import FLAGS as F
+    _run_join_cases(expr, F)
     q.put((rank, 'ok'))
   except Exception as e:  # pragma: no cover - reported to the parent
     import traceback

@@ -625,3 +625,38 @@ def test_transfer_pipeline_gpu(ex, tmp_path):
   np.testing.assert_array_equal(x.glom(), big)
   np.testing.assert_allclose(x.sum(0).glom(), big.astype(np.float64).sum(0), rtol=1e-5)
   del mm
+
+
+# ---------------------------------------------- joins: map2 / outer (8(f) rank 4)
+@pytest.mark.parametrize('W', [1, 3])
+def test_join_gpu(ex, W):
+  """The reference's k-means mappers through expr.outer / map2 (spx_cdist,
+  spx_bincount, spx_kmeans_accumulate), the fused argmin (spx_kmeans_assign),
+  bincount / concatenate and traced elementwise joins, on the GPU."""
+  from test_join import _run_join_cases
+  from spartan_amd.config import FLAGS
+  expr, setw = ex
+  setw(W)
+  _run_join_cases(expr, FLAGS)
+
+
+def test_cdist_and_fused_kmeans_gpu(ex):
+  """spx_cdist bit-exact against scipy at a size that spans many 64 x 64
+  tiles and a D that is not a multiple of the 16-dim chunk; the unmodified
+  KMeans driver on fp32 points with D % 64 == 0 (the certified bf16x3 filter
+  inside the fused argmin) against the oracle."""
+  from scipy.spatial.distance import cdist
+  from spartan_amd.examples.kmeans import KMeans, kmeans_dist_mapper
+  from test_join import _kmeans_oracle
+  expr, setw = ex
+  setw(2)
+  X = rng.rand((3001, 37), 61, np.float64)
+  C = rng.rand((130, 37), 62, np.float64)
+  d = expr.outer((expr.from_numpy(X), expr.from_numpy(C)), (0, 0), fn=kmeans_dist_mapper, shape=(3001, 130))
+  np.testing.assert_array_equal(d.glom(), cdist(X, C))
+  X32 = rng.rand((40000, 64), 63, np.float32)
+  c0 = X32[:48].astype(np.float64)
+  got_c, got_l = KMeans(48, 3).fit(expr.from_numpy(X32), centers=c0)
+  wc, wl = _kmeans_oracle(X32, c0, 3, center_dtype=np.float32)
+  np.testing.assert_array_equal(got_l.glom(), wl)
+  np.testing.assert_allclose(got_c, wc, rtol=1e-6)

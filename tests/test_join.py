@@ -1,0 +1,182 @@
+"""Joins: ``map2`` / ``outer`` with the reference's
+k-means mappers run unmodified (k_means_.py:52-152), the OuterArgminFusion
+rewrite, ``bincount`` / ``concatenate`` (builtins.py:815-905) and traced
+elementwise join mappers.  ``_run_join_cases`` is shared by the CPU test
+double here, the GPU parity test and the gloo world-2 test."""
+import numpy as np
+import pytest
+from scipy.spatial.distance import cdist
+
+from oracle import rng
+
+
+def _kmeans_oracle(X, centers, n_iter, seed=0, center_dtype=np.float64):
+  """KMeans 'outer' with the build's documented semantics: labels =
+  argmin(cdist) (fp64), counts and centre sums summed over tiles, the sums
+  held in the target dtype (X's, as the reference's map2 target), empty
+  clusters reseeded from default_rng(seed)."""
+  X = np.asarray(X)
+  K, D = centers.shape
+  g = np.random.default_rng(seed)
+  labels = None
+  for _ in range(n_iter):
+    labels = cdist(X.astype(np.float64), centers).argmin(axis=1)
+    counts = np.bincount(labels, minlength=K)
+    sums = np.zeros((K, D))
+    np.add.at(sums, labels, X.astype(np.float64))
+    sums = sums.astype(center_dtype).astype(np.float64)
+    empty = counts == 0
+    if np.any(empty):
+      counts[empty] = 1
+      sums[empty] = g.standard_normal((int(empty.sum()), D))
+    centers = sums / counts.reshape(K, 1)
+  return centers, labels
+
+
+def _run_join_cases(expr, flags):
+  from spartan_amd.examples.kmeans import (KMeans, kmeans_center_mapper, kmeans_count_mapper,
+                                           kmeans_dist_mapper)
+  from spartan_amd.expr.local import CodegenError
+  X = rng.rand((500, 12), 51, np.float64)
+  C = rng.rand((7, 12), 52, np.float64)
+  Xe = expr.from_numpy(X)
+  Ce = expr.from_numpy(C)
+  ref = cdist(X, C)
+
+  # outer with the distance mapper, materialised (fp64 target = X's dtype)
+  d = expr.outer((Xe, Ce), (0, 0), fn=kmeans_dist_mapper, shape=(500, 7))
+  np.testing.assert_array_equal(d.glom(), ref)
+  # ... an fp32 target rounds the fp64 distances once, as target.update does
+  d32 = expr.outer((Xe, Ce), (0, 0), fn=kmeans_dist_mapper, shape=(500, 7), dtype=np.float32)
+  np.testing.assert_array_equal(d32.glom(), ref.astype(np.float32))
+
+  # argmin over it: fused (optimized) and materialised (force / flag off) agree
+  want = ref.argmin(axis=1)
+  lab = expr.argmin(expr.outer((Xe, Ce), (0, 0), fn=kmeans_dist_mapper, shape=(500, 7)), axis=1)
+  opt = lab.optimized()
+  assert type(opt).__name__ == 'ArgminJoinExpr'
+  np.testing.assert_array_equal(opt.glom(), want)
+  np.testing.assert_array_equal(expr.argmin(
+      expr.outer((Xe, Ce), (0, 0), fn=kmeans_dist_mapper, shape=(500, 7)), axis=1).force().glom(), want)
+  flags.opt_outer_argmin_fusion = False
+  try:
+    plain = expr.argmin(expr.outer((Xe, Ce), (0, 0), fn=kmeans_dist_mapper, shape=(500, 7)), axis=1).optimized()
+    assert type(plain).__name__ != 'ArgminJoinExpr'
+    np.testing.assert_array_equal(plain.glom(), want)
+  finally:
+    flags.opt_outer_argmin_fusion = True
+  # ties: duplicated centres -> the first index wins in both paths
+  Cd = np.concatenate([C[:3], C[1:2], C[3:]])
+  tie = expr.argmin(expr.outer((Xe, expr.from_numpy(Cd)), (0, 0), fn=kmeans_dist_mapper, shape=(500, 8)), axis=1)
+  np.testing.assert_array_equal(tie.optimized().glom(), cdist(X, Cd).argmin(axis=1))
+
+  # the count / centre mappers
+  labels = expr.from_numpy(want.astype(np.int64))
+  counts = expr.map2(labels, 0, fn=kmeans_count_mapper, fn_kw={'centers_count': 7}, shape=(7,))
+  np.testing.assert_array_equal(counts.glom(), np.bincount(want, minlength=7))
+  sums = expr.map2((Xe, labels), (0, 0), fn=kmeans_center_mapper, fn_kw={'centers_count': 7}, shape=(7, 12))
+  want_s = np.zeros((7, 12))
+  np.add.at(want_s, want, X)
+  np.testing.assert_allclose(sums.glom(), want_s, rtol=1e-12)
+
+  # the whole driver, unmodified (fp64 and fp32 points)
+  c0 = X[:7].copy()
+  got_c, got_l = KMeans(7, 4).fit(Xe, centers=c0)
+  wc, wl = _kmeans_oracle(X, c0, 4)
+  np.testing.assert_array_equal(got_l.glom(), wl)
+  np.testing.assert_allclose(got_c, wc, rtol=1e-10)
+  X32 = X.astype(np.float32)
+  got_c, got_l = KMeans(7, 3).fit(expr.from_numpy(X32), centers=c0)
+  wc, wl = _kmeans_oracle(X32, c0, 3, center_dtype=np.float32)
+  np.testing.assert_array_equal(got_l.glom(), wl)
+  np.testing.assert_allclose(got_c, wc, rtol=1e-6)
+  # an empty cluster is reseeded
+  cz = np.vstack([X[:3], np.full((1, 12), 50.0)])
+  got_c, got_l = KMeans(4, 2).fit(Xe, centers=cz)
+  wc, wl = _kmeans_oracle(X, cz, 2)
+  np.testing.assert_array_equal(got_l.glom(), wl)
+  np.testing.assert_allclose(got_c, wc, rtol=1e-10)
+
+  # bincount / concatenate builtins
+  v = (rng.rand((300,), 53, np.float64) * 9).astype(np.int64)
+  np.testing.assert_array_equal(expr.bincount(expr.from_numpy(v)).glom(), np.bincount(v))
+  np.testing.assert_array_equal(expr.bincount(expr.from_numpy(v), minlength=15).glom(), np.bincount(v, minlength=15))
+  wts = rng.rand((300,), 54, np.float64) * 4
+  np.testing.assert_array_equal(expr.bincount(expr.from_numpy(v), weights=expr.from_numpy(wts)).glom(),
+                                np.bincount(v, weights=wts).astype(np.int64))
+  a = np.arange(60.).reshape(10, 6)
+  b = np.arange(100., 136.).reshape(6, 6)
+  np.testing.assert_array_equal(expr.concatenate(expr.from_numpy(a), expr.from_numpy(b), 0).glom(),
+                                np.concatenate([a, b], 0))
+  b1 = np.arange(100., 140.).reshape(10, 4)
+  np.testing.assert_array_equal(expr.concatenate(expr.from_numpy(a), expr.from_numpy(b1), 1).glom(),
+                                np.concatenate([a, b1], 1))
+
+  # traced elementwise join mappers
+  p = rng.rand((40, 30), 55, np.float64)
+  q = rng.rand((40, 30), 56, np.float64)
+  pe, qe = expr.from_numpy(p), expr.from_numpy(q)
+
+  def axpy(ex, tiles, alpha):
+    yield ex, tiles[0] * alpha + np.exp(tiles[1])
+
+  got = expr.map2((pe, qe), fn=axpy, fn_kw={'alpha': 2.0}, shape=(40, 30)).glom()
+  np.testing.assert_allclose(got, p * 2.0 + np.exp(q), rtol=1e-14)
+
+  def joined(exs, tiles):
+    yield exs[0], tiles[0] - tiles[1]
+
+  got = expr.map2((pe, qe), (0, 0), fn=joined, shape=(40, 30)).glom()
+  np.testing.assert_allclose(got, p - q, rtol=1e-14)
+
+  def shift(ex_a, ta, ex_b, tb):  # outer with the whole second array per tile
+    yield ex_a, ta + 1.0
+
+  got = expr.outer((pe, expr.from_numpy(np.ones((3, 3)))), (0, None), fn=shift, shape=(40, 30)).glom()
+  np.testing.assert_allclose(got, p + 1.0)
+
+  def twice(ex, tiles):  # two pieces into the same extent: the first replaces, the second adds
+    yield ex, tiles[0]
+    yield ex, tiles[0] * 2.0
+
+  got = expr.map2(pe, fn=twice, shape=(40, 30), reducer=np.add).glom()
+  np.testing.assert_allclose(got, p * 3.0, rtol=1e-14)
+
+  def mismatched(ex, tiles):  # a value whose shape is not its extent's
+    from spartan_amd.array import extent as ext
+    yield ext.create((0, ex.ul[1]), (1, ex.lr[1]), (1, 30)), tiles[0]
+
+  def opaque(ex, tiles):
+    yield ex, tiles[0][::2]
+
+  with pytest.raises(CodegenError):
+    expr.map2(pe, fn=opaque, shape=(40, 30)).glom()
+  with pytest.raises(CodegenError):
+    expr.map2(pe, fn=mismatched, shape=(1, 30)).glom()
+
+
+@pytest.mark.parametrize('W', [1, 3, 4])
+def test_join_host(host_ctx, W):
+  host_ctx(W)
+  from spartan_amd import expr
+  from spartan_amd.config import FLAGS
+  _run_join_cases(expr, FLAGS)
+
+
+def test_join_instances():
+  from spartan_amd.array import extent as ext
+  from spartan_amd.expr.join import join_instances
+
+  class A:
+    def __init__(self, shape, tiles):
+      self.shape, self.tiles = shape, tiles
+  a = A((6, 4), {ext.create((0, 0), (3, 4), (6, 4)): 0, ext.create((3, 0), (6, 4), (6, 4)): 1})
+  b = A((6, 2), {ext.create((0, 0), (6, 2), (6, 2)): 0})
+  inst = join_instances('map2', [a, b], (0, 0))
+  assert [(w, [(e.ul, e.lr) for e in exs]) for w, exs, _ in inst] == [
+      (0, [((0, 0), (3, 4)), ((0, 0), (3, 2))]), (1, [((3, 0), (6, 4)), ((3, 0), (6, 2))])]
+  c = A((4, 3), {ext.create((0, 0), (2, 3), (4, 3)): 0, ext.create((2, 0), (4, 3), (4, 3)): 1})
+  inst = join_instances('outer', [a, c], (0, 0))
+  assert len(inst) == 4 and [e.ul for e in inst[1][1]] == [(0, 0), (2, 0)]
+  inst = join_instances('outer', [a, c], (0, None))
+  assert len(inst) == 2 and inst[0][1][1].shape == (4, 3)
