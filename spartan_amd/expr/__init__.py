@@ -9,6 +9,7 @@ from .builtins import (abs, add, arange, argmax, argmin, astype, bincount, conca
 from .dot import dot
 from .join import map2, outer
 from .map import map
+from .map_with_location import map_with_location, region_map
 from .ndarray import ndarray
 from .reduce import reduce
 from .reshape import reshape

@@ -24,7 +24,7 @@ from ..array import distarray, extent as ext
 from ..array.distarray import DistArrayImpl, LocalWrapper, ReplicatedArray
 from ..util import prod
 from .broadcast import Broadcast
-from .local import CodegenError, LowerEnv, Pre, lower
+from .local import CodegenError, LowerEnv, Pre, has_location, lower
 
 
 # --------------------------------------------------------------- binding
@@ -37,11 +37,12 @@ def _scalar_value(child):
   return None
 
 
-def bind(children, child_to_var, op):
-  """Lower ``op`` with children bound to IR leaves.
+def bind(children, child_to_var, op, extent=None):
+  """Lower ``op`` with children bound to IR leaves (``extent``: the tile, for
+  trees holding a location map).
 
   Returns (root, array_slots {slot: child index}, pres [Pre leaves])."""
-  env = LowerEnv({})
+  env = LowerEnv({}, extent)
   slots = {}
   for i, (child, var) in enumerate(zip(children, child_to_var)):
     sv = _scalar_value(child)
@@ -139,8 +140,45 @@ def materialise_pres(pres, children, child_to_var, ex, inputs):
 
 
 # ----------------------------------------------------------------- map
+def run_location_map(children, child_to_var, op):
+  """A map whose tree holds a map_with_location call: lowered once per tile
+  with that tile's extent (map_with_location.py:22-60), one kernel per tile."""
+  import torch
+  ctx = runtime.get()
+  be = backend.get()
+  largest = distarray.largest_value(children)
+  tiles = driving_tiles(largest)
+  arrays = {i: i for i, c in enumerate(children) if _scalar_value(c) is None}
+  per_ex = fetch_inputs(children, arrays, tiles)
+  out_local, dtype = {}, None
+  for ex, fetched in per_ex.items():
+    root, slots, pres = bind(children, child_to_var, op, extent=ex)
+    if dtype is not None and np.dtype(root.dtype) != dtype:
+      raise CodegenError('location map yields %s on one tile and %s on another' % (dtype, root.dtype))
+    dtype = np.dtype(root.dtype)
+    inputs = {slot: fetched[ci] for slot, ci in slots.items()}
+    materialise_pres(pres, children, child_to_var, ex, inputs)
+    out = torch.empty(ex.shape if ex.ndim else (), dtype=backend.torch_dtype(root.dtype), device=ctx.device)
+    if isinstance(root, codegen.In) and not isinstance(root, Pre):
+      be.copy_region(out, (0,) * out.dim(), inputs[root.slot], (0,) * out.dim(), tuple(out.shape))
+    elif isinstance(root, (codegen.Const, codegen.Sc)):
+      be.fill(out, backend.FILL_CONST, root.value, 0.0, 0, ex.ul, ex.array_shape or ())
+    else:
+      be.map(root, inputs, out)
+    out_local[ex] = out
+  if dtype is None:  # no local tile: every rank must agree on the dtype
+    root, _, _ = bind(children, child_to_var, op, extent=next(iter(tiles)))
+    dtype = np.dtype(root.dtype)
+  if all(w == -1 for w in tiles.values()):
+    (ex, out), = out_local.items()
+    return ReplicatedArray(out)
+  return distarray.from_tiles(largest.shape, dtype, tiles, out_local)
+
+
 def run_map(children, child_to_var, op):
   ctx = runtime.get()
+  if has_location(op):
+    return run_location_map(children, child_to_var, op)
   largest = distarray.largest_value(children)
   root, slots, pres = bind(children, child_to_var, op)
   tiles = driving_tiles(largest)

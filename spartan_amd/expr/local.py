@@ -140,10 +140,11 @@ def register_lowering(fn, lowering):
 class LowerEnv:
   """Maps LocalInput names to IR leaves while lowering one tree."""
 
-  def __init__(self, leaves):
+  def __init__(self, leaves, extent=None):
     self.leaves = leaves  # var name -> IR leaf (In / Sc / Const) or ('array', dtype) placeholders
     self.pres = []        # Pre leaves created
     self.scalars = []     # Sc leaves created
+    self.extent = extent  # the tile's TileExtent when lowering a location map per tile
 
   def new_scalar(self, value):
     sc = codegen.Sc(len(self.scalars), value)
@@ -171,6 +172,14 @@ def lower(op, env):
     return _BUILTIN_LOWERINGS[fn](op, env)
   deps = [d for d in op.deps if not (isinstance(d, LocalInput) and d.idx == 'extent')]
   args = [lower(d, env) for d in deps]
+  if isinstance(op, LocalMapLocationExpr):
+    # map_with_location: fn(*tiles, (ul, lr, array_shape), **kw), traced once
+    # per tile with that tile's location as plain Python values
+    # (local.py:130-142); the location enters the IR as kernel-argument
+    # scalars, so tiles whose traces agree share one compiled kernel
+    if env.extent is None:
+      raise CodegenError('location map %s lowered without a tile extent' % op.fn_name())
+    return trace_callable(fn, args, op.kw, env, extra=(env.extent.to_tuple(),))
   if isinstance(fn, np.ufunc):
     if op.kw:
       raise CodegenError('ufunc %s with keywords %s' % (fn.__name__, op.kw))
@@ -254,10 +263,17 @@ class Sym:
   __hash__ = object.__hash__
 
 
-def trace_callable(fn, args, kw, env):
+def has_location(op):
+  """True iff a LocalExpr tree contains a map_with_location call."""
+  if isinstance(op, LocalMapLocationExpr):
+    return True
+  return any(has_location(d) for d in getattr(op, 'deps', ()))
+
+
+def trace_callable(fn, args, kw, env, extra=()):
   syms = [Sym(a, env) for a in args]
   try:
-    out = fn(*syms, **kw)
+    out = fn(*syms, *extra, **kw)
   except CodegenError:
     raise
   except Exception as e:
@@ -265,5 +281,9 @@ def trace_callable(fn, args, kw, env):
                        % (getattr(fn, '__name__', fn), type(e).__name__, e))
   if isinstance(out, Sym):
     return out.node
+  if extra and args and isinstance(out, (bool, int, float, np.generic)) and np.ndim(out) == 0:
+    # a location mapper returning a scalar for a whole tile (e.g. nbody.py:30-40
+    # _set_diagonal_mapper): the tile is filled with it, in the input's dtype
+    return codegen.Const(out.item() if isinstance(out, np.generic) else out, args[0].dtype)
   raise CodegenError('mapper %s did not return a traced tile value'
                      % getattr(fn, '__name__', fn))

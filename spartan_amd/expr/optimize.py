@@ -12,7 +12,8 @@ import numpy as np
 
 from ..config import FLAGS
 from .base import AsArray, CollectionExpr, Expr, ListExpr, Val, expr_like, lazify
-from .local import FnCallExpr, LocalInput, LocalMapLocationExpr, LocalReduceExpr, LocalRowDot, make_var
+from .local import (FnCallExpr, LocalInput, LocalMapLocationExpr, LocalReduceExpr, LocalRowDot, has_location,
+                    make_var)
 from .map import MapExpr
 from .ndarray import NdArrayExpr
 from .reduce import ReduceExpr
@@ -95,8 +96,8 @@ class ReduceMapFusion(OptimizePass):
   def visit_ReduceExpr(self, expr):
     children = self.visit(expr.children)
     for c in children:
-      if not isinstance(c, MapExpr) or getattr(c, 'not_idempotent', False):
-        return expr.visit(self)
+      if not isinstance(c, MapExpr) or getattr(c, 'not_idempotent', False) or has_location(c.op):
+        return expr.visit(self)  # location maps lower per tile: kept out of the fused reduce
     combined = LocalReduceExpr(fn=expr.op.fn, kw=expr.op.kw, deps=[expr.op.deps[0]])
     new_children, new_vars = [], []
     for c in children:

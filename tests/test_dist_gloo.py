@@ -110,6 +110,8 @@ def _body(rank, world, port, W, q):
     from test_join import _run_join_cases
     from spartan_amd.config import FLAGS as F
     _run_join_cases(expr, F)
+    from test_location import _run_location_cases
+    _run_location_cases(expr, W)
     q.put((rank, 'ok'))
   except Exception as e:  # pragma: no cover - reported to the parent
     import traceback

@@ -660,3 +660,12 @@ def test_cdist_and_fused_kmeans_gpu(ex):
   wc, wl = _kmeans_oracle(X32, c0, 3, center_dtype=np.float32)
   np.testing.assert_array_equal(got_l.glom(), wl)
   np.testing.assert_allclose(got_c, wc, rtol=1e-6)
+
+
+@pytest.mark.parametrize('W', [1, 3])
+def test_location_gpu(ex, W):
+  """map_with_location (per-tile traced kernels) and region_map on the GPU."""
+  from test_location import _run_location_cases
+  expr, setw = ex
+  setw(W)
+  _run_location_cases(expr, W)
