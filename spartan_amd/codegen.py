@@ -25,11 +25,22 @@ code object cached on disk by source hash) and launched through the C ABI
 (spx_launch).  Nothing here executes on the CPU.
 """
 import ctypes
+import os
 
 import numpy as np
 
 MAX_IN = 16
 MAX_DIM = 8
+# streamed contiguous vector loads carry the non-temporal hint (global_load
+# ... nt): the inputs of a fused map / reduce are read exactly once
+NT_LOADS = os.environ.get('SPX_NT_LOADS', '1') != '0'
+
+
+def _vload(vtype, ptr_expr):
+  """Source of one contiguous vector load of type ``vtype`` at ``ptr_expr``."""
+  if NT_LOADS:
+    return '__builtin_nontemporal_load((const GLOBAL %s*)(%s))' % (vtype, ptr_expr)
+  return '*(const GLOBAL %s*)(%s)' % (vtype, ptr_expr)
 
 # --------------------------------------------------------------------- IR
 
@@ -381,7 +392,7 @@ def _load_vec(slot, dt, cls, off, V):
   if cls == 'c':
     vt = '%s __attribute__((ext_vector_type(%d)))' % (ct, V)
     lines = ['typedef %s vt%d;' % (vt, slot),
-             'vt%d xv%d = *(const GLOBAL vt%d*)(%s + %s);' % (slot, slot, slot, p, off)]
+             'vt%d xv%d = %s;' % (slot, slot, _vload('vt%d' % slot, '%s + %s' % (p, off)))]
     lines += ['%s x%d_%d = xv%d[%d];' % (ct, slot, j, slot, j) for j in range(V)]
     return lines
   if cls == 'b':
@@ -758,7 +769,7 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
       pre = ['const i64 off = %s;' % off]
       if V > 1 and cls == 'c':
         pre.append('typedef %s __attribute__((ext_vector_type(%d))) vt;' % (ct, V))
-        pre.append('const vt xv = *(const GLOBAL vt*)(%s + off);' % p)
+        pre.append('const vt xv = %s;' % _vload('vt', '%s + off' % p))
         return ['xv[%d]' % j for j in range(V)], pre
       if V > 1 and cls == 'b':
         pre.append('const %s xb = %s[off];' % (ct, p))

@@ -112,6 +112,18 @@ static int grid_for(i64 n, int per_thread = 1) {
   return (int)g;
 }
 
+// Streamed once-read loads carry the non-temporal hint (global_load ... nt;
+// measured +5-9 % on the generated streaming kernels).  SPX_NO_NT builds a
+// variant without it for A/B timing (tools/km_split.py).
+template <typename T>
+__device__ __forceinline__ T ld_stream(const T* p) {
+#ifdef SPX_NO_NT
+  return *p;
+#else
+  return __builtin_nontemporal_load(p);
+#endif
+}
+
 // =================================================================== fills
 __device__ __forceinline__ u64 mix64(u64 z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -1081,7 +1093,7 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
     i64 row = tl * 32 + r;
     row = row < N ? row : N - 1;
     const float* p = P + row * ldp + ks * 16 + 8 * h;
-    ra[s][0] = *(const kb_f4*)p;
+    ra[s][0] = *(const kb_f4*)p;  // (nt measured no faster here)
     ra[s][1] = *(const kb_f4*)(p + 4);
   };
 #pragma unroll
@@ -1429,7 +1441,6 @@ constexpr int KA_WAVES = KA_THREADS / 64;  // centre owners per tile
 constexpr int KA_CPW = 16;                 // centres per wave (register sums)
 constexpr int KA_CB = KA_WAVES * KA_CPW;   // centres per tile
 constexpr int KA_STAGES = 4;               // register prefetch ring depth
-constexpr int KA_UNROLL = 4;               // points whose LDS reads are issued together
 
 template <typename TP>
 __global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_kmeans_accum(i64 N, i64 D, i64 K, const TP* __restrict__ P, i64 ldp,
@@ -1450,8 +1461,6 @@ __global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(1, 4
   const int lp = t / LPR, lc = (t % LPR) * VE;
   // 16-byte loads need the slice inside the row and aligned; else per element
   const bool vec = d0 + lc + VE <= D && (ldp % VE) == 0 && ((uintptr_t)P % 16) == 0;
-  // padding slots of a partial unrolled step add +0.0 (exact: a sum that
-  // starts at +0.0 never becomes -0.0) and no count to centre slot 0
   double acc[KA_CPW];
 #pragma unroll
   for (int j = 0; j < KA_CPW; ++j) acc[j] = 0.0;
@@ -1468,7 +1477,7 @@ __global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(1, 4
     const i64 p0 = (ch < nch ? ch : nch - 1) * CH;
     const i64 pr = p0 + lp < N ? p0 + lp : N - 1;
     if (vec) {
-      pf[s] = *(const V*)(P + pr * ldp + d0 + lc);
+      pf[s] = ld_stream((const V*)(P + pr * ldp + d0 + lc));  // read once: nt
     } else {
 #pragma unroll
       for (int j = 0; j < VE; ++j) {
@@ -1507,25 +1516,17 @@ __global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(1, 4
 #pragma unroll
     for (int s = 0; s < ST; ++s) {
       const int r = lane < CH ? lab_s[buf][s][lane] : -1;
+      const int jl = (int)((unsigned)r / (unsigned)KA_WAVES);  // this lane's point's register slot
       unsigned long long m = __ballot(r >= 0 && (r % KA_WAVES) == w);
+      // one point per step, in point order: the loop is issue-bound, so no
+      // padded slots (unrolled variants that batch the LDS reads measured
+      // slower: 2 -> 13.9 ms, 4 -> 16.6 ms vs 12.3 ms at cfg3); the LDS
+      // latency is hidden by the other waves of the SIMD
       while (m) {  // wave-uniform
-        int jj[KA_UNROLL];
-        double xx[KA_UNROLL];
-#pragma unroll
-        for (int q = 0; q < KA_UNROLL; ++q) {
-          int p = 0;
-          bool ok = false;
-          jj[q] = 0;
-          if (m) {
-            p = __ffsll((long long)m) - 1;
-            m &= m - 1;
-            jj[q] = __builtin_amdgcn_readlane(r, p) / KA_WAVES;
-            ok = true;
-          }
-          xx[q] = ok ? (double)xs[buf][s][p * KA_DB + lane] : 0.0;
-        }
-#pragma unroll
-        for (int q = 0; q < KA_UNROLL; ++q) acc[jj[q]] += xx[q];  // in point order
+        const int p = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const int j = __builtin_amdgcn_readlane(jl, p);
+        acc[j] += (double)xs[buf][s][p * KA_DB + lane];
       }
     }
     buf ^= 1;
