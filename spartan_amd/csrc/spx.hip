@@ -1008,7 +1008,10 @@ typedef KF_PROD KfProd;
 // xor-shuffles.
 constexpr int KB_WAVES = 4;
 constexpr int KB_DMAX = 128;
-constexpr int KB_GRP = 4;  // k-steps per fresh accumulator (divides 4)
+constexpr int KB_GRP = 4;  // k-steps per MFMA group (divides 4)
+#ifndef KB_FRESH
+#define KB_FRESH 1  // 1: every group into a fresh accumulator (tighter bound), 0: one chain per tile
+#endif
 typedef __bf16 kb_bf8 __attribute__((ext_vector_type(8)));
 typedef float kb_acc __attribute__((ext_vector_type(16)));
 typedef float kb_f4 __attribute__((ext_vector_type(4)));
@@ -1082,8 +1085,10 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
   const double cmax = *cmax_p;
   const double u32 = 5.9604644775390625e-08;
   const int KS = (int)D / 16;
-  const double eS =
-      (u32 + 3.1 * 3.814697265625e-06 + 2.0 * (48.0 * KB_GRP + (double)(KS / KB_GRP) + 3.0) * u32) * 1.01 * cmax;
+  // chain length of one accumulator: 48 KB_GRP products then KS / KB_GRP
+  // adds (fresh accumulators), or all 48 KS products in one MFMA chain
+  const double chain = KB_FRESH ? 48.0 * KB_GRP + (double)(KS / KB_GRP) : 48.0 * (double)KS;
+  const double eS = (u32 + 3.1 * 3.814697265625e-06 + 2.0 * (chain + 3.0) * u32) * 1.01 * cmax;
   const i64 ntiles = (N + 31) / 32;
   const i64 stride = (i64)gridDim.x * KB_WAVES;
   i64 tile = (i64)blockIdx.x * KB_WAVES + w;
@@ -1151,14 +1156,20 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
           // fresh accumulator that is then added to the running sum: the
           // rounding bound is that chain + D / (16 KB_GRP) adds instead of
           // one 3D-long chain
+#if KB_FRESH
           kb_acc tk = (kb_acc){};
+#else
+          kb_acc& tk = acc[ct];
+#endif
 #pragma unroll
           for (int g = 0; g < KB_GRP; ++g) {
             tk = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[g], bh[ct & 1][g], tk, 0, 0, 0);
             tk = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[g], bl[ct & 1][g], tk, 0, 0, 0);
             tk = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[g], bh[ct & 1][g], tk, 0, 0, 0);
           }
+#if KB_FRESH
           acc[ct] += tk;
+#endif
         }
       }
     }
