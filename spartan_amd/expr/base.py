@@ -130,13 +130,22 @@ class Expr:
 
   @property
   def shape(self):
+    # a node's shape never changes (rewrites that keep the id keep the
+    # shape), so the first answer is memoised: the optimiser asks for it
+    # thousands of times per DAG
+    s = self.__dict__.get('_shape_memo')
+    if s is not None:
+      return s
     c = self.cache()
     if c is not None:
-      return c.shape
-    try:
-      return self.compute_shape()
-    except NotShapeable:
-      return evaluate(self).shape
+      s = tuple(c.shape)
+    else:
+      try:
+        s = tuple(self.compute_shape())
+      except NotShapeable:
+        s = tuple(evaluate(self).shape)
+    self.__dict__['_shape_memo'] = s
+    return s
 
   @property
   def ndim(self):
