@@ -1329,21 +1329,54 @@ static void kb_launch(hipStream_t s, i64 N, i64 D, const float* P, i64 ldp, cons
 
 // Exact-order labels of the undecided points from their candidate masks
 // (K <= 256); equal distances go to the lower index (= first occurrence).
-// Eight lanes per point: in round j lane s takes the (8 j + s)-th candidate,
-// so the sequential fp64 d-loops of up to 8 candidates run side by side
-// (one lane per point serialised them); then a (distance, index) min over
-// the 8 lanes.
+// KC_LPP lanes per point: in round j lane s takes the (KC_LPP j + s)-th
+// candidate (undecided points keep ~2 candidates: 99 % have <= 3, measured
+// at cfg3, tools/km_undecided.py), and a (distance, index) min over the
+// point's lanes.  The sequential fp64 d-loop reads the point and the centre
+// in 16-dim chunks through a 2-deep register ring (16-byte loads, the next
+// chunk in flight while this one is summed): the per-element loads of the
+// first version paid an L2 / HBM latency per dim.
 // NATURAL: bit k of word w <-> centre 32 w + k (bf16x3 filter); else centre
 // w + 8 k (fp32 filter).
+#define KC_LPP 4
+#define KC_DC 16
+template <typename TP>
+__device__ __forceinline__ void kc_chunk(const TP* __restrict__ x, const double* __restrict__ cc, i64 d, bool vec,
+                                         TP (&xv)[KC_DC], double (&cv)[KC_DC]) {
+  if (vec) {
+    typedef TP V4 __attribute__((ext_vector_type(16 / sizeof(TP))));
+    constexpr int E = 16 / sizeof(TP);
+#pragma unroll
+    for (int k = 0; k < KC_DC; k += E) {
+      const V4 v = *(const V4*)(x + d + k);
+#pragma unroll
+      for (int e = 0; e < E; ++e) xv[k + e] = v[e];
+    }
+#pragma unroll
+    for (int k = 0; k < KC_DC; k += 2) {
+      const double2 v = *(const double2*)(cc + d + k);
+      cv[k] = v.x;
+      cv[k + 1] = v.y;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < KC_DC; ++k) {
+      xv[k] = x[d + k];
+      cv[k] = cc[d + k];
+    }
+  }
+}
+
 template <typename TP, bool NATURAL>
 __global__ __launch_bounds__(256) void k_kmeans_cand(i64 D, const TP* __restrict__ P, i64 ldp,
                                                      const double* __restrict__ C, i64* __restrict__ labels,
                                                      const unsigned int* __restrict__ counters,
                                                      const KfCand* __restrict__ cand_list) {
   const i64 n = counters[1];
-  const int sub = threadIdx.x & 7;
-  const i64 step = ((i64)gridDim.x * 256) >> 3;
-  for (i64 q = ((i64)blockIdx.x * 256 + threadIdx.x) >> 3; q < n; q += step) {  // uniform per 8 lanes
+  const int sub = threadIdx.x % KC_LPP;
+  const i64 step = ((i64)gridDim.x * 256) / KC_LPP;
+  const i64 Dc = D / KC_DC * KC_DC;  // chunked part of the d-loop
+  for (i64 q = ((i64)blockIdx.x * 256 + threadIdx.x) / KC_LPP; q < n; q += step) {  // uniform per point lanes
     const i64 row = cand_list[q].row;
     unsigned int mw[8];
     int tot = 0;
@@ -1355,8 +1388,8 @@ __global__ __launch_bounds__(256) void k_kmeans_cand(i64 D, const TP* __restrict
     const TP* x = P + row * ldp;
     double best = 0.0;
     int bi = -1;
-    for (int j = 0; 8 * j < tot; ++j) {  // uniform per 8 lanes
-      int nth = 8 * j + sub, c = -1;
+    for (int j = 0; KC_LPP * j < tot; ++j) {  // uniform per point lanes
+      int nth = KC_LPP * j + sub, c = -1;
 #pragma unroll
       for (int wd = 0; wd < 8; ++wd) {
         const int pc = __popc(mw[wd]);
@@ -1370,8 +1403,29 @@ __global__ __launch_bounds__(256) void k_kmeans_cand(i64 D, const TP* __restrict
         }
       }
       const double* cc = C + (i64)(c < 0 ? 0 : c) * D;
+      const bool vec = ((uintptr_t)x % 16) == 0 && ((uintptr_t)cc % 16) == 0;
       double acc = 0.0;
-      for (i64 d = 0; d < D; ++d) {
+      TP xv[2][KC_DC];
+      double cv[2][KC_DC];
+      if (Dc > 0) kc_chunk<TP>(x, cc, 0, vec, xv[0], cv[0]);
+      for (i64 d0 = 0; d0 < Dc; d0 += 2 * KC_DC) {
+        if (d0 + KC_DC < Dc) kc_chunk<TP>(x, cc, d0 + KC_DC, vec, xv[1], cv[1]);
+#pragma unroll
+        for (int k = 0; k < KC_DC; ++k) {
+          const double df = (double)xv[0][k] - cv[0][k];
+          const double sq = df * df;
+          acc = acc + sq;
+        }
+        if (d0 + KC_DC >= Dc) break;
+        if (d0 + 2 * KC_DC < Dc) kc_chunk<TP>(x, cc, d0 + 2 * KC_DC, vec, xv[0], cv[0]);
+#pragma unroll
+        for (int k = 0; k < KC_DC; ++k) {
+          const double df = (double)xv[1][k] - cv[1][k];
+          const double sq = df * df;
+          acc = acc + sq;
+        }
+      }
+      for (i64 d = Dc; d < D; ++d) {
         const double df = (double)x[d] - cc[d];
         const double sq = df * df;
         acc = acc + sq;
@@ -1383,7 +1437,7 @@ __global__ __launch_bounds__(256) void k_kmeans_cand(i64 D, const TP* __restrict
       }
     }
 #pragma unroll
-    for (int o = 1; o < 8; o <<= 1) {
+    for (int o = 1; o < KC_LPP; o <<= 1) {
       const double ob = __shfl_xor(best, o, 64);
       const int oi = __shfl_xor(bi, o, 64);
       if (oi >= 0 && (bi < 0 || ob < best || (ob == best && oi < bi))) {

@@ -28,5 +28,13 @@ for it in range(iters):
   cnt = be._ws[off:off + 8].view(torch.int32).cpu().numpy()
   print('iter %d: full %d (%.4f%%)  candidates %d (%.4f%%)' % (it, cnt[0], 100 * cnt[0] / n, cnt[1], 100 * cnt[1] / n),
         flush=True)
+  # candidates per undecided point: KfCand = {i64 row; u32 mask[8]} (40 B)
+  base = off + 16 + n * 8
+  raw = be._ws[base:base + int(cnt[1]) * 40].cpu().numpy().reshape(-1, 40)
+  pc = np.unpackbits(raw[:, 8:].copy(), axis=1).sum(1)
+  if len(pc):
+    print('  candidates per point: mean %.2f  p50 %d  p90 %d  max %d  hist(1..8,>8) %s'
+          % (pc.mean(), np.percentile(pc, 50), np.percentile(pc, 90), pc.max(),
+             [int((pc == k).sum()) for k in range(1, 9)] + [int((pc > 8).sum())]), flush=True)
   c, _ = workloads.kmeans_fit(X, K, 1, centers=c.cpu().numpy())
   c = torch.as_tensor(c).to(P.device)
