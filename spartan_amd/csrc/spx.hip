@@ -1053,6 +1053,67 @@ __global__ __launch_bounds__(256) void k_kmeans_prep_b3(i64 D, i64 K, i64 Kp, co
 
 static size_t kb_lds_bytes(i64 D, int nct) { return (size_t)2 * 32 * nct * (D + 8) * 2 + (size_t)32 * nct * 4; }
 
+// Step (B) of the bf16x3 filter epilogue, as a function (tools/perm_probe.hip
+// checks it against a brute-force top-2).
+__device__ __forceinline__ void kb_top2_lanes(float (&lo)[16], float (&sec)[16], int (&li)[16], int lane) {
+    // (B) across the 32 lanes of each half, halving the registers per lane at
+  // every step: a lane keeps the half its lane bit picks and receives the
+  // partner's copy of it.  Partners differ in the step's lane bit and agree
+  // on the bits already processed, which is all a min-reduction over the
+  // 32 centres needs: bit 4 by ds_swizzle (lane ^ 16), bits 3 / 2 / 1 / 0 by
+  // DPP row_mirror (lane ^ 15), row_half_mirror (^ 7), quad_perm ^ 2 and ^ 1
+  // -- VALU moves instead of ds_bpermute round trips (tools/perm_probe.hip,
+  // tools/top2_probe.hip).
+  // Lane (h, r) ends with register q = r >> 1, i.e. row rt(q, h), over all
+  // centres.  A (value, index) pair combines to the smaller value, the
+  // lower index on equal values.
+  auto comb = [](float a, int ai, float as, float b, int bi, float bs, float& l, int& li2, float& s2) {
+    s2 = __builtin_amdgcn_fmed3f(a, b, fminf(as, bs));
+    li2 = (b < a || (b == a && bi < ai)) ? bi : ai;
+    l = fminf(a, b);
+  };
+  // bit 4: ds_swizzle (bit mode, xor 16 within each 32-lane half; no address
+  // operand, no memory access).  v_permlane16_swap would do it in one VALU
+  // op, but the compiler folded its two results into one (tools/top2_probe).
+  auto xor16 = [](int v) { return __builtin_amdgcn_ds_swizzle(v, 0x401F); };
+  {
+    const bool up = (lane & 16) != 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float kl = up ? lo[k + 8] : lo[k], ks2 = up ? sec[k + 8] : sec[k];
+      const int ki = up ? li[k + 8] : li[k];
+      const float sl = up ? lo[k] : lo[k + 8], ss = up ? sec[k] : sec[k + 8];
+      const int si = up ? li[k] : li[k + 8];
+      comb(kl, ki, ks2, __builtin_bit_cast(float, xor16(__builtin_bit_cast(int, sl))), xor16(si),
+           __builtin_bit_cast(float, xor16(__builtin_bit_cast(int, ss))), lo[k], li[k], sec[k]);
+    }
+  }
+  auto dpp_step = [&](auto ctrl, int n, int o) {
+    constexpr int C = decltype(ctrl)::value;
+    const bool up = (lane & o) != 0;
+#pragma unroll
+    for (int k = 0; k < n; ++k) {
+      const float kl = up ? lo[k + n] : lo[k], ks2 = up ? sec[k + n] : sec[k];
+      const int ki = up ? li[k + n] : li[k];
+      const float sl = up ? lo[k] : lo[k + n], ss = up ? sec[k] : sec[k + n];
+      const int si = up ? li[k] : li[k + n];
+      const float ol = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sl), C, 0xF, 0xF, false));
+      const float os = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, ss), C, 0xF, 0xF, false));
+      const int oi = __builtin_amdgcn_update_dpp(0, si, C, 0xF, 0xF, false);
+      comb(kl, ki, ks2, ol, oi, os, lo[k], li[k], sec[k]);
+    }
+  };
+  dpp_step(std::integral_constant<int, 0x140>{}, 4, 8);  // row_mirror: lane ^ 15
+  dpp_step(std::integral_constant<int, 0x141>{}, 2, 4);  // row_half_mirror: lane ^ 7
+  dpp_step(std::integral_constant<int, 0x4E>{}, 1, 2);   // quad_perm [2,3,0,1]: lane ^ 2
+  {
+    const float ol = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, lo[0]), 0xB1, 0xF, 0xF, false));
+    const float os = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sec[0]), 0xB1, 0xF, 0xF, false));
+    const int oi = __builtin_amdgcn_update_dpp(0, li[0], 0xB1, 0xF, 0xF, false);
+    comb(lo[0], li[0], sec[0], ol, oi, os, lo[0], li[0], sec[0]);
+  }
+}
+
 template <int NCT>
 __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D, const float* __restrict__ P, i64 ldp,
                                                                     const __bf16* __restrict__ CBh,
@@ -1225,35 +1286,7 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
       sec[reg] = s2;
       li[reg] = r;
     }
-    // (B) across the 32 lanes of each half, halving the registers per lane at
-    // every step (xor 16, 8, 4, 2: a lane keeps the half its lane bit picks and
-    // sends the other), then xor 1 between the two lanes holding one row.  Lane
-    // (h, r) ends with register q = r >> 1, i.e. row rt(q, h), over all centres.
-#pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      const int n = 8 >> st;  // pairs this step
-      const int o = 16 >> st;
-      const bool up = (lane & o) != 0;
-#pragma unroll
-      for (int k = 0; k < n; ++k) {
-        const float sl = up ? lo[k] : lo[k + n], ss = up ? sec[k] : sec[k + n];
-        const int si = up ? li[k] : li[k + n];
-        const float kl = up ? lo[k + n] : lo[k], ks2 = up ? sec[k + n] : sec[k];
-        const int ki = up ? li[k + n] : li[k];
-        const float ol = __shfl_xor(sl, o, 64), os = __shfl_xor(ss, o, 64);
-        const int oi = __shfl_xor(si, o, 64);
-        sec[k] = __builtin_amdgcn_fmed3f(kl, ol, fminf(ks2, os));
-        li[k] = ol < kl ? oi : ki;
-        lo[k] = fminf(kl, ol);
-      }
-    }
-    {
-      const float ol = __shfl_xor(lo[0], 1, 64), os = __shfl_xor(sec[0], 1, 64);
-      const int oi = __shfl_xor(li[0], 1, 64);
-      sec[0] = __builtin_amdgcn_fmed3f(lo[0], ol, fminf(sec[0], os));
-      li[0] = (ol < lo[0] || (ol == lo[0] && oi < li[0])) ? oi : li[0];
-      lo[0] = fminf(lo[0], ol);
-    }
+    kb_top2_lanes(lo, sec, li, lane);
     // (C) one decision per row, by the even lane of its pair
     const int q = r >> 1;
     const int rt = (q & 3) + 8 * (q >> 2) + 4 * h;
