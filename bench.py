@@ -199,7 +199,12 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
   n = npts * ctx.world_size
   out = {'ms_per_iter': round(el * 1e3, 3), 'points_per_s': round(n / el, 1),
          'gemm_form_tflops': round(2.0 * n * K * D / el / 1e12, 2),
-         'gemm_form_mfma_f32_frac_per_gpu': round(2.0 * n * K * D / el / 1e12 / (157.3 * ctx.world_size), 4),
+         # the filter runs the distance GEMM as three bf16 MFMA products
+         # (bf16x3), so its matrix-core rate is 3x the GEMM-form rate against
+         # the dense bf16 peak; the iteration also streams X twice (assign +
+         # accumulate: 2 * 4 * N * D bytes)
+         'bf16x3_mfma_frac_per_gpu': round(3.0 * 2.0 * n * K * D / el / 1e12 / (2500.0 * ctx.world_size), 4),
+         'hbm_GBps_two_passes': round(2.0 * 4.0 * n * D / el / 1e9, 1),
          'config': 'cfg3: %d x %d fp32 points (U[0,1), seed 21) per GPU, k=%d, centres = first %d points; '
                    'assign = bf16x3-MFMA certified filter + exact-order fp64 recompute of undecided points '
                    '(bit-exact labels), fp64 centroid sums' % (npts, D, K, K)}
