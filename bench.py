@@ -183,8 +183,9 @@ def bench_dot(S, ctx, be, expr, comm, sync):
 
 
 def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
-  """configs[2]: one k-means iteration (exact-order fp64 assign + fp64
-  centroid accumulation + all-reduce) over npts x 128 fp32 points, k=256."""
+  """configs[2]: one k-means iteration (certified bf16x3 filter + exact-order
+  fp64 recompute = scipy-exact labels, fp64 centroid accumulation,
+  all-reduce) over npts x 128 fp32 points, k=256."""
   import torch
   from spartan_amd import workloads
   X = expr.rand(npts * ctx.world_size, D, dtype=np.float32, seed=21).force()
