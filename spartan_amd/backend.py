@@ -338,7 +338,15 @@ class HipBackend:
       strides = [broadcast_strides(tuple(inputs[s].shape), in_shape) for s in slots]
       view = reduce_view(in_shape, strides, axis)
     if view is None:
-      raise NotImplementedError('reduction view not coalescible; materialise the map first')
+      # inputs broadcast along different dims of an N-d iteration space (e.g.
+      # (N, 1, D) - (1, K, D) reduced over the last axis): the rows of the
+      # (O, R, I) form have no single stride.  Materialise the mapped values
+      # with the N-d map kernel, then reduce that dense array.
+      if codegen.rowdots(root):
+        raise NotImplementedError('row-dot reduction over a non-coalescible view')
+      tmp = torch.empty(tuple(in_shape), dtype=torch_dtype(root.dtype), device=out_device(inputs, slots))
+      self.map(root, inputs, tmp)
+      return self.reduce(codegen.In(0, root.dtype), op, {0: tmp}, in_shape, axis, out_shape, out_dtype, idx_geom)
     O, R, I, vstr = view
     dev = out_device(inputs, slots)
     n_out = O * I

@@ -195,8 +195,10 @@ class KMeans(object):
   def fit(self, X, centers=None, implementation='outer'):
     """X: (N, D) array tiled by rows; centers: (K, D) host array / Expr, or
     None (``expr.rand``).  Returns (centers (K, D) host fp64, labels)."""
+    if implementation == 'broadcast':
+      return self._fit_broadcast(X, centers)
     if implementation != 'outer':
-      raise NotImplementedError('implementation %r: only the reference default "outer" is on the path'
+      raise NotImplementedError('implementation %r: "outer" (default) and "broadcast" are on the path'
                                 % implementation)
     num_dim = X.shape[1]
     rng = np.random.default_rng(self.seed)
@@ -216,6 +218,42 @@ class KMeans(object):
                               shape=(centers.shape[0], centers.shape[1]))
       counts = counts.optimized().glom()
       centers = new_centers.optimized().glom()
+      zcount_indices = (counts == 0).reshape(self.n_clusters)
+      if np.any(zcount_indices):
+        n_points = np.count_nonzero(zcount_indices)
+        counts[zcount_indices] = 1
+        centers[zcount_indices, :] = rng.standard_normal((n_points, num_dim))
+      centers = centers / counts.reshape(centers.shape[0], 1)
+      centers = expr.from_numpy(centers)
+    return centers.glom(), labels
+
+  def _fit_broadcast(self, X, centers):
+    """k_means_.py:153-187: the same iteration written with broadcasting
+    only -- (N, 1, D) - (1, K, D) squared and summed over the last axis (one
+    fused map+reduce over the (N, K, D) iteration space, never
+    materialised), argmin, one-hot matches by ``==`` against an arange,
+    counts and centre sums as axis-0 reductions of broadcast products.  The
+    distances are squared sums in the points' dtype (no sqrt, no fp64
+    cdist), so near-tie labels follow this float order, as in the reference."""
+    num_dim = X.shape[1]
+    rng = np.random.default_rng(self.seed)
+    if centers is None:
+      centers = expr.rand(self.n_clusters, num_dim)
+    elif isinstance(centers, np.ndarray):
+      centers = expr.from_numpy(centers)
+    labels = None
+    for i in range(self.n_iter):
+      X_broadcast = expr.reshape(X, (X.shape[0], 1, X.shape[1]))
+      centers_broadcast = expr.reshape(centers, (1, centers.shape[0], centers.shape[1]))
+      distances = expr.sum(expr.square(X_broadcast - centers_broadcast), axis=2)
+      labels = expr.argmin(distances, axis=1)
+      center_idx = expr.arange((1, centers.shape[0]))
+      matches = expr.reshape(labels, (labels.shape[0], 1)) == center_idx
+      matches = matches.astype(np.int64)
+      counts = expr.sum(matches, axis=0)
+      centers = expr.sum(X_broadcast * expr.reshape(matches, (matches.shape[0], matches.shape[1], 1)), axis=0)
+      counts = counts.optimized().glom()
+      centers = centers.optimized().glom()
       zcount_indices = (counts == 0).reshape(self.n_clusters)
       if np.any(zcount_indices):
         n_points = np.count_nonzero(zcount_indices)

@@ -97,6 +97,22 @@ def _run_join_cases(expr, flags):
   np.testing.assert_array_equal(got_l.glom(), wl)
   np.testing.assert_allclose(got_c, wc, rtol=1e-10)
 
+  # the reference's 'broadcast' implementation (k_means_.py:153-187)
+  Xs = X[:120, :5].copy()
+  cs = Xs[:4].copy()
+  got_c, got_l = KMeans(4, 2).fit(expr.from_numpy(Xs), centers=cs, implementation='broadcast')
+  c_np = cs
+  for _ in range(2):
+    d2 = ((Xs[:, None, :] - c_np[None, :, :]) ** 2).sum(2)
+    lab_np = d2.argmin(1)
+    cnt = np.bincount(lab_np, minlength=4)
+    sm = np.zeros((4, 5))
+    np.add.at(sm, lab_np, Xs)
+    cnt = np.where(cnt == 0, 1, cnt)
+    c_np = sm / cnt.reshape(4, 1)
+  np.testing.assert_array_equal(got_l.glom(), lab_np)
+  np.testing.assert_allclose(got_c, c_np, rtol=1e-10)
+
   # bincount / concatenate builtins
   v = (rng.rand((300,), 53, np.float64) * 9).astype(np.int64)
   np.testing.assert_array_equal(expr.bincount(expr.from_numpy(v)).glom(), np.bincount(v))
