@@ -1,5 +1,9 @@
 """Cross-rank data movement for tiles (torch.distributed: RCCL on GPU, gloo in tests).
 
+With ``SPARTAN_DIST_BACKEND=gloo`` on GPUs (rehearsing N ranks on one
+device, e.g. the 1-GPU box) device tensors are staged through host memory,
+since gloo moves host buffers only; the RCCL path never stages.
+
 Replaces the reference's pickled ZeroMQ point-to-point messages
 (spartan/rpc/common.py:52-62, spartan/blob_ctx.py:127-179): every exchange here
 is a collective that all ranks enter with identical arguments, because every
@@ -17,11 +21,20 @@ def _dist():
   return dist
 
 
+def _staged(ctx, t):
+  return ctx.dist_backend == 'gloo' and t.device.type != 'cpu'
+
+
 def all_reduce(t, op):
   ctx = runtime.get()
   if not ctx.distributed:
     return t
   dist = _dist()
+  if _staged(ctx, t):
+    h = t.cpu()
+    dist.all_reduce(h, op=getattr(dist.ReduceOp, _OPS[op]))
+    t.copy_(h)
+    return t
   dist.all_reduce(t, op=getattr(dist.ReduceOp, _OPS[op]))
   return t
 
@@ -31,7 +44,7 @@ def reduce_scatter_rows(out, full, op):
   ctx = runtime.get()
   dist = _dist()
   if ctx.dist_backend == 'gloo':  # gloo has no reduce_scatter: all_reduce + slice
-    dist.all_reduce(full, op=getattr(dist.ReduceOp, _OPS[op]))
+    all_reduce(full, op)
     n = out.shape[0]
     out.copy_(full[ctx.rank * n:(ctx.rank + 1) * n])
     return out
@@ -47,14 +60,25 @@ def all_gather_stack(t):
     return t.unsqueeze(0)
   dist = _dist()
   out = torch.empty((ctx.world_size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-  dist.all_gather_into_tensor(out, t.contiguous()) if ctx.dist_backend != 'gloo' else \
-      dist.all_gather(list(out.unbind(0)), t.contiguous())
+  if _staged(ctx, t):
+    h = torch.empty(out.shape, dtype=t.dtype)
+    dist.all_gather(list(h.unbind(0)), t.contiguous().cpu())
+    out.copy_(h)
+  elif ctx.dist_backend == 'gloo':
+    dist.all_gather(list(out.unbind(0)), t.contiguous())
+  else:
+    dist.all_gather_into_tensor(out, t.contiguous())
   return out
 
 
 def broadcast(t, src_rank):
   ctx = runtime.get()
   if not ctx.distributed:
+    return t
+  if _staged(ctx, t):
+    h = t.cpu()
+    _dist().broadcast(h, src=src_rank)
+    t.copy_(h)
     return t
   _dist().broadcast(t, src=src_rank)
   return t
@@ -73,11 +97,26 @@ def exchange(sends, recvs):
   ctx = runtime.get()
   if not ctx.distributed or (not sends and not recvs):
     return
+  import torch
   dist = _dist()
+  post = []
+  if ctx.dist_backend == 'gloo':  # host staging for device tensors (rehearsal mode)
+    sends = [(t.contiguous().cpu() if _staged(ctx, t) else t, peer) for t, peer in sends]
+    staged = []
+    for t, peer in recvs:
+      if _staged(ctx, t):
+        h = torch.empty(t.shape, dtype=t.dtype)
+        post.append((t, h))
+        staged.append((h, peer))
+      else:
+        staged.append((t, peer))
+    recvs = staged
   ops = [dist.P2POp(dist.isend, t.contiguous(), peer) for t, peer in sends]
   ops += [dist.P2POp(dist.irecv, t, peer) for t, peer in recvs]
   for req in dist.batch_isend_irecv(ops):
     req.wait()
+  for t, h in post:
+    t.copy_(h)
 
 
 def barrier():

@@ -70,10 +70,13 @@ def initialize(argv=None, device=None):
   if world > 1:
     import torch.distributed as dist
     backend = 'nccl' if device.type == 'cuda' else 'gloo'
+    # SPARTAN_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (device
+    # tensors staged through the host by comm.py); RCCL otherwise
+    backend = os.environ.get('SPARTAN_DIST_BACKEND', backend)
     if not dist.is_initialized():
       os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
       kw = {}
-      if device.type == 'cuda':
+      if device.type == 'cuda' and backend == 'nccl':
         kw['device_id'] = device
       dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
   _ctx = Context(rank, world, local_rank, device, backend)

@@ -8,11 +8,16 @@ north_star): integer / index results bit-exact; fp32 1e-5 relative, fp64
 result, or at least as close to the exact (fp64-accumulated) value as the
 reference CPU result is.
 """
+import os
+import sys
+
 import numpy as np
 import pytest
 
 from oracle import rng
 from oracle import spartan_cpu as O
+
+HERE = os.path.dirname(os.path.abspath(__file__))
 
 pytestmark = pytest.mark.gpu
 
@@ -669,3 +674,20 @@ def test_location_gpu(ex, W):
   expr, setw = ex
   setw(W)
   _run_location_cases(expr, W)
+
+
+def test_multirank_rehearsal_gpu(tmp_path):
+  """N = 2 ranks on this one GPU (torchrun, gloo with host staging): the
+  multi-rank tile plans, exchanges and combines with the real kernels."""
+  import subprocess
+  import socket
+  s = socket.socket()
+  s.bind(('127.0.0.1', 0))
+  port = s.getsockname()[1]
+  s.close()
+  env = dict(os.environ, SPARTAN_DIST_BACKEND='gloo', REHEARSAL_WORKERS='3')
+  cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=2',
+         '--master-addr=127.0.0.1', '--master-port=%d' % port, os.path.join(HERE, 'mrank_body.py')]
+  r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
+  assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+  assert r.stdout.count('rehearsal ok') == 2, r.stdout[-2000:]
