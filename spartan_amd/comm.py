@@ -84,6 +84,28 @@ def broadcast(t, src_rank):
   return t
 
 
+def reduce_async(t, dst_rank, op):
+  """Start reducing ``t`` (contiguous, same shape on every rank) into
+  ``t`` on ``dst_rank``; returns a handle for ``wait_all``.  On RCCL the
+  reduction runs on the process group's stream, after the work already
+  queued on the current stream and concurrently with what follows it."""
+  ctx = runtime.get()
+  dist = _dist()
+  if _staged(ctx, t):  # rehearsal: synchronous through the host
+    h = t.cpu()
+    dist.reduce(h, dst=dst_rank, op=getattr(dist.ReduceOp, _OPS[op]))
+    if ctx.rank == dst_rank:
+      t.copy_(h)
+    return None
+  return dist.reduce(t, dst=dst_rank, op=getattr(dist.ReduceOp, _OPS[op]), async_op=True)
+
+
+def wait_all(handles):
+  for h in handles:
+    if h is not None:
+      h.wait()
+
+
 def all_to_all_single(out, inp, out_splits, in_splits):
   _dist().all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits)
   return out

@@ -22,6 +22,7 @@ reference forces a single (M, N) tile on worker 0; values are identical).
 import numpy as np
 
 from .. import backend, comm, runtime
+from ..config import FLAGS
 from ..array import distarray, extent as ext
 from ..array.distarray import LocalWrapper
 from .base import Expr, as_array
@@ -184,6 +185,9 @@ def run_dot(a, b, tile_hint=None):
     requests.append((A.to_base(a_region), dst))
     plan.append((bex, dst))
   got = distarray.gather_regions(a, requests)
+  output = distarray.create(out_shape, dtype, reducer=np.add, tile_hint=tile_hint)
+  if ctx.distributed and len(out_shape) == 2 and FLAGS.dot_overlap and _owner_slabs(output, ctx, M):
+    return _dot_overlapped(output, got, plan, b, B, K, M, N, dtype, C)
   for qi, (bex, dst) in enumerate(plan):
     if dst != ctx.rank:
       continue
@@ -198,8 +202,52 @@ def run_dot(a, b, tile_hint=None):
     beta = 0.0 if (lone and key not in started) else 1.0
     started.add(key)
     be.gemm(at, bt, cview, 1.0, beta)
-  output = distarray.create(out_shape, dtype, reducer=np.add, tile_hint=tile_hint)
   _scatter_full(output, C.reshape(out_shape), 'sum')
+  return output
+
+
+OVERLAPPED_CALLS = 0  # how often the overlapped path ran (tests check it is taken)
+
+
+def _owner_slabs(output, ctx, M):
+  from .engine import _rank_slabs
+  return _rank_slabs(output, ctx) and M % ctx.world_size == 0
+
+
+def _dot_overlapped(output, got, plan, b, B, K, M, N, dtype, C):
+  """K-split partials reduced chunk by chunk while the next chunk computes.
+
+  The output is one row slab per rank.  Every rank computes its partial of
+  slab j (its local K blocks, MFMA GEMM into C[slab j]) and immediately
+  starts an RCCL reduce of that slab to its owner j on the process group's
+  stream; the GEMM of slab j + 1 runs meanwhile on the compute stream.  The
+  bytes moved equal the reduce-scatter's, but the xGMI time hides behind the
+  GEMMs instead of following them."""
+  global OVERLAPPED_CALLS
+  OVERLAPPED_CALLS += 1
+  ctx = runtime.get()
+  be = backend.get()
+  slab = M // ctx.world_size
+  local = []
+  for qi, (bex, dst) in enumerate(plan):
+    if dst != ctx.rank:
+      continue
+    at = _as_dtype(got[qi].reshape(M, bex.shape[0]), dtype)
+    if b.replicated:
+      bt = b.fetch(ext.from_shape(b.shape)).reshape(K, N)
+    else:
+      bt = b.fetch(B.to_base(bex)).reshape(bex.shape)
+    local.append((bex, at, _as_dtype(bt, dtype)))
+  handles = []
+  for j in range(ctx.world_size):
+    r0, r1 = j * slab, (j + 1) * slab
+    for bex, at, bt in local:
+      be.gemm(at[r0:r1], bt, C[r0:r1, bex.ul[1]:bex.lr[1]], 1.0, 1.0)
+    handles.append(comm.reduce_async(C[r0:r1], j, 'sum'))
+  comm.wait_all(handles)
+  (d, t), = output.local.items()
+  t.data = C[ctx.rank * slab:(ctx.rank + 1) * slab].clone()  # free the full-size partial buffer
+  t.written = [d]
   return output
 
 

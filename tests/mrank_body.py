@@ -43,6 +43,15 @@ def main():
   a = rng.rand((96, 80), 1, np.float64)
   b = rng.rand((80, 72), 2, np.float64)
   np.testing.assert_allclose(expr.dot(expr.from_numpy(a), expr.from_numpy(b)).glom(), a @ b, rtol=1e-12)
+  # one output row slab per rank: the overlapped slab-by-slab dot reduction
+  ctx.num_workers = ctx.world_size  # (the context caches FLAGS.num_workers at initialize)
+  dot_mod = sys.modules['spartan_amd.expr.dot']
+  n0 = dot_mod.OVERLAPPED_CALLS
+  a2 = rng.rand((128, 96), 3, np.float32)
+  b2 = rng.rand((96, 80), 4, np.float32)
+  np.testing.assert_allclose(expr.dot(expr.from_numpy(a2), expr.from_numpy(b2)).glom(), a2 @ b2, rtol=1e-5)
+  assert dot_mod.OVERLAPPED_CALLS == n0 + 1
+  ctx.num_workers = W
   from spartan_amd import workloads
   from oracle import workloads as OW
   pts = rng.rand((3000, 64), 21, np.float32)

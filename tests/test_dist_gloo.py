@@ -75,8 +75,12 @@ def _body(rank, world, port, W, q):
     # dot: K-split with the A column-strip exchange and the partial reduction
     a = rng.rand((24, 36), 1, np.float64)
     b = rng.rand((36, 20), 2, np.float64)
+    dot_mod = sys.modules['spartan_amd.expr.dot']
+    n0 = dot_mod.OVERLAPPED_CALLS
     got = expr.dot(expr.from_numpy(a), expr.from_numpy(b)).glom()
     np.testing.assert_allclose(got, a @ b, rtol=1e-12)
+    if W == world:  # one row slab per rank: the overlapped slab reduction ran
+      assert dot_mod.OVERLAPPED_CALLS == n0 + 1
     np.testing.assert_allclose(expr.dot(expr.from_numpy(a), b).glom(), a @ b, rtol=1e-12)
     v = rng.rand((36,), 3, np.float64)
     np.testing.assert_allclose(expr.dot(expr.from_numpy(a), expr.from_numpy(v)).glom(), a @ v, rtol=1e-12)
