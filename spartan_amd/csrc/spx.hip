@@ -1131,11 +1131,17 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
   float* cns = (float*)(Bl + NC * Dp);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, h = lane >> 5;
   {
-    const int D8 = (int)D / 8;
-    for (int i = t; i < NC * D8; i += KB_WAVES * 64) {
-      const int c = i / D8, d = (i % D8) * 8;
-      *(kb_bf8*)&Bh[c * Dp + d] = *(const kb_bf8*)&CBh[(i64)c * D + d];
-      *(kb_bf8*)&Bl[c * Dp + d] = *(const kb_bf8*)&CBl[(i64)c * D + d];
+    // k-order inside every 16-dim step is permuted (dim quads 1 and 2
+    // swapped) so that an A lane's two 16-byte loads are adjacent in its row
+    // (lane h takes dims 4h..4h+3 and 8+4h..8+4h+3): the B rows are stored in
+    // the same order, so the dot products are unchanged up to summation order
+    typedef unsigned int kb_u2 __attribute__((ext_vector_type(2)));
+    const int D4 = (int)D / 4;
+    for (int i = t; i < NC * D4; i += KB_WAVES * 64) {
+      const int c = i / D4, q = i % D4, qi = q & 3;
+      const int pq = (q & ~3) | (qi == 1 ? 2 : qi == 2 ? 1 : qi);
+      *(kb_u2*)&Bh[c * Dp + 4 * pq] = *(const kb_u2*)&CBh[(i64)c * D + 4 * q];
+      *(kb_u2*)&Bl[c * Dp + 4 * pq] = *(const kb_u2*)&CBl[(i64)c * D + 4 * q];
     }
     for (int i = t; i < NC; i += KB_WAVES * 64) cns[i] = cnf[i];
   }
@@ -1158,9 +1164,9 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
   auto load = [&](int s, i64 tl, int ks) {
     i64 row = tl * 32 + r;
     row = row < N ? row : N - 1;
-    const float* p = P + row * ldp + ks * 16 + 8 * h;
-    ra[s][0] = *(const kb_f4*)p;  // (nt measured no faster here)
-    ra[s][1] = *(const kb_f4*)(p + 4);
+    const float* p = P + row * ldp + ks * 16 + 4 * h;
+    ra[s][0] = *(const kb_f4*)p;  // dims 4h..4h+3 (nt measured no faster here)
+    ra[s][1] = *(const kb_f4*)(p + 8);  // dims 8+4h..8+4h+3
   };
 #pragma unroll
   for (int s = 0; s < 4; ++s) load(s, tile, s);
