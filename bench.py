@@ -40,7 +40,7 @@ def main():
   ap.add_argument('--dot', type=int, default=1, help='also time the dot config (1/0)')
   ap.add_argument('--dot-size', type=int, default=32768)
   ap.add_argument('--cpu-baseline', type=int, default=1)
-  ap.add_argument('--cpu-rows', type=int, default=4096)
+  ap.add_argument('--cpu-rows', type=int, default=32768, help='rows of the CPU baseline sample (full cfg2 strip: ~10-20 s of CPU work)')
   ap.add_argument('--strong', action='store_true', help='fixed 2^30 global array (strong scaling)')
   ap.add_argument('--workloads', type=int, default=1, help='also time k-means (cfg3) and lreg (cfg5)')
   ap.add_argument('--km-points', type=int, default=100000000)
@@ -147,7 +147,7 @@ def main():
 
   if args.cpu_baseline and N == 1 and ctx.rank == 0:
     from oracle.cpu_baseline import cfg2_cpu_baseline
-    cb = cfg2_cpu_baseline(rows=min(args.cpu_rows, S), cols=S)
+    cb = cfg2_cpu_baseline(rows=min(args.cpu_rows, S), cols=S, reps=5)
     result['cpu_baseline'] = {k: cb[k] for k in ('value', 'unit', 'cores', 'kind', 'sample')}
     result['cpu_baseline']['value'] = round(cb['value'], 3)
   if ctx.rank == 0:
