@@ -688,6 +688,6 @@ def test_multirank_rehearsal_gpu(tmp_path):
   env = dict(os.environ, SPARTAN_DIST_BACKEND='gloo', REHEARSAL_WORKERS='3')
   cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=2',
          '--master-addr=127.0.0.1', '--master-port=%d' % port, os.path.join(HERE, 'mrank_body.py')]
-  r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
+  r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
   assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
   assert r.stdout.count('rehearsal ok') == 2, r.stdout[-2000:]
