@@ -691,3 +691,36 @@ def test_multirank_rehearsal_gpu(tmp_path):
   r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
   assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
   assert r.stdout.count('rehearsal ok') == 2, r.stdout[-2000:]
+
+
+@pytest.mark.parametrize('W', [1, 3])
+def test_nonfinite_reductions(ex, W):
+  """NaN / +-inf through sum / min / max / argmin / argmax, across tiles:
+  NaN propagates as in np.minimum / np.maximum (the reference's accumulate
+  functions), arg-reductions return the first NaN (numpy's rule)."""
+  expr, setw = ex
+  setw(W)
+  a = rng.rand((37, 23), 71, np.float32)
+  a[3, 5] = np.nan
+  a[20, 7] = np.inf
+  a[30, 11] = -np.inf
+  a[31, 5] = np.nan
+  A = expr.from_numpy(a)
+  for axis in (None, 0, 1):
+    np.testing.assert_array_equal(expr.min(A, axis).glom(), np.min(a, axis))
+    np.testing.assert_array_equal(expr.max(A, axis).glom(), np.max(a, axis))
+    np.testing.assert_array_equal(A.argmin(axis).glom(), a.argmin(axis))
+    np.testing.assert_array_equal(A.argmax(axis).glom(), a.argmax(axis))
+    got = np.asarray(expr.sum(A, axis).glom(), dtype=np.float64)
+    want = np.sum(a.astype(np.float64), axis)
+    np.testing.assert_array_equal(np.isnan(got), np.isnan(want))
+  b = rng.rand((37, 23), 72, np.float64)
+  b[:, 4] = np.inf
+  b[9, 4] = -np.inf
+  B = expr.from_numpy(b)
+  for axis in (None, 0, 1):
+    got = np.asarray(expr.sum(B, axis).glom())
+    want = np.sum(b, axis)
+    np.testing.assert_array_equal(np.isnan(got), np.isnan(want))
+    np.testing.assert_array_equal(np.isinf(got), np.isinf(want))
+    np.testing.assert_array_equal(A.argmin(axis).glom(), a.argmin(axis))
