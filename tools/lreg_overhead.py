@@ -30,4 +30,4 @@ pr.enable()
 workloads.sgd_train(X, Y, w, 1e-6, iters)
 torch.cuda.synchronize()
 pr.disable()
-pstats.Stats(pr).sort_stats('cumulative').print_stats(35)
+pstats.Stats(pr).sort_stats("tottime").print_stats(30)
