@@ -341,10 +341,19 @@ class HipBackend:
       # inputs broadcast along different dims of an N-d iteration space (e.g.
       # (N, 1, D) - (1, K, D) reduced over the last axis): the rows of the
       # (O, R, I) form have no single stride.  Materialise the mapped values
-      # with the N-d map kernel, then reduce that dense array.
+      # with the N-d map kernel, then reduce that dense array -- in slabs of a
+      # kept dim when the whole iteration space exceeds MATERIALISE_LIMIT bytes.
       if codegen.rowdots(root):
         raise NotImplementedError('row-dot reduction over a non-coalescible view')
-      tmp = torch.empty(tuple(in_shape), dtype=torch_dtype(root.dtype), device=out_device(inputs, slots))
+      dev = out_device(inputs, slots)
+      esize = np.dtype(root.dtype).itemsize
+      total = prod(in_shape) * esize
+      if axis is not None and total > self.MATERIALISE_LIMIT:
+        kept = [d for d in range(len(in_shape)) if d != axis and in_shape[d] > 1]
+        if kept:
+          return self._reduce_slabs(root, op, inputs, tuple(in_shape), axis, tuple(out_shape), out_dtype,
+                                    idx_geom, kept[0], dev)
+      tmp = torch.empty(tuple(in_shape), dtype=torch_dtype(root.dtype), device=dev)
       self.map(root, inputs, tmp)
       return self.reduce(codegen.In(0, root.dtype), op, {0: tmp}, in_shape, axis, out_shape, out_dtype, idx_geom)
     O, R, I, vstr = view
@@ -511,6 +520,38 @@ class HipBackend:
                                     _arr(tuple(dst.shape)), _arr(dst_ul), spx_dtype(np_dtype(src.dtype)),
                                     ctypes.c_void_p(src.data_ptr()), _arr(tuple(src.shape)), _arr(src_ul), nd,
                                     _arr(shape), self.stream()), 'spx_copy_region')
+
+  MATERIALISE_LIMIT = 2 << 30  # bytes of one materialised slab (non-coalescible reductions)
+
+  def _reduce_slabs(self, root, op, inputs, in_shape, axis, out_shape, out_dtype, idx_geom, d, dev):
+    """reduce() over slabs of the kept dim ``d`` (each slab materialised and
+    reduced on its own), results copied into place."""
+    import torch
+    nd = len(in_shape)
+    per = prod(in_shape) // in_shape[d] * np.dtype(root.dtype).itemsize
+    nc = max(1, self.MATERIALISE_LIMIT // max(1, per))
+    od = d if d < axis else d - 1  # the same dim in the output
+    arg = op in ('argmin', 'argmax')
+    res_v = res_i = None
+    for c0 in range(0, in_shape[d], nc):
+      c1 = min(in_shape[d], c0 + nc)
+      sub = {}
+      for sl, t in inputs.items():
+        td = d - (nd - t.dim())  # inputs broadcast from the right
+        sub[sl] = t.narrow(td, c0, c1 - c0) if td >= 0 and t.shape[td] == in_shape[d] else t
+      sshape = in_shape[:d] + (c1 - c0,) + in_shape[d + 1:]
+      soshape = out_shape[:od] + (c1 - c0,) + out_shape[od + 1:]
+      got = self.reduce(root, op, sub, sshape, axis, soshape, out_dtype, idx_geom)
+      ul = tuple(c0 if k == od else 0 for k in range(len(out_shape)))
+      parts = got if arg else (got,)
+      if res_v is None:
+        res_v = torch.empty(out_shape, dtype=parts[0].dtype, device=dev)
+        if arg:
+          res_i = torch.empty(out_shape, dtype=parts[1].dtype, device=dev)
+      self.copy_region(res_v, ul, parts[0], (0,) * len(out_shape), soshape)
+      if arg:
+        self.copy_region(res_i, ul, parts[1], (0,) * len(out_shape), soshape)
+    return (res_v, res_i) if arg else res_v
 
   # ----------------------------------------------------------------- gemm
   def gemm(self, A, B, C, alpha=1.0, beta=0.0):

@@ -724,3 +724,30 @@ def test_nonfinite_reductions(ex, W):
     np.testing.assert_array_equal(np.isnan(got), np.isnan(want))
     np.testing.assert_array_equal(np.isinf(got), np.isinf(want))
     np.testing.assert_array_equal(A.argmin(axis).glom(), a.argmin(axis))
+
+
+@pytest.mark.parametrize('limit', [None, 4096])
+def test_broadcast_reduce_views(ex, limit):
+  """Reductions whose inputs broadcast along different dims ((N,1,D) - (1,K,D)
+  and friends): materialised then reduced, whole or -- above the byte limit
+  -- in slabs of a kept dim; every axis, sum and argmin."""
+  from spartan_amd import backend
+  expr, setw = ex
+  setw(2)
+  be = backend.get()
+  old = be.MATERIALISE_LIMIT
+  if limit is not None:
+    be.MATERIALISE_LIMIT = limit
+  try:
+    X = rng.rand((50, 6), 81, np.float64)
+    C = rng.rand((7, 6), 82, np.float64)
+    Xb = expr.reshape(expr.from_numpy(X), (50, 1, 6))
+    Cb = expr.reshape(expr.from_numpy(C), (1, 7, 6))
+    d3 = (X[:, None, :] - C[None, :, :]) ** 2
+    for axis in (0, 1, 2):
+      np.testing.assert_allclose(expr.sum(expr.square(Xb - Cb), axis=axis).optimized().glom(), d3.sum(axis),
+                                 rtol=1e-12)
+      np.testing.assert_array_equal(expr.argmin(expr.square(Xb - Cb), axis=axis).optimized().glom(),
+                                    d3.argmin(axis))
+  finally:
+    be.MATERIALISE_LIMIT = old
