@@ -751,3 +751,14 @@ def test_broadcast_reduce_views(ex, limit):
                                     d3.argmin(axis))
   finally:
     be.MATERIALISE_LIMIT = old
+
+
+@pytest.mark.parametrize('W', [1, 3])
+def test_optimization_dags_gpu(ex, W):
+  """tests/test_optimization.py's nonordered / reduced DAGs at the reference's
+  size (1000 x 1000 fp64): slices of fused maps, a dot of slices, a sum."""
+  from test_views import _optimization_dag_cases
+  expr, setw = ex
+  setw(W)
+  for name, e, want in _optimization_dag_cases(expr, 1000):
+    np.testing.assert_allclose(e.optimized().glom(), want, rtol=1e-10, err_msg=name)

@@ -85,3 +85,80 @@ def test_fancy_indexing_is_refused(host_ctx):
   x = expr.arange((5, 5))
   with pytest.raises(NotImplementedError):
     x[np.array([1, 2])]
+
+
+def _optimization_dag_cases(expr, n=1000):
+  """The reference's tests/test_optimization.py:9-44 (nonordered) and
+  :124-163 (reduced): maps, slices of maps, a dot of slices and a final sum,
+  optimised as one DAG."""
+  na = rng.rand((n, n), 91, np.float64)
+  nb = rng.rand((n, n), 92, np.float64)
+  a = expr.from_numpy(na)
+  b = expr.from_numpy(nb)
+  s1, s2, s3 = slice(n // 5, 9 * n // 10), slice(n // 10, n // 2), slice(n // 10, n // 5)
+  c = a + b
+  d = a + c
+  f = c[s1, s1]
+  g = d[s1, s1]
+  h = f + g
+  i = f + h
+  j = h[s2, s2]
+  k = i[s2, s2]
+  l = expr.dot(j, k)
+  m = j + k
+  nn = k + l
+  o = nn + m
+  q = o[s3, s3]
+  nc = na + nb
+  nd = na + nc
+  nf = nc[s1, s1]
+  ng = nd[s1, s1]
+  nh = nf + ng
+  ni = nf + nh
+  nj = nh[s2, s2]
+  nk = ni[s2, s2]
+  nl = nj @ nk
+  nm = nj + nk
+  nno = nk + nl
+  no = nno + nm
+  nq = no[s3, s3]
+  out = [('nonordered', q, nq)]
+  c = a - b
+  d = a + c
+  f = c[s1, s1]
+  g = d[s1, s1]
+  h = f - g
+  i = f + h
+  j = h[s2, s2]
+  k = i[s2, s2]
+  l = expr.dot(j, k)
+  m = j + k
+  nn = k - l
+  o = nn - m
+  q = nn + o
+  r = q - m
+  s = expr.sum(r)
+  nc = na - nb
+  nd = na + nc
+  nf = nc[s1, s1]
+  ng = nd[s1, s1]
+  nh = nf - ng
+  ni = nf + nh
+  nj = nh[s2, s2]
+  nk = ni[s2, s2]
+  nl = nj @ nk
+  nm = nj + nk
+  nno = nk - nl
+  no = nno - nm
+  nq = nno + no
+  nr = nq - nm
+  out.append(('reduced', s, nr.sum()))
+  return out
+
+
+@pytest.mark.parametrize('W', [1, 3])
+def test_optimization_dags_host(host_ctx, W):
+  host_ctx(W)
+  from spartan_amd import expr
+  for name, e, want in _optimization_dag_cases(expr, 200):
+    np.testing.assert_allclose(e.optimized().glom(), want, rtol=1e-10, err_msg=name)
