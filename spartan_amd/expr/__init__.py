@@ -5,7 +5,7 @@ from .base import (Expr, NotShapeable, as_array, eager, evaluate, force, glom, l
 from .builtins import (abs, add, arange, argmax, argmin, astype, bincount, concatenate, count_nonzero,
                        count_zero, exp,
                        ln, log, maximum, max, mean, min, minimum, multiply, ones, power, rand, randn,
-                       size, sqrt, square, sub, sum, zeros)
+                       size, sqrt, square, std, sub, sum, zeros)
 from .dot import dot
 from .join import map2, outer
 from .map import map

@@ -223,6 +223,14 @@ def mean(x, axis=None):
   return map((s, n), fn=np.true_divide)
 
 
+def std(a, axis=None):
+  """Standard deviation (builtins.py:549-565): sqrt(mean(a^2) - mean(a)^2) in
+  fp64, i.e. two fused map+reduce passes (x*x summed, x summed) and one
+  elementwise map over the two partial results."""
+  a64 = astype(a, np.float64)
+  return sqrt(mean(a64 ** 2, axis) - mean(a64, axis) ** 2)
+
+
 def _int64(input):
   return np.dtype(np.int64)
 
