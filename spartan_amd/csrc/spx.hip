@@ -1544,10 +1544,15 @@ constexpr int KA_DB = 64;                  // columns per tile = lanes per wave
 constexpr int KA_WAVES = KA_THREADS / 64;  // centre owners per tile
 constexpr int KA_CPW = 16;                 // centres per wave (register sums)
 constexpr int KA_CB = KA_WAVES * KA_CPW;   // centres per tile
-constexpr int KA_STAGES = 4;               // register prefetch ring depth
+#ifndef KA_STAGES
+#define KA_STAGES 3                        // register prefetch ring depth (chunks per barrier): 3 -> 10.1 ms, 2 -> 10.2, 4 -> 10.7, 1 -> 11.8 at cfg3 (profiles/r01_ka_variants.txt)
+#endif
+#ifndef KA_BPC
+#define KA_BPC 1                           // resident blocks per CU (LDS: 2 KA_STAGES x 16 KiB per block)
+#endif
 
 template <typename TP>
-__global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_kmeans_accum(i64 N, i64 D, i64 K, const TP* __restrict__ P, i64 ldp,
+__global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(4 * KA_BPC, 8))) void k_kmeans_accum(i64 N, i64 D, i64 K, const TP* __restrict__ P, i64 ldp,
                                                              const i64* __restrict__ labels, double* __restrict__ psum,
                                                              unsigned long long* __restrict__ pcnt, int ndb) {
   constexpr int VE = 16 / (int)sizeof(TP);                // elements per 16-byte load
@@ -1676,7 +1681,7 @@ static void ka_grid(int dtype, i64 N, i64 D, i64 K, i64* G, i64* ndb, i64* ncb) 
   *ndb = (D + KA_DB - 1) / KA_DB;
   *ncb = (K + KA_CB - 1) / KA_CB;
   const i64 nch = (N + ch - 1) / ch;
-  i64 g = 256 / (*ndb * *ncb);  // one block per CU over all tiles
+  i64 g = 256 * KA_BPC / (*ndb * *ncb);  // KA_BPC blocks per CU over all tiles
   if (g < 1) g = 1;
   if (g > nch) g = nch;
   *G = g < 1 ? 1 : g;
