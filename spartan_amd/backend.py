@@ -378,7 +378,7 @@ class HipBackend:
       for d in range(3):
         args.str[s][d] = vstr[k][d]
     args.dim[0], args.dim[1], args.dim[2] = O, R, I
-    target_blocks = 2048
+    target_blocks = int(os.environ.get('SPX_REDUCE_BLOCKS', '2048'))  # env: dev knob (experiments only)
     if I == 1 and R <= 64 * V * 16:
       # short segments: several per wave (LPR lanes each), grid-stride over O
       kind = 'rowsp'

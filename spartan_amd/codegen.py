@@ -435,6 +435,8 @@ def cols_unroll(inputs, classes, vec, row_strides=None):
   columns ('b') or along the reduced rows (row stride 0, e.g. the (1, K) row
   vector of a fused row dot) cost no HBM stream; one row of 3 contiguous
   fp32x4 inputs is 3 KiB per wave."""
+  if os.environ.get('SPX_COLS_UNROLL'):  # dev knob (tools/, experiments only)
+    return int(os.environ['SPX_COLS_UNROLL'])
   streamed = 0
   for k, ((s, dt), cls) in enumerate(zip(inputs, classes)):
     if cls != 'b' and not (row_strides is not None and row_strides[k] == 0):
