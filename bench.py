@@ -140,7 +140,11 @@ def main():
 
   def leg(fn, *a):
     # a failing secondary leg is reported in the line, not allowed to take
-    # the cfg2 headline down with it
+    # the cfg2 headline down with it; each leg starts from a clean host state
+    import gc
+    from spartan_amd.expr.base import eval_cache
+    eval_cache.clear()
+    gc.collect()
     try:
       return fn(*a)
     except Exception as e:  # noqa: BLE001
@@ -151,8 +155,8 @@ def main():
     result['dot'] = leg(bench_dot, args.dot_size, ctx, be, expr, comm, sync)
 
   if args.workloads:
-    result['kmeans'] = leg(bench_kmeans, args.km_points, ctx, expr, comm, sync)
     result['lreg'] = leg(bench_lreg, args.lreg_points, ctx, expr, comm, sync)
+    result['kmeans'] = leg(bench_kmeans, args.km_points, ctx, expr, comm, sync)
 
   if args.cpu_baseline and N == 1 and ctx.rank == 0:
     from oracle.cpu_baseline import cfg2_cpu_baseline
@@ -223,7 +227,7 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
   return out
 
 
-def bench_lreg(npts, ctx, expr, comm, sync, D=64, iters=5):
+def bench_lreg(npts, ctx, expr, comm, sync, D=64, iters=10):
   """configs[4]: linear-regression gradient step X^T(Xw - y) + all-reduce."""
   import torch
   from spartan_amd import workloads
@@ -231,7 +235,7 @@ def bench_lreg(npts, ctx, expr, comm, sync, D=64, iters=5):
   Y = expr.rand(npts * ctx.world_size, 1, dtype=np.float32, seed=42).force()
   w = np.random.default_rng(43).random((D, 1)).astype(np.float32)
   Xe, Ye = expr.lazify(X), expr.lazify(Y)
-  workloads.linear_regression_update(Xe, Ye, w, 1e-6)
+  workloads.sgd_train(Xe, Ye, w, 1e-6, 2)  # warm-up (kernel compile / load, plan caches)
   sync()
   comm.barrier()
   t0 = time.perf_counter()
