@@ -67,7 +67,8 @@ class DotExpr(Expr):
 
 def dot(a, b, tile_hint=None):
   """Matrix / vector product of two arrays (dot.py:238-283)."""
-  if not isinstance(b, Expr) and not isinstance(b, np.ndarray):
+  from ..array.distarray import DistArray
+  if not isinstance(b, (Expr, np.ndarray, DistArray)):  # forced DistArrays stay device operands
     b = np.asarray(b)
   e = DotExpr(matrix_a=as_array(a), matrix_b=as_array(b) if not isinstance(b, np.ndarray) else b)
   e.tile_hint = tile_hint

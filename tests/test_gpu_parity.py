@@ -762,3 +762,16 @@ def test_optimization_dags_gpu(ex, W):
   setw(W)
   for name, e, want in _optimization_dag_cases(expr, 1000):
     np.testing.assert_allclose(e.optimized().glom(), want, rtol=1e-10, err_msg=name)
+
+
+@pytest.mark.parametrize('W', WORKERS)
+def test_dot_forced_operands_gpu(ex, W):
+  """dot() of forced DistArrays (device operands, no host round trip)."""
+  expr, setw = ex
+  setw(W)
+  for dt in (np.float32, np.float64):
+    a = expr.rand(96, 160, dtype=dt, seed=3).force()
+    b = expr.rand(160, 72, dtype=dt, seed=4).force()
+    na, nb = rng.rand((96, 160), 3, dt), rng.rand((160, 72), 4, dt)
+    exact = na.astype(np.float64) @ nb.astype(np.float64)
+    check_fp(expr.dot(a, b).glom(), O.dot_tiles(na, nb, W), exact, 1e-5 if dt == np.float32 else 1e-12)

@@ -223,3 +223,15 @@ def test_automatic_tiling(host_ctx):
     assert hints(expr.sum(expr.rand(n, m, seed=5), axis=0).optimized()) == [None]
   finally:
     FLAGS.opt_auto_tiling = True
+
+
+def test_dot_forced_operands(host_ctx):
+  """dot() of already-forced DistArrays keeps them as device operands (the
+  reference's dot takes any non-ndarray operand as an array, dot.py:238-283)."""
+  import numpy as np
+  from spartan_amd import expr
+  host_ctx(2)
+  a, b = expr.arange((30, 20)).force(), expr.arange((20, 10)).force()
+  na, nb = np.arange(600.).reshape(30, 20), np.arange(200.).reshape(20, 10)
+  np.testing.assert_array_equal(expr.dot(a, b).glom(), na @ nb)
+  np.testing.assert_array_equal(expr.dot(a, expr.arange((20,)).force()).glom(), na @ np.arange(20.))
