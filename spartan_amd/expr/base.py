@@ -248,7 +248,8 @@ class AsArray(Expr):
     return np.shape(self.val)
 
   def compute_dtype(self):
-    return np.asarray(self.val).dtype
+    dt = getattr(self.val, 'dtype', None)  # DistArray / ndarray: no host materialisation
+    return np.dtype(dt) if dt is not None else np.asarray(self.val).dtype
 
   def _evaluate(self, deps):
     return distarray.as_array(self.val)

@@ -19,11 +19,10 @@ def divup(a, b):
 
 
 def is_iterable(x):
-  try:
-    iter(x)
-    return True
-  except TypeError:
-    return False
+  """util.py:412-413: an explicit ``__iter__`` (a DistArray, which only has
+  ``__getitem__`` / ``__len__``, is ONE operand, not a sequence of rows;
+  Python-2 ``str`` had no ``__iter__`` either)."""
+  return hasattr(x, '__iter__') and not isinstance(x, (str, bytes))
 
 
 def prod(shape):

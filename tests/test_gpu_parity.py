@@ -775,3 +775,17 @@ def test_dot_forced_operands_gpu(ex, W):
     na, nb = rng.rand((96, 160), 3, dt), rng.rand((160, 72), 4, dt)
     exact = na.astype(np.float64) @ nb.astype(np.float64)
     check_fp(expr.dot(a, b).glom(), O.dot_tiles(na, nb, W), exact, 1e-5 if dt == np.float32 else 1e-12)
+
+
+@pytest.mark.parametrize('W', WORKERS)
+def test_map_forced_operands_gpu(ex, W):
+  """Fused map / reduce over forced DistArrays (one operand each)."""
+  expr, setw = ex
+  setw(W)
+  a = expr.rand(130, 70, dtype=np.float32, seed=5).force()
+  na = rng.rand((130, 70), 5, np.float32)
+  np.testing.assert_allclose(expr.exp(a).glom(), np.exp(na), rtol=1e-6)
+  np.testing.assert_array_equal(expr.map((a, a), np.multiply).glom(), na * na)
+  got = expr.sum(expr.map(a, np.sqrt), axis=0).optimized().glom()
+  mapped = np.sqrt(na)
+  check_fp(got, O.sum_tiles(mapped, 0, W), mapped.astype(np.float64).sum(0), 1e-5)

@@ -235,3 +235,18 @@ def test_dot_forced_operands(host_ctx):
   na, nb = np.arange(600.).reshape(30, 20), np.arange(200.).reshape(20, 10)
   np.testing.assert_array_equal(expr.dot(a, b).glom(), na @ nb)
   np.testing.assert_array_equal(expr.dot(a, expr.arange((20,)).force()).glom(), na @ np.arange(20.))
+
+
+def test_map_forced_operands(host_ctx):
+  """map / ufunc builtins over forced DistArrays: one operand each (the
+  reference's util.is_iterable looks for __iter__, which a DistArray lacks),
+  dtype from the array, never a host materialisation."""
+  import numpy as np
+  from spartan_amd import expr
+  host_ctx(2)
+  a = expr.arange((12, 8)).force()
+  na = np.arange(96.).reshape(12, 8)
+  np.testing.assert_array_equal(expr.map(a, np.sqrt).glom(), np.sqrt(na))
+  np.testing.assert_array_equal(expr.map((a, a), np.add).glom(), na + na)
+  np.testing.assert_array_equal(expr.astype(a, np.float32).glom(), na.astype(np.float32))
+  np.testing.assert_allclose(expr.std(a, 0).glom(), na.std(0), rtol=1e-12)
