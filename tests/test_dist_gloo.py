@@ -54,6 +54,15 @@ def _body(rank, world, port, W, q):
       np.testing.assert_array_equal(X.argmax(axis).glom(), nx.argmax(axis))
       np.testing.assert_array_equal(expr.min(X, axis).glom(), nx.min(axis))
 
+    # forced DistArrays as direct operands of dot / map (tiles on both ranks)
+    xf = expr.arange((40, 30)).force()
+    nxf = np.arange(1200.).reshape(40, 30)
+    yf = expr.arange((30, 20)).force()
+    np.testing.assert_array_equal(expr.dot(xf, yf).glom(), nxf @ np.arange(600.).reshape(30, 20))
+    np.testing.assert_array_equal(expr.map(xf, np.sqrt).glom(), np.sqrt(nxf))
+    np.testing.assert_allclose(expr.sum(expr.sqrt(xf), 0).glom(), O.sum_tiles(np.sqrt(nxf), 0, W),
+                               rtol=1e-12)
+
     # fused cfg2 class over ranks
     shape = (64, 48)
     xs = expr.rand(*shape, dtype=np.float32, seed=11)
