@@ -30,6 +30,13 @@ def main():
   for axis in (None, 0, 1):
     np.testing.assert_array_equal(X.sum(axis).glom(), O.sum_tiles(nx, axis, W))
     np.testing.assert_array_equal(X.argmin(axis).glom(), nx.argmin(axis))
+  # forced DistArrays as direct dot / map / fused-reduce operands
+  xf = expr.arange((40, 30)).force()
+  nxf = np.arange(1200.).reshape(40, 30)
+  yf = expr.arange((30, 20)).force()
+  np.testing.assert_array_equal(expr.dot(xf, yf).glom(), nxf @ np.arange(600.).reshape(30, 20))
+  np.testing.assert_allclose(expr.map(xf, np.sqrt).glom(), np.sqrt(nxf), rtol=1e-15)
+  np.testing.assert_allclose(expr.sum(expr.sqrt(xf), 0).glom(), O.sum_tiles(np.sqrt(nxf), 0, W), rtol=1e-12)
   shape = (64, 48)
   xs = expr.rand(*shape, dtype=np.float32, seed=11)
   ys = expr.rand(*shape, dtype=np.float32, seed=12)
