@@ -51,6 +51,9 @@ def compute_extents(shape, tile_hint=None, num_shards=-1):
   """{extent: worker} in itertools.product order (distarray.py:69-106)."""
   if len(shape) == 0:
     return {ext.create([], [], ()): 0}
+  if any(int(d) == 0 for d in shape):
+    # TileExtent has no empty extent (extent.pyx:141-153 returns None for ul >= lr)
+    raise ValueError('zero-size arrays are not supported: shape %s' % (tuple(shape),))
   if tile_hint is None:
     tile_hint = good_tile_shape(shape, num_shards)
   else:
