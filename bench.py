@@ -31,7 +31,46 @@ MFMA_F32_TFS = 157.3       # dense fp32 MFMA (v_mfma_f32_32x32x2_f32)
 MFMA_F64_TFS = 78.6        # dense fp64 MFMA
 
 
+def launch_ranks(n, argv):
+  """``--gpus N`` without a torchrun environment: start N ranks with
+  torch.distributed.run as a CHILD process (never exec: this process has not
+  touched the GPU and must not be replaced), relay rank 0's JSON line and
+  exit with the child's status (non-zero if any rank failed).  Reference
+  harness: tests/test_common.py:102-121 sweeps its worker counts itself."""
+  import socket
+  import subprocess
+  s = socket.socket()
+  s.bind(('127.0.0.1', 0))
+  port = s.getsockname()[1]
+  s.close()
+  cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(n),
+         '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.abspath(__file__)] + argv
+  env = dict(os.environ)
+  env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+  proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True)
+  line = None
+  for raw in proc.stdout:  # stream: progress lines pass through as they come
+    if raw.startswith('{') and '"metric"' in raw:
+      line = raw.strip()
+    else:
+      sys.stdout.write(raw)
+      sys.stdout.flush()
+  rc = proc.wait()
+  if line is not None:
+    print(line, flush=True)
+  if rc != 0 or line is None:
+    sys.stderr.write('bench.py: %d-rank run failed (exit %d%s)\n' % (n, rc, '' if line else ', no result line'))
+    return rc or 1
+  return 0
+
+
 def main():
+  if '--gpus' in sys.argv or any(a.startswith('--gpus=') for a in sys.argv):
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument('--gpus', type=int, default=1)
+    known, _ = pre.parse_known_args()
+    if known.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+      sys.exit(launch_ranks(known.gpus, sys.argv[1:]))
   ap = argparse.ArgumentParser()
   ap.add_argument('--gpus', type=int, default=1)
   ap.add_argument('--steps', type=int, default=10)
@@ -56,6 +95,8 @@ def main():
   assert isinstance(be, backend.HipBackend)
   S = args.size
   N = ctx.world_size
+  if N != args.gpus:
+    raise SystemExit('bench.py: --gpus %d but the launcher started %d ranks' % (args.gpus, N))
 
   def sync():
     torch.cuda.synchronize()
@@ -112,6 +153,8 @@ def main():
       'value': round(value, 2),
       'unit': 'GB/s',
       'n_gpus': N,
+      'n_ranks_seen': _ranks_seen(),
+      'dist_backend': ctx.dist_backend,
       'steps': args.steps,
       'warmup': args.warmup,
       'ms_per_step': round(elapsed / args.steps * 1e3, 4),
@@ -168,30 +211,46 @@ def main():
   spartan_amd.shutdown()
 
 
-def bench_dot(S, ctx, be, expr, comm, sync):
-  """dot(A, B) for S x S fp32 and fp64 (configs[3]); GFLOP/s over all ranks."""
+def _ranks_seen():
+  import torch.distributed as dist
+  return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def bench_dot(S, ctx, be, expr, comm, sync, runs=10, warm=2):
+  """dot(A, B) for S x S fp32 and fp64 (configs[3]); GFLOP/s over all ranks.
+  SURVEY.md 8(d): median of ``runs`` timed evaluations after ``warm``
+  warm-ups, each bracketed by barrier + synchronize, max over ranks."""
   import torch
   out = {}
   for dt, peak in ((np.float32, MFMA_F32_TFS), (np.float64, MFMA_F64_TFS)):
     a = expr.rand(S, S, dtype=dt, seed=31).force()
     b = expr.rand(S, S, dtype=dt, seed=32).force()
     A, B = expr.lazify(a), expr.lazify(b)
-    expr.dot(A, B).force()  # warm-up (JIT-free: spx_gemm is ahead-of-time)
-    sync()
-    comm.barrier()
-    be.kernel_events = None
-    t0 = time.perf_counter()
-    c = expr.dot(A, B).force()
-    sync()
-    comm.barrier()
-    el = comm.max_over_ranks(time.perf_counter() - t0)
+    for _ in range(warm):  # JIT-free: spx_gemm is ahead-of-time
+      c = expr.dot(A, B).force()
+      del c
+    times = []
+    for _ in range(runs):
+      sync()
+      comm.barrier()
+      sync()
+      t0 = time.perf_counter()
+      c = expr.dot(A, B).force()
+      sync()
+      comm.barrier()
+      sync()
+      times.append(comm.max_over_ranks(time.perf_counter() - t0))
+      del c
+    el = float(np.median(times))
     flops = 2.0 * S ** 3
     name = 'f32' if dt == np.float32 else 'f64'
     out[name] = {'gflops': round(flops / el / 1e9, 1), 'seconds': round(el, 4),
+                 'seconds_min_max': [round(min(times), 4), round(max(times), 4)],
                  'mfma_frac_per_gpu': round(flops / el / 1e12 / (peak * ctx.world_size), 4)}
-    del a, b, A, B, c
+    del a, b, A, B
     torch.cuda.empty_cache()
-  out['config'] = 'dot(A, B), A, B ~ U[0,1) (%d, %d), K-split over ranks' % (S, S)
+  out['config'] = ('dot(A, B), A, B ~ U[0,1) (%d, %d), K-split over ranks; median of %d runs after %d warm-ups'
+                   % (S, S, runs, warm))
   return out
 
 

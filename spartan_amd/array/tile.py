@@ -104,8 +104,10 @@ def merge(tile, region, update, reducer_op):
     return tile
   if reducer_op is None or _disjoint(region, tile.written):
     be.copy_region(tile.data, local_ul, update, (0,) * len(local_ul), region.shape)
+    tile.mask = None  # these branches do not set mask bits: rebuild from `written` when next needed
   elif _covered(region, tile.written):
     be.merge(tile.data, None, local_ul, update, reducer_op, fastpath=False)
+    tile.mask = None
   else:
     if tile.mask is None:
       import torch

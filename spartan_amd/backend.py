@@ -492,6 +492,15 @@ class HipBackend:
     return out
 
   # ------------------------------------------------------------ finalize
+  def finalize(self, op, parts, P, n, out):
+    """out[i] = fold over p < P of parts[p * n + i] in p order (sum / min /
+    max; NaN propagates for min / max like np.minimum / np.maximum)."""
+    dt = spx_dtype(np_dtype(parts.dtype))
+    _check(self.lib.spx_reduce_finalize(OP_CODE[op], dt, spx_dtype(np_dtype(out.dtype)),
+                                        ctypes.c_void_p(parts.data_ptr()), ctypes.c_void_p(0), P, n,
+                                        ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(0), self.stream()),
+           'spx_reduce_finalize')
+
   def argcombine(self, op, vals, idx):
     """vals/idx: [R, n] -> (val[n], idx[n]) best-of-R with first-index ties."""
     import torch

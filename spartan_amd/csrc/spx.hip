@@ -273,22 +273,39 @@ __device__ __forceinline__ bool arg_better(int op, double v, i64 vi, double b, i
   if (v == b) return vi < bi;
   return op == SPX_OP_ARGMIN ? (v < b) : (v > b);
 }
+// integer values compare as int64 (a double compare would merge distinct
+// values above 2^53 and hand the tie to the lower index)
+__device__ __forceinline__ bool arg_better_i(int op, i64 v, i64 vi, i64 b, i64 bi) {
+  if (v == b) return vi < bi;
+  return op == SPX_OP_ARGMIN ? (v < b) : (v > b);
+}
+// fold partial p = (v, vi) into the running best (b, bi); ARG_EMPTY slots
+// never win
+template <typename V>
+__device__ __forceinline__ void arg_fold(int op, V v, i64 vi, V& b, i64& bi) {
+  bool better;
+  if constexpr (std::is_same<V, double>::value) better = arg_better(op, v, vi, b, bi);
+  else better = arg_better_i(op, v, vi, b, bi);
+  if (vi != ARG_EMPTY && (bi == ARG_EMPTY || better)) { b = v; bi = vi; }
+}
 
 __global__ __launch_bounds__(256) void k_finalize(int op, int acc_dt, int out_dt, const void* pv,
                                                   const i64* pi, i64 P, i64 n, void* out,
                                                   void* out_val) {
   i64 stride = (i64)gridDim.x * 256;
   for (i64 i = (i64)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-    if (op == SPX_OP_ARGMIN || op == SPX_OP_ARGMAX) {
+    if ((op == SPX_OP_ARGMIN || op == SPX_OP_ARGMAX) && is_float_dt(acc_dt)) {
       double b = ld_f(pv, acc_dt, i);
       i64 bi = pi[i];
-      for (i64 p = 1; p < P; ++p) {
-        double v = ld_f(pv, acc_dt, p * n + i);
-        i64 vi = pi[p * n + i];
-        if (vi != ARG_EMPTY && (bi == ARG_EMPTY || arg_better(op, v, vi, b, bi))) { b = v; bi = vi; }
-      }
+      for (i64 p = 1; p < P; ++p) arg_fold(op, ld_f(pv, acc_dt, p * n + i), pi[p * n + i], b, bi);
       ((i64*)out)[i] = bi;
       if (out_val) st_f(out_val, acc_dt, i, b);
+    } else if (op == SPX_OP_ARGMIN || op == SPX_OP_ARGMAX) {
+      i64 b = ld_i(pv, acc_dt, i);
+      i64 bi = pi[i];
+      for (i64 p = 1; p < P; ++p) arg_fold(op, ld_i(pv, acc_dt, p * n + i), pi[p * n + i], b, bi);
+      ((i64*)out)[i] = bi;
+      if (out_val) st_i(out_val, acc_dt, i, b);
     } else if (is_float_dt(acc_dt)) {
       double acc = ld_f(pv, acc_dt, i);
       if (acc_dt == SPX_F32) {  // keep fp32 rounding of each step for fp32 accumulators
@@ -320,18 +337,20 @@ __global__ __launch_bounds__(256) void k_finalize_wide(int op, int acc_dt, int o
                                                        void* out_val) {
   __shared__ double sv[256];
   __shared__ i64 si[256];
+  __shared__ i64 sw[256];  // integer arg values (compared as int64)
   const int t = threadIdx.x;
   const bool arg = op == SPX_OP_ARGMIN || op == SPX_OP_ARGMAX;
   const bool fl = is_float_dt(acc_dt);
   for (i64 i = blockIdx.x; i < n; i += gridDim.x) {
     double b = 0.0;
+    i64 bw = 0;
     i64 bi = ARG_EMPTY;
     bool have = false;
     for (i64 p = t; p < P; p += 256) {
-      if (arg) {
-        double v = ld_f(pv, acc_dt, p * n + i);
-        i64 vi = pi[p * n + i];
-        if (vi != ARG_EMPTY && (bi == ARG_EMPTY || arg_better(op, v, vi, b, bi))) { b = v; bi = vi; }
+      if (arg && fl) {
+        arg_fold(op, ld_f(pv, acc_dt, p * n + i), pi[p * n + i], b, bi);
+      } else if (arg) {
+        arg_fold(op, ld_i(pv, acc_dt, p * n + i), pi[p * n + i], bw, bi);
       } else if (fl) {
         double v = ld_f(pv, acc_dt, p * n + i);
         b = have ? comb_f(op, b, v) : v;
@@ -343,17 +362,25 @@ __global__ __launch_bounds__(256) void k_finalize_wide(int op, int acc_dt, int o
     }
     sv[t] = b;
     si[t] = bi;
+    sw[t] = bw;
     __syncthreads();
     // lanes with no partial (P < 256) hold have=false: they are skipped by
     // letting the tree only combine slots < min(P, 256)
     const int m = P < 256 ? (int)P : 256;
     for (int h = 128; h > 0; h >>= 1) {
       if (t < h && t + h < m) {
-        if (arg) {
-          if (si[t + h] != ARG_EMPTY && (si[t] == ARG_EMPTY || arg_better(op, sv[t + h], si[t + h], sv[t], si[t]))) {
-            sv[t] = sv[t + h];
-            si[t] = si[t + h];
-          }
+        if (arg && fl) {
+          double vb = sv[t];
+          i64 ib = si[t];
+          arg_fold(op, sv[t + h], si[t + h], vb, ib);
+          sv[t] = vb;
+          si[t] = ib;
+        } else if (arg) {
+          i64 vb = sw[t];
+          i64 ib = si[t];
+          arg_fold(op, sw[t + h], si[t + h], vb, ib);
+          sw[t] = vb;
+          si[t] = ib;
         } else if (fl) {
           sv[t] = comb_f(op, sv[t], sv[t + h]);
         } else {
@@ -365,7 +392,10 @@ __global__ __launch_bounds__(256) void k_finalize_wide(int op, int acc_dt, int o
     if (t == 0) {
       if (arg) {
         ((i64*)out)[i] = si[0];
-        if (out_val) st_f(out_val, acc_dt, i, sv[0]);
+        if (out_val) {
+          if (fl) st_f(out_val, acc_dt, i, sv[0]);
+          else st_i(out_val, acc_dt, i, sw[0]);
+        }
       } else if (fl) {
         if (is_float_dt(out_dt)) st_f(out, out_dt, i, sv[0]);
         else st_i(out, out_dt, i, (i64)sv[0]);
@@ -542,15 +572,19 @@ __global__ __launch_bounds__(256) void k_argcombine(int op, int dt, const void* 
                                                     i64 R, i64 n, void* out_val, i64* out_idx) {
   i64 stride = (i64)gridDim.x * 256;
   for (i64 i = (i64)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-    double b = ld_f(vals, dt, i);
-    i64 bi = idx[i];
-    for (i64 r = 1; r < R; ++r) {
-      double v = ld_f(vals, dt, r * n + i);
-      i64 vi = idx[r * n + i];
-      if (vi != ARG_EMPTY && (bi == ARG_EMPTY || arg_better(op, v, vi, b, bi))) { b = v; bi = vi; }
+    if (is_float_dt(dt)) {
+      double b = ld_f(vals, dt, i);
+      i64 bi = idx[i];
+      for (i64 r = 1; r < R; ++r) arg_fold(op, ld_f(vals, dt, r * n + i), idx[r * n + i], b, bi);
+      out_idx[i] = bi;
+      if (out_val) st_f(out_val, dt, i, b);
+    } else {
+      i64 b = ld_i(vals, dt, i);
+      i64 bi = idx[i];
+      for (i64 r = 1; r < R; ++r) arg_fold(op, ld_i(vals, dt, r * n + i), idx[r * n + i], b, bi);
+      out_idx[i] = bi;
+      if (out_val) st_i(out_val, dt, i, b);
     }
-    out_idx[i] = bi;
-    if (out_val) st_f(out_val, dt, i, b);
   }
 }
 

@@ -264,7 +264,9 @@ def _scatter_full(output, full, op):
       t.written = [d]
       return
   if ctx.distributed:
-    if _rank_slabs(output, ctx) and ctx.dist_backend == 'nccl':
+    if _rank_slabs(output, ctx):
+      from .engine import COMBINE_CALLS
+      COMBINE_CALLS['reduce_scatter'] += 1
       (d, t), = output.local.items()
       comm.reduce_scatter_rows(t.data, full.contiguous(), op)
       t.written = [d]

@@ -256,7 +256,8 @@ def run_reduce(children, child_to_var, local_op, axis, dtype, accumulate_fn, til
     partials[ex] = (dst, be.reduce(root, opname, inputs, ex.shape if nd else (), ax,
                                    dst.shape if dst.ndim else (), out_dtype, geom))
   output = distarray.create(out_shape, out_dtype, reducer=accumulate_fn, tile_hint=tile_hint)
-  combine_partials(output, partials, tiles, ax, opname)
+  combine_partials(output, partials, tiles, ax, opname,
+                   value_dtype=codegen.acc_dtype(opname, root.dtype) if arg else None)
   return output
 
 
@@ -272,9 +273,16 @@ def _identity(op, dt):
   return float(info.max) if op == 'min' else float(info.min)
 
 
-def combine_partials(output, partials, tiles, ax, opname):
+# How many times each cross-rank combine ran (tests assert the branch taken).
+COMBINE_CALLS = {'reduce_scatter': 0, 'all_reduce': 0, 'gather_combine': 0, 'arg_gather': 0}
+
+
+def combine_partials(output, partials, tiles, ax, opname, value_dtype=None):
   """Merge tile partials into ``output`` (reference: _reduce_mapper ->
-  output.update(dst, partial) -> tile.merge with accumulate_fn)."""
+  output.update(dst, partial) -> tile.merge with accumulate_fn).
+
+  ``value_dtype``: for argmin/argmax, the dtype of the partial values (the
+  same on every rank, also on ranks without a local partial)."""
   import torch
   ctx = runtime.get()
   be = backend.get()
@@ -304,18 +312,21 @@ def combine_partials(output, partials, tiles, ax, opname):
     return
   shape = output.shape
   if arg:
-    vdt = None
+    # values keep their own dtype end to end: int64 compares as int64 (a
+    # float64 detour would merge distinct values above 2^53)
+    vdt = backend.torch_dtype(value_dtype) if value_dtype is not None else None
     for _, (d, (pv, pi)) in partials.items():
       vdt = pv.dtype
-    if vdt is None:  # this rank has no partial: value dtype from any rank (bool->int64 etc.)
-      vdt = backend.torch_dtype(np.dtype(np.float64))
+    if vdt is None:
+      raise ValueError('combine_partials: value dtype of the arg-reduction unknown on this rank')
     full_v = torch.zeros(shape, dtype=vdt, device=ctx.device)
     full_i = torch.empty(shape, dtype=torch.int64, device=ctx.device)
     be.fill(full_i, backend.FILL_CONST, 9.3e18, 0.0, 0, (0,) * len(shape), shape)
     for ex, (d, (pv, pi)) in partials.items():
       _arg_merge_region(be, full_v, full_i, d, pv, pi, opname)
     if ctx.distributed:
-      vs = comm.all_gather_stack(full_v.reshape(-1).to(torch.float64))
+      COMBINE_CALLS['arg_gather'] += 1
+      vs = comm.all_gather_stack(full_v.reshape(-1))
       is_ = comm.all_gather_stack(full_i.reshape(-1))
       _, best_i = be.argcombine(opname, vs, is_)
       full_i = best_i.reshape(shape)
@@ -327,12 +338,25 @@ def combine_partials(output, partials, tiles, ax, opname):
   for ex, (d, part) in partials.items():
     be.merge(full, None, d.ul, part.reshape(d.shape if d.ndim else ()), opname, fastpath=False)
   if ctx.distributed:
-    if _rank_slabs(output, ctx) and ctx.dist_backend == 'nccl':
+    if opname != 'sum':
+      # min / max across ranks: gather every rank's partial and fold them in
+      # rank order with the local kernels' NaN rule (np.minimum / np.maximum
+      # propagate NaN; the collective library's MIN / MAX need not)
+      COMBINE_CALLS['gather_combine'] += 1
+      stack = comm.all_gather_stack(full.reshape(-1))
+      n = full.numel()
+      folded = torch.empty((n,), dtype=full.dtype, device=full.device)
+      be.finalize(opname, stack.reshape(-1), ctx.world_size, n, folded)
+      full = folded.reshape(shape)
+    elif _rank_slabs(output, ctx):
+      COMBINE_CALLS['reduce_scatter'] += 1
       (d, t), = output.local.items()
       comm.reduce_scatter_rows(t.data, full, opname)
       t.written = [d]
       return
-    comm.all_reduce(full, opname)
+    else:
+      COMBINE_CALLS['all_reduce'] += 1
+      comm.all_reduce(full, opname)
   for d, t in output.local.items():
     _copy_out(be, t, full, d)
 

@@ -23,6 +23,20 @@ def _free_port():
   return p
 
 
+def _big_int_cases():
+  """int64 arrays around 2^60 whose arg winner is within 1 of other values
+  held in other row blocks (a float64 compare would call them equal)."""
+  base = 2 ** 60
+  a = np.full((40, 30), base, dtype=np.int64)
+  a[35, 7] = base + 1   # argmax in the last row block
+  a[33, 20] = base - 1  # argmin in the last row block
+  b = np.full((40, 30), base, dtype=np.int64)
+  b[:, :] -= np.arange(40, dtype=np.int64).reshape(40, 1) % 3  # ties across blocks
+  b[38, 0] = base + 2
+  b[39, 29] = base - 5
+  return [a, b]
+
+
 def _body(rank, world, port, W, q):
   try:
     sys.path.insert(0, os.path.dirname(HERE))
@@ -53,6 +67,33 @@ def _body(rank, world, port, W, q):
       np.testing.assert_array_equal(X.argmin(axis).glom(), nx.argmin(axis))
       np.testing.assert_array_equal(X.argmax(axis).glom(), nx.argmax(axis))
       np.testing.assert_array_equal(expr.min(X, axis).glom(), nx.min(axis))
+
+    # int64 arg-reductions above 2^53: values a float64 combine would merge
+    # sit in different tiles / ranks; the winner must keep its own index
+    from spartan_amd.expr import engine as E
+    for big in _big_int_cases():
+      B = expr.from_numpy(big)
+      for axis in (None, 0, 1):
+        np.testing.assert_array_equal(B.argmax(axis).glom(), big.argmax(axis), err_msg=str(axis))
+        np.testing.assert_array_equal(B.argmin(axis).glom(), big.argmin(axis), err_msg=str(axis))
+        np.testing.assert_array_equal(expr.max(B, axis).glom(), big.max(axis))
+    assert E.COMBINE_CALLS['arg_gather'] > 0
+    # NaN in one rank's rows: min / max across ranks keep numpy's NaN
+    nf = np.arange(1200.0).reshape(40, 30)
+    nf[37, 4] = np.nan
+    nf[2, 9] = np.nan
+    F_ = expr.from_numpy(nf)
+    n_gc = E.COMBINE_CALLS['gather_combine']
+    for axis in (None, 0):
+      np.testing.assert_array_equal(expr.min(F_, axis).glom(), nf.min(axis))
+      np.testing.assert_array_equal(expr.max(F_, axis).glom(), nf.max(axis))
+    assert E.COMBINE_CALLS['gather_combine'] == n_gc + 4
+    # axis-0 sum onto one row slab per rank: the reduce-scatter branch runs
+    n_rs = E.COMBINE_CALLS['reduce_scatter']
+    if W == world:
+      fx = expr.from_numpy(np.arange(40 * 32.0).reshape(40, 32))
+      np.testing.assert_array_equal(fx.sum(0).glom(), np.arange(40 * 32.0).reshape(40, 32).sum(0))
+      assert E.COMBINE_CALLS['reduce_scatter'] == n_rs + 1
 
     # forced DistArrays as direct operands of dot / map (tiles on both ranks)
     xf = expr.arange((40, 30)).force()

@@ -65,6 +65,40 @@ def _run_write_cases(expr, tmpdir):
     np.testing.assert_array_equal(got[10:20, 10:20], b[0:10, 5:15])
     np.testing.assert_array_equal(got[20:30, 5:20], b[10:20])
 
+  # a longer sequence: irregular overlap (device mask built), then a disjoint
+  # and an irregular write again -- the mask must still know every element
+  # written since it was built (tile.pyx:284 sets mask[subslice] on every merge)
+  # Model: per tile, a write covering the whole tile reduces everywhere iff
+  # the tile's first element was written, else replaces (tile.pyx:264-269);
+  # a partial write replaces unwritten and reduces written elements.
+  # ``defined`` tracks elements whose value does not depend on uninitialised
+  # memory (a reduce into a never-written element stays undefined).
+  for fn in (np.add, np.maximum):
+    t = expr.ndarray((12,), dtype=np.float64, reduce_fn=fn).force()
+    tiles = sorted((ex.ul[0], ex.lr[0]) for ex in t.tiles)
+    want = np.zeros(12)
+    seen = np.zeros(12, bool)
+    defined = np.zeros(12, bool)
+    for k, (lo, hi) in enumerate([(0, 4), (2, 6), (7, 9), (5, 9), (0, 12), (10, 12), (4, 11)]):
+      piece = np.arange(lo, hi, dtype=np.float64) * (k + 2) + 0.5
+      expr.write(t, (slice(lo, hi),), piece, ()).force()
+      full = np.zeros(12)
+      full[lo:hi] = piece
+      for tu, tl in tiles:
+        a, b = max(lo, tu), min(hi, tl)
+        if a >= b:
+          continue
+        idx = np.arange(a, b)
+        if (a, b) == (tu, tl):
+          red = np.full(b - a, seen[tu])
+        else:
+          red = seen[a:b].copy()
+        want[idx[~red]] = full[idx[~red]]
+        defined[idx[~red]] = True
+        want[idx[red]] = fn(want[idx[red]], full[idx[red]])
+        seen[a:b] = True
+      np.testing.assert_array_equal(t.glom()[defined], want[defined], err_msg='%s write %d' % (fn.__name__, k))
+
   # write from a transposed view, and a write whose source is the target itself
   src = np.arange(40 * 30, dtype=np.float64).reshape(40, 30)
   t = expr.zeros((30, 40)).force()
