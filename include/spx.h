@@ -201,6 +201,41 @@ int spx_mincost_tiling(int32_t t, int64_t n_edges, const int32_t* eu, const int3
                        int64_t n_split, const int32_t* su, const int32_t* sv, uint8_t* chosen,
                        int64_t* total_cost);
 
+/* ----------------------------------------------------------- collectives
+ * RCCL over xGMI, one communicator per process (one process per GPU).  The
+ * reference has no collectives: every exchange below replaces a pattern of
+ * pickled ZeroMQ point-to-point messages merged at an owner tile --
+ *   partials of an axis reduction sent to the output tiles' owners and merged
+ *     with np.add / np.minimum / np.maximum (reduce.py:53-67 ->
+ *     distarray.py:384-421 -> tile.pyx:201-298): spx_reduce_scatter (row-slab
+ *     outputs), spx_allreduce (others);
+ *   dot partials reduced to the target tile's owner (map.py:326-328 with
+ *     target reducer np.add, dot.py:268-283): spx_reduce / spx_reduce_scatter;
+ *   argmin / argmax (value, index) partials gathered for the device combine
+ *     (builtins.py:610-666): spx_allgather;
+ *   a replicated small operand (the NumPy array2 pickled into every
+ *     RunKernelReq, dot.py:249-257; k-means centres, k_means_.py:150-151):
+ *     spx_broadcast;
+ *   DistArray.fetch / update of remote regions (distarray.py:290-421 over
+ *     blob_ctx.get / update): spx_sendrecv (one grouped point-to-point batch).
+ * RCCL is opened at run time: spx_comm_load(path) dlopens it (NULL path:
+ * "librccl.so.1"); the compute entry points never need it.  Counts are in
+ * elements of dtype; ops are SPX_OP_SUM / MIN / MAX; all calls are enqueued
+ * on `stream` (in-place send == recv allowed as in RCCL). */
+int spx_comm_load(const char* rccl_path);
+int spx_comm_unique_id(uint8_t* out, int64_t nbytes);          /* nbytes >= 128 */
+int spx_comm_init(const uint8_t* unique_id, int64_t nbytes, int rank, int world, void** comm_out);
+int spx_comm_destroy(void* comm);
+int spx_allreduce(void* comm, const void* send, void* recv, int64_t count, int dtype, int op, void* stream);
+int spx_reduce_scatter(void* comm, const void* send, void* recv, int64_t recvcount, int dtype, int op,
+                       void* stream);
+int spx_allgather(void* comm, const void* send, void* recv, int64_t sendcount, int dtype, void* stream);
+int spx_broadcast(void* comm, const void* send, void* recv, int64_t count, int dtype, int root, void* stream);
+int spx_reduce(void* comm, const void* send, void* recv, int64_t count, int dtype, int op, int root, void* stream);
+/* grouped point-to-point: nsend byte buffers to speers[i], nrecv from rpeers[i] */
+int spx_sendrecv(void* comm, int nsend, const void* const* sbufs, const int64_t* sbytes, const int* speers,
+                 int nrecv, void* const* rbufs, const int64_t* rbytes, const int* rpeers, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,4 +1,4 @@
-"""Zero-copy views over a DistArray: Slice and Transpose.
+"""Zero-copy views over a DistArray: Slice, Transpose and UnitDims.
 
 Restate spartan/expr/slice.py:41-84 (``Slice``) and
 spartan/expr/transpose.py:25-65 (``Transpose``): a view reports tiles in its
@@ -103,6 +103,72 @@ class Transpose(DistArray):
     return np.ascontiguousarray(np.transpose(self.base.glom()))
 
 
+class UnitDims(DistArray):
+  """``base`` with length-1 dimensions dropped and / or inserted, without a
+  copy: the reference's ReshapeExpr after an int / newaxis index
+  (base.py:388-430).  Non-unit dims keep their order; every region maps to
+  the base region with the unit dims set to [0, 1), and a fetched piece is a
+  reshaped (still strided) view of the base piece."""
+
+  def __init__(self, base, shape):
+    shape = tuple(int(s) for s in shape)
+    nb = [i for i, s in enumerate(base.shape) if s != 1]
+    nn = [j for j, s in enumerate(shape) if s != 1]
+    if [base.shape[i] for i in nb] != [shape[j] for j in nn]:
+      raise ValueError('UnitDims: %s -> %s changes a non-unit dimension' % (base.shape, shape))
+    self.base = base
+    self.shape = shape
+    self.dtype = base.dtype
+    self.bad_tiles = []
+    self._b2n = dict(zip(nb, nn))   # base dim -> view dim (non-unit dims)
+    self._n2b = dict(zip(nn, nb))
+    self.tiles = {self.from_base(ex): w for ex, w in base.tiles.items()}
+
+  def from_base(self, region):
+    ul = [0] * len(self.shape)
+    lr = [1] * len(self.shape)
+    for i, j in self._b2n.items():
+      ul[j], lr[j] = region.ul[i], region.lr[i]
+    return ext.create(tuple(ul), tuple(lr), self.shape)
+
+  def to_base(self, region):
+    ul = [0] * len(self.base.shape)
+    lr = [1] * len(self.base.shape)
+    for j, i in self._n2b.items():
+      ul[i], lr[i] = region.ul[j], region.lr[j]
+    return ext.create(tuple(ul), tuple(lr), self.base.shape)
+
+  def tile_shape(self):
+    counts = {}
+    for ex in self.tiles:
+      counts[ex.shape] = counts.get(ex.shape, 0) + 1
+    return sorted(counts.items(), key=lambda kv: (kv[1], kv[0]))[-1][0]
+
+  def _v(self, t, region):
+    return t.reshape(tuple(region.shape) if region.ndim else ())
+
+  def fetch(self, region):
+    return self._v(self.base.fetch(self.to_base(region)), region)
+
+  def owner_of_region(self, region):
+    return self.base.owner_of_region(self.to_base(region))
+
+  def gather(self, requests):
+    got = gather_regions(self.base, [(self.to_base(r), d) for r, d in requests])
+    return {k: self._v(v, requests[k][0]) for k, v in got.items()}
+
+  def glom(self):
+    return np.asarray(self.base.glom()).reshape(self.shape)
+
+
+def unit_dims_of(array, shape):
+  if tuple(shape) == tuple(array.shape):
+    return array
+  if isinstance(array, UnitDims):
+    array = array.base
+  return UnitDims(array, shape)
+
+
 def slice_of(array, idx):
   return Slice(array, idx)
 
@@ -114,5 +180,5 @@ def transpose_of(array):
 
 
 def is_view(array):
-  return isinstance(array, (Slice, Transpose))
+  return isinstance(array, (Slice, Transpose, UnitDims))
 

@@ -98,6 +98,24 @@ _SIGS = {
                    ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p], ctypes.c_int),
     'spx_bincount': ([ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int,
                       ctypes.c_void_p], ctypes.c_int),
+    'spx_comm_load': ([ctypes.c_char_p], ctypes.c_int),
+    'spx_comm_unique_id': ([ctypes.c_void_p, ctypes.c_int64], ctypes.c_int),
+    'spx_comm_init': ([ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)],
+                      ctypes.c_int),
+    'spx_comm_destroy': ([ctypes.c_void_p], ctypes.c_int),
+    'spx_allreduce': ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                       ctypes.c_void_p], ctypes.c_int),
+    'spx_reduce_scatter': ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                            ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
+    'spx_allgather': ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                       ctypes.c_void_p], ctypes.c_int),
+    'spx_broadcast': ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                       ctypes.c_void_p], ctypes.c_int),
+    'spx_reduce': ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                    ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
+    'spx_sendrecv': ([ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), _I64P,
+                      ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), _I64P,
+                      ctypes.POINTER(ctypes.c_int), ctypes.c_void_p], ctypes.c_int),
     'spx_mincost_tiling': ([ctypes.c_int32, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
                             ctypes.POINTER(ctypes.c_int32), _I64P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
                             ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_uint8), _I64P], ctypes.c_int),

@@ -1,19 +1,30 @@
-"""Cross-rank data movement for tiles (torch.distributed: RCCL on GPU, gloo in tests).
+"""Cross-rank data movement for tiles.
 
-With ``SPARTAN_DIST_BACKEND=gloo`` on GPUs (rehearsing N ranks on one
-device, e.g. the 1-GPU box) device tensors are staged through host memory,
-since gloo moves host buffers only; the RCCL path never stages.
+Data plane, by ``ctx.dist_backend``:
+
+* ``'rccl'`` (the GPU default at N > 1): every collective is a libspx.so
+  C-ABI call (``spx_allreduce`` / ``spx_reduce_scatter`` / ``spx_allgather``
+  / ``spx_broadcast`` / ``spx_reduce`` / ``spx_sendrecv``, include/spx.h) on
+  the RCCL communicator the runtime created, enqueued on the current HIP
+  stream.  torch.distributed (gloo) is the host control plane only: the
+  unique-id hand-off, ``barrier`` and ``max_over_ranks`` of host floats.
+* ``'gloo'``: CPU tests, and the one-GPU multi-rank rehearsal
+  (``SPARTAN_DIST_BACKEND=gloo``), where device tensors are staged through
+  host memory.
+* ``'nccl'``: torch.distributed's own RCCL process group
+  (``SPARTAN_COMM=torch``, a debugging switch).
 
 Replaces the reference's pickled ZeroMQ point-to-point messages
-(spartan/rpc/common.py:52-62, spartan/blob_ctx.py:127-179): every exchange here
-is a collective that all ranks enter with identical arguments, because every
-rank computes the same tile plan (SPMD).
+(spartan/rpc/common.py:52-62, spartan/blob_ctx.py:127-179): every exchange
+here is a collective that all ranks enter with identical arguments, because
+every rank computes the same tile plan (SPMD).
 """
-import numpy as np
+import ctypes
 
 from . import runtime
 
 _OPS = {'sum': 'SUM', 'min': 'MIN', 'max': 'MAX'}
+_SPX_OP = {'sum': 0, 'min': 1, 'max': 2}
 
 
 def _dist():
@@ -25,9 +36,78 @@ def _staged(ctx, t):
   return ctx.dist_backend == 'gloo' and t.device.type != 'cpu'
 
 
+# ------------------------------------------------------- libspx RCCL plane
+def _lib():
+  from . import backend
+  return backend.load_library()
+
+
+def _check(rc, what):
+  if rc != 0:
+    raise RuntimeError('%s failed (%d): %s' % (what, rc, _lib().spx_last_error().decode()))
+
+
+def _dt(t):
+  from . import backend
+  return backend.spx_dtype(backend.np_dtype(t.dtype))
+
+
+def _stream():
+  import torch
+  return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t):
+  return ctypes.c_void_p(t.data_ptr())
+
+
+def rccl_path():
+  """The RCCL PyTorch-ROCm itself loaded (one RCCL, one HIP runtime per
+  process); /opt/rocm's librccl.so.1 otherwise."""
+  import os
+  import torch
+  p = os.path.join(os.path.dirname(torch.__file__), 'lib', 'librccl.so')
+  return p if os.path.exists(p) else 'librccl.so.1'
+
+
+def rccl_init(rank, world, unique_id=None):
+  """Create this rank's RCCL communicator through libspx.so.  ``unique_id``:
+  the 128 bytes rank 0 made (``rccl_unique_id``); returns the handle."""
+  lib = _lib()
+  _check(lib.spx_comm_load(rccl_path().encode()), 'spx_comm_load')
+  buf = (ctypes.c_uint8 * 128).from_buffer_copy(bytes(unique_id))
+  comm = ctypes.c_void_p()
+  _check(lib.spx_comm_init(buf, 128, int(rank), int(world), ctypes.byref(comm)), 'spx_comm_init')
+  return comm
+
+
+def rccl_unique_id():
+  lib = _lib()
+  _check(lib.spx_comm_load(rccl_path().encode()), 'spx_comm_load')
+  buf = (ctypes.c_uint8 * 128)()
+  _check(lib.spx_comm_unique_id(buf, 128), 'spx_comm_unique_id')
+  return bytes(buf)
+
+
+def rccl_destroy(comm):
+  if comm is not None and comm.value:
+    _check(_lib().spx_comm_destroy(comm), 'spx_comm_destroy')
+
+
+def _contig(t, what):
+  if not t.is_contiguous():
+    raise ValueError('%s needs a contiguous tensor' % what)
+
+
+# ------------------------------------------------------------- collectives
 def all_reduce(t, op):
   ctx = runtime.get()
   if not ctx.distributed:
+    return t
+  if ctx.dist_backend == 'rccl':
+    _contig(t, 'all_reduce')
+    _check(_lib().spx_allreduce(ctx.rccl, _p(t), _p(t), t.numel(), _dt(t), _SPX_OP[op], _stream()),
+           'spx_allreduce')
     return t
   dist = _dist()
   if _staged(ctx, t):
@@ -42,6 +122,13 @@ def all_reduce(t, op):
 def reduce_scatter_rows(out, full, op):
   """out = rank-th equal row slab of the element-wise reduction of ``full``."""
   ctx = runtime.get()
+  if ctx.dist_backend == 'rccl':
+    _contig(out, 'reduce_scatter')
+    _contig(full, 'reduce_scatter')
+    assert full.numel() == out.numel() * ctx.world_size
+    _check(_lib().spx_reduce_scatter(ctx.rccl, _p(full), _p(out), out.numel(), _dt(out), _SPX_OP[op],
+                                     _stream()), 'spx_reduce_scatter')
+    return out
   dist = _dist()
   if ctx.dist_backend == 'gloo':  # gloo has no reduce_scatter: all_reduce + slice
     all_reduce(full, op)
@@ -58,8 +145,12 @@ def all_gather_stack(t):
   ctx = runtime.get()
   if not ctx.distributed:
     return t.unsqueeze(0)
-  dist = _dist()
   out = torch.empty((ctx.world_size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+  if ctx.dist_backend == 'rccl':
+    t = t.contiguous()
+    _check(_lib().spx_allgather(ctx.rccl, _p(t), _p(out), t.numel(), _dt(t), _stream()), 'spx_allgather')
+    return out
+  dist = _dist()
   if _staged(ctx, t):
     h = torch.empty(out.shape, dtype=t.dtype)
     dist.all_gather(list(h.unbind(0)), t.contiguous().cpu())
@@ -75,6 +166,11 @@ def broadcast(t, src_rank):
   ctx = runtime.get()
   if not ctx.distributed:
     return t
+  if ctx.dist_backend == 'rccl':
+    _contig(t, 'broadcast')
+    _check(_lib().spx_broadcast(ctx.rccl, _p(t), _p(t), t.numel(), _dt(t), int(src_rank), _stream()),
+           'spx_broadcast')
+    return t
   if _staged(ctx, t):
     h = t.cpu()
     _dist().broadcast(h, src=src_rank)
@@ -84,12 +180,39 @@ def broadcast(t, src_rank):
   return t
 
 
+class _Pending:
+  """An RCCL reduce running on the side stream; ``wait`` makes the current
+  stream wait for it (no host synchronisation)."""
+
+  def __init__(self, event, keep):
+    self.event = event
+    self.keep = keep  # the tensor stays alive until the wait
+
+  def wait(self):
+    import torch
+    torch.cuda.current_stream().wait_event(self.event)
+    self.keep = None
+
+
 def reduce_async(t, dst_rank, op):
   """Start reducing ``t`` (contiguous, same shape on every rank) into
-  ``t`` on ``dst_rank``; returns a handle for ``wait_all``.  On RCCL the
-  reduction runs on the process group's stream, after the work already
-  queued on the current stream and concurrently with what follows it."""
+  ``t`` on ``dst_rank``; returns a handle for ``wait_all``.  The reduction
+  runs on a side stream, after the work already queued on the current
+  stream and concurrently with what follows it."""
   ctx = runtime.get()
+  if ctx.dist_backend == 'rccl':
+    import torch
+    _contig(t, 'reduce')
+    cur = torch.cuda.current_stream()
+    side = ctx.comm_stream()
+    ready = torch.cuda.Event()
+    ready.record(cur)
+    side.wait_event(ready)
+    _check(_lib().spx_reduce(ctx.rccl, _p(t), _p(t), t.numel(), _dt(t), _SPX_OP[op], int(dst_rank),
+                             ctypes.c_void_p(side.cuda_stream)), 'spx_reduce')
+    done = torch.cuda.Event()
+    done.record(side)
+    return _Pending(done, t)
   dist = _dist()
   if _staged(ctx, t):  # rehearsal: synchronous through the host
     h = t.cpu()
@@ -106,11 +229,6 @@ def wait_all(handles):
       h.wait()
 
 
-def all_to_all_single(out, inp, out_splits, in_splits):
-  _dist().all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits)
-  return out
-
-
 def exchange(sends, recvs):
   """Point-to-point batch.  sends: [(tensor, dst_rank)], recvs: [(tensor, src_rank)].
 
@@ -120,6 +238,20 @@ def exchange(sends, recvs):
   if not ctx.distributed or (not sends and not recvs):
     return
   import torch
+  if ctx.dist_backend == 'rccl':
+    sends = [(t.contiguous(), peer) for t, peer in sends]
+    for t, _ in recvs:
+      _contig(t, 'exchange recv')
+    ns, nr = len(sends), len(recvs)
+    VP, I64, I32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+    sb = (VP * max(ns, 1))(*[t.data_ptr() for t, _ in sends])
+    sn = (I64 * max(ns, 1))(*[t.numel() * t.element_size() for t, _ in sends])
+    sp = (I32 * max(ns, 1))(*[int(p) for _, p in sends])
+    rb = (VP * max(nr, 1))(*[t.data_ptr() for t, _ in recvs])
+    rn = (I64 * max(nr, 1))(*[t.numel() * t.element_size() for t, _ in recvs])
+    rp = (I32 * max(nr, 1))(*[int(p) for _, p in recvs])
+    _check(_lib().spx_sendrecv(ctx.rccl, ns, sb, sn, sp, nr, rb, rn, rp, _stream()), 'spx_sendrecv')
+    return
   dist = _dist()
   post = []
   if ctx.dist_backend == 'gloo':  # host staging for device tensors (rehearsal mode)
@@ -142,17 +274,20 @@ def exchange(sends, recvs):
 
 
 def barrier():
+  """Host barrier over the control plane (callers synchronise their device
+  streams around it)."""
   ctx = runtime.get()
   if ctx.distributed:
     _dist().barrier()
 
 
 def max_over_ranks(x):
-  """Max of a host float over all ranks (bench timing)."""
+  """Max of a host float over all ranks (bench timing), on the control plane."""
   import torch
   ctx = runtime.get()
   if not ctx.distributed:
     return x
-  t = torch.tensor([float(x)], dtype=torch.float64, device=ctx.device)
-  all_reduce(t, 'max')
+  dev = ctx.device if ctx.dist_backend == 'nccl' else torch.device('cpu')
+  t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+  _dist().all_reduce(t, op=_dist().ReduceOp.MAX)
   return float(t.item())

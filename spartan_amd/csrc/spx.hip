@@ -11,6 +11,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <type_traits>
@@ -50,6 +51,11 @@ static int set_err(int code, const char* fmt, ...) {
 
 extern "C" int spx_abi_version(void) { return SPX_ABI_VERSION; }
 extern "C" const char* spx_last_error(void) { return g_err.c_str(); }
+// error text from the host-only translation units (comm.cpp)
+extern "C" int spx_comm_set_error(const char* msg) {
+  g_err = msg ? msg : "";
+  return 0;
+}
 
 static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
@@ -1156,7 +1162,12 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
                                                                     i64* __restrict__ labels,
                                                                     unsigned int* __restrict__ counters,
                                                                     i64* __restrict__ full_list,
-                                                                    KfCand* __restrict__ cand_list) {
+                                                                    KfCand* __restrict__ cand_list,
+                                                                    const i64* __restrict__ rows_in,
+                                                                    const unsigned int* __restrict__ nrows_in) {
+  // rows_in != NULL (list mode): only the *nrows_in points rows_in[0..n) --
+  // the rows the A-stationary filter left undecided; slot s of the list plays
+  // the role of row s below
   extern __shared__ __attribute__((aligned(16))) unsigned char kb_lds[];
   constexpr int NC = 32 * NCT;
   const int Dp = (int)D + 8;
@@ -1190,14 +1201,19 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
   // adds (fresh accumulators), or all 48 KS products in one MFMA chain
   const double chain = KB_FRESH ? 48.0 * KB_GRP + (double)(KS / KB_GRP) : 48.0 * (double)KS;
   const double eS = (u32 + 3.1 * 3.814697265625e-06 + 2.0 * (chain + 3.0) * u32) * 1.01 * cmax;
-  const i64 ntiles = (N + 31) / 32;
+  const i64 nslots = rows_in ? (i64)*nrows_in : N;
+  if (nslots == 0) return;
+  const i64 ntiles = (nslots + 31) / 32;
   const i64 stride = (i64)gridDim.x * KB_WAVES;
   i64 tile = (i64)blockIdx.x * KB_WAVES + w;
+  auto row_of = [&](i64 slot) -> i64 {
+    slot = slot < nslots ? slot : nslots - 1;
+    return rows_in ? rows_in[slot] : slot;
+  };
   // A ring: 4 k-steps in flight, addresses clamped into the array
   kb_f4 ra[4][2];
   auto load = [&](int s, i64 tl, int ks) {
-    i64 row = tl * 32 + r;
-    row = row < N ? row : N - 1;
+    const i64 row = row_of(tl * 32 + r);
     const float* p = P + row * ldp + ks * 16 + 4 * h;
     ra[s][0] = *(const kb_f4*)p;  // dims 4h..4h+3 (nt measured no faster here)
     ra[s][1] = *(const kb_f4*)(p + 8);  // dims 8+4h..8+4h+3
@@ -1330,7 +1346,8 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
     // (C) one decision per row, by the even lane of its pair
     const int q = r >> 1;
     const int rt = (q & 3) + 8 * (q >> 2) + 4 * h;
-    const i64 grow = tile * 32 + rt;
+    const i64 gslot = tile * 32 + rt;
+    const i64 grow = row_of(gslot);
     const float b1 = lo[0], b2 = sec[0];
     const int i1 = 32 * (int)(__builtin_bit_cast(unsigned int, b1) & 7u) + li[0];
     const float p2f = __shfl(p2, rt, 64);
@@ -1342,7 +1359,7 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
     const double e = 2.0 * eS * pn + 2.02 * u32 * (cmax * cmax + pn * cmax) +
                      1e-28 * (double)D * (1.0 + cmax) * (1.0 + cmax) + 1e-8 * (pp2 + cmax * cmax) +
                      8.0 * 1.1920928955078125e-07 * amax + 1e-300;
-    const bool live = grow < N && (r & 1) == 0;
+    const bool live = gslot < nslots && (r & 1) == 0;
     // finite point, no overflow possible in S or a' (every a' then finite)
     const bool fin = isfinite(p2f) && isfinite(e) && pn * cmax < 1e36 && cmax * cmax < 1e36 &&
                      isfinite(b1) && isfinite(b2);
@@ -1388,7 +1405,8 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
 template <int NCT>
 static void kb_launch(hipStream_t s, i64 N, i64 D, const float* P, i64 ldp, const __bf16* CBh, const __bf16* CBl,
                       const float* cnf, const double* cmax, i64* labels, unsigned int* counters, i64* full_list,
-                      KfCand* cand_list, int grid) {
+                      KfCand* cand_list, int grid, const i64* rows_in = nullptr,
+                      const unsigned int* nrows_in = nullptr) {
   const size_t lds = kb_lds_bytes(D, NCT);
   static bool attr = false;
   if (!attr) {
@@ -1397,7 +1415,299 @@ static void kb_launch(hipStream_t s, i64 N, i64 D, const float* P, i64 ldp, cons
     attr = true;
   }
   k_kmeans_filter_b3<NCT><<<grid, KB_WAVES * 64, lds, s>>>(N, D, P, ldp, CBh, CBl, cnf, cmax, labels, counters,
-                                                           full_list, cand_list);
+                                                           full_list, cand_list, rows_in, nrows_in);
+}
+
+// ---------------------------------------------------------------------------
+// A-stationary bf16x3 filter: the fast first pass of the certified
+// assignment (same bf16 split, same rigorous bound e and same decision rule
+// a point is labelled iff b2 - b1 > 2e as k_kmeans_filter_b3 above).
+// k_kmeans_filter_b3 keeps all NCT accumulator tiles (128 registers) live so
+// that it can emit candidate masks, which forces one wave per SIMD (no
+// partner to cover the A loads or the epilogue, which follows all 192
+// MFMAs).  Here a wave instead holds its 32-point tile as the bf16 split for
+// the whole centre sweep (8 KS registers) and sweeps the centre tiles one at
+// a time: 3 KS MFMAs into two accumulator chains of KS / 2 k-steps each
+// (added once: the fresh-accumulator bound with G = KS / 2), then the tile's
+// a' = fl(|c|^2 - 2S), tagged with ct in its 3 low mantissa bits, are folded
+// into a per-lane running top-2 (fma, and-or, med3, min per value), so the
+// epilogue work sits between MFMAs instead of after all of them.  The next
+// point tile's loads are issued right after the split, into the registers
+// the split just freed, and land during the sweep.  ~230 registers: two
+// waves per SIMD, 8 waves per block, one block per CU (the split centres,
+// 137 KiB for K = 256, D = 128, stay resident in LDS).  Undecided rows
+// (near-ties, ~1-3 %) go to a row list; the list-mode run of
+// k_kmeans_filter_b3 gives them candidate masks (k_kmeans_cand then
+// recomputes the candidates in scipy's exact order); non-finite rows go to
+// the all-centre exact kernel as before.
+#ifndef KS_WAVES_CFG
+#define KS_WAVES_CFG 8  // waves per block (one block per CU): 8 = two per SIMD (<= 256 registers), 4 = one (<= 512)
+#endif
+#ifndef KS_CHAINS
+#define KS_CHAINS 2  // accumulator chains per centre tile (2: the fresh-accumulator bound, one add per value)
+#endif
+constexpr int KS_WAVES = KS_WAVES_CFG;
+#ifndef KS_PREFETCH
+#define KS_PREFETCH 0  // 1: next tile's loads in flight during the sweep (+64 registers: spills at 2 waves/SIMD)
+#endif
+// LDS row of centre c: [hi: D bf16][lo: D bf16][48-byte pad]; the row stride
+// is 4 D + 48 bytes = 12 (mod 64) banks, so the 16-lane groups of a
+// ds_read_b128 (rows 0-3, 12-15, 20-27 ...) hit 16 distinct 4-bank quads,
+// and every read of a tile's k-loop is one base register + an immediate.
+__host__ __device__ constexpr int ks_row_bytes(int D) { return 4 * D + 48; }
+static size_t ks_lds_bytes(i64 D, int nct) { return (size_t)32 * nct * ks_row_bytes((int)D) + (size_t)32 * nct * 4; }
+
+// Plain v_min_f32 / v_med3_f32 / v_and_or_b32: fminf / fmed3 on values
+// built by bit operations make the compiler canonicalize every operand first
+// (a v_max_f32 x, x each), which doubled the per-value epilogue here.  The
+// operands are finite or +inf (non-finite points are routed by the |p|^2 /
+// cmax checks before any of these values is used).
+__device__ __forceinline__ float ks_min(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float ks_med3(float a, float b, float c) {
+  float r;
+  asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float ks_tag(float a, unsigned int ct) {  // (bits(a) & ~7) | ct
+  unsigned int r;
+  asm("v_and_or_b32 %0, %1, -8, %2" : "=v"(r) : "v"(__builtin_bit_cast(unsigned int, a)), "v"(ct));
+  return __builtin_bit_cast(float, r);
+}
+
+// Top-2 VALUES across the 32 lanes of each half (register halving as in
+// kb_top2_lanes, without carrying an index: the argmin lane is found
+// afterwards by one ballot per row).  Lane (h, r) ends with register 0 =
+// row rt(r >> 1, h) over all 32 centres of every tile.
+__device__ __forceinline__ void ks_top2_vals(float (&lo)[16], float (&sec)[16], int lane) {
+  auto comb = [](float a, float as, float b, float bs, float& l, float& s2) {
+    s2 = ks_med3(a, b, ks_min(as, bs));
+    l = ks_min(a, b);
+  };
+  auto xor16 = [](float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x401F));
+  };
+  {
+    const bool up = (lane & 16) != 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float kl = up ? lo[k + 8] : lo[k], ks2 = up ? sec[k + 8] : sec[k];
+      const float sl = up ? lo[k] : lo[k + 8], ss = up ? sec[k] : sec[k + 8];
+      comb(kl, ks2, xor16(sl), xor16(ss), lo[k], sec[k]);
+    }
+  }
+  auto dpp_step = [&](auto ctrl, int n, int o) {
+    constexpr int C = decltype(ctrl)::value;
+    const bool up = (lane & o) != 0;
+#pragma unroll
+    for (int k = 0; k < n; ++k) {
+      const float kl = up ? lo[k + n] : lo[k], ks2 = up ? sec[k + n] : sec[k];
+      const float sl = up ? lo[k] : lo[k + n], ss = up ? sec[k] : sec[k + n];
+      const float ol = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sl), C, 0xF, 0xF, false));
+      const float os = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, ss), C, 0xF, 0xF, false));
+      comb(kl, ks2, ol, os, lo[k], sec[k]);
+    }
+  };
+  dpp_step(std::integral_constant<int, 0x140>{}, 4, 8);  // row_mirror: lane ^ 15
+  dpp_step(std::integral_constant<int, 0x141>{}, 2, 4);  // row_half_mirror: lane ^ 7
+  dpp_step(std::integral_constant<int, 0x4E>{}, 1, 2);   // quad_perm [2,3,0,1]: lane ^ 2
+  {
+    const float ol = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, lo[0]), 0xB1, 0xF, 0xF, false));
+    const float os = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sec[0]), 0xB1, 0xF, 0xF, false));
+    comb(lo[0], sec[0], ol, os, lo[0], sec[0]);
+  }
+}
+
+template <int NCT, int KS>
+__global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const float* __restrict__ P, i64 ldp,
+                                                                    const __bf16* __restrict__ CBh,
+                                                                    const __bf16* __restrict__ CBl,
+                                                                    const float* __restrict__ cnf,
+                                                                    const double* cmax_p, i64* __restrict__ labels,
+                                                                    unsigned int* __restrict__ counters,
+                                                                    i64* __restrict__ full_list,
+                                                                    i64* __restrict__ und_list) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char kb_lds[];
+  constexpr int NC = 32 * NCT, D = 16 * KS, RB = ks_row_bytes(D);
+  static_assert(KS % 2 == 0, "two accumulator chains");
+  float* cns = (float*)(kb_lds + NC * RB);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, h = lane >> 5;
+  {
+    // centre rows in the permuted k order of k_kmeans_filter_b3 (dim quads
+    // 1 and 2 of every 16-dim step swapped: an A lane's two 16-byte loads
+    // are adjacent in its row)
+    typedef unsigned int kb_u2 __attribute__((ext_vector_type(2)));
+    constexpr int D4 = D / 4;
+    for (int i = t; i < NC * D4; i += KS_WAVES * 64) {
+      const int c = i / D4, q = i % D4, qi = q & 3;
+      const int pq = (q & ~3) | (qi == 1 ? 2 : qi == 2 ? 1 : qi);
+      unsigned char* row = kb_lds + c * RB;
+      *(kb_u2*)(row + 8 * pq) = *(const kb_u2*)&CBh[(i64)c * D + 4 * q];
+      *(kb_u2*)(row + 2 * D + 8 * pq) = *(const kb_u2*)&CBl[(i64)c * D + 4 * q];
+    }
+    for (int i = t; i < NC; i += KS_WAVES * 64) cns[i] = cnf[i];
+  }
+  __syncthreads();
+  const double cmax = *cmax_p;
+  const double u32 = 5.9604644775390625e-08;
+  // each accumulator chain: 48 products per k-step over KS / 2 k-steps, then
+  // one add of the two chains
+  const double chain = KS_CHAINS == 2 ? 48.0 * (double)(KS / 2) + 1.0 : 48.0 * (double)KS;
+  const double eS = (u32 + 3.1 * 3.814697265625e-06 + 2.0 * (chain + 3.0) * u32) * 1.01 * cmax;
+  const i64 ntiles = (N + 31) / 32;
+  const i64 stride = (i64)gridDim.x * KS_WAVES;
+  i64 tile = (i64)blockIdx.x * KS_WAVES + w;
+  kb_f4 ra[KS][2];
+  auto load = [&](i64 tl) {
+    i64 row = tl * 32 + r;
+    row = row < N ? row : N - 1;
+#ifdef KS_DEV_NOGLOBAL  // timing split only (tools/km_modes.py dev builds); never set in the product build
+    row = r;
+#endif
+    const float* p = P + row * ldp + 4 * h;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      ra[ks][0] = *(const kb_f4*)(p + ks * 16);      // dims 4h..4h+3 of the k-step
+      ra[ks][1] = *(const kb_f4*)(p + ks * 16 + 8);  // dims 8+4h..8+4h+3
+    }
+  };
+#if KS_PREFETCH
+  if (tile < ntiles) load(tile);
+#endif
+  for (; tile < ntiles; tile += stride) {
+#if !KS_PREFETCH
+    load(tile);  // the partner wave's sweep covers the latency
+#endif
+    kb_bf8 ah[KS], al[KS];
+    float p2 = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = j < 4 ? ra[ks][0][j] : ra[ks][1][j - 4];
+        p2 = __builtin_fmaf(x, x, p2);  // |p|^2 only feeds the bound (x 1.001 slack)
+        ah[ks][j] = (__bf16)x;
+        al[ks][j] = (__bf16)(x - (float)ah[ks][j]);
+      }
+    }
+#if KS_PREFETCH
+    // the split above must finish reading ra before the next tile's loads
+    // land in it: without this fence the scheduler hoists the loads above
+    // the split (three tiles' worth of registers live at once -> spills)
+    __builtin_amdgcn_sched_barrier(0);
+    if (tile + stride < ntiles) load(tile + stride);  // lands during the sweep below
+#endif
+    float lo[16], sec[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      lo[q] = INFINITY;
+      sec[q] = INFINITY;
+    }
+    const unsigned char* rowp = kb_lds + r * RB + 16 * h;
+#pragma unroll 1
+    for (int ct = 0; ct < NCT; ++ct) {  // rolled: bounds the scheduler's window (and the LDS reads it hoists)
+      kb_acc c0 = (kb_acc){}, c1 = (kb_acc){};
+      const unsigned char* rp = rowp + ct * 32 * RB;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+#ifdef KS_DEV_NOLDS  // timing split only; never set in the product build
+        kb_bf8 bh = ah[(ks + ct) % KS], bl = al[(ks + 3 * ct) % KS];
+        bh[0] = (__bf16)(float)ct;
+#else
+        const kb_bf8 bh = *(const kb_bf8*)(rp + 32 * ks);
+        const kb_bf8 bl = *(const kb_bf8*)(rp + 2 * D + 32 * ks);
+#endif
+        kb_acc& c = (KS_CHAINS == 2 && ks >= KS / 2) ? c1 : c0;
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bl, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ks], bh, c, 0, 0, 0);
+      }
+      const float cc = cns[ct * 32 + r];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float sq = KS_CHAINS == 2 ? c0[q] + c1[q] : c0[q];
+#ifdef KS_DEV_NOEPI  // timing split only; never set in the product build
+        lo[q] = ks_min(lo[q], sq);
+#else
+        const float v = ks_tag(__builtin_fmaf(-2.f, sq, cc), (unsigned int)ct);
+        sec[q] = ks_med3(v, lo[q], sec[q]);
+        lo[q] = ks_min(lo[q], v);
+#endif
+      }
+    }
+    float lo0[16];  // this lane's minimum per register (its centre r over all tiles)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) lo0[q] = lo[q];
+    ks_top2_vals(lo, sec, lane);
+    // the centre of each row's minimum: lane (h, 2q) holds row rt(q, h)'s
+    // b1; the lowest lane of that half whose own minimum equals it is the
+    // centre r (ties in the tagged value share the tile, so the lowest r is
+    // the lowest centre index, the first occurrence)
+    int rmin = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float b0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lo[0]), 2 * q));
+      const float b1h = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lo[0]), 32 + 2 * q));
+      const unsigned long long m = __ballot(lo0[q] == (h ? b1h : b0));
+      const unsigned int m0 = (unsigned int)m, m1 = (unsigned int)(m >> 32);
+      const int r0 = m0 ? __builtin_ctz(m0) : 0, r1 = m1 ? __builtin_ctz(m1) : 0;
+      if (r == 2 * q) rmin = h ? r1 : r0;
+    }
+    p2 += __shfl_xor(p2, 32, 64);  // row r's |p|^2 in lanes r and r + 32
+    // one decision per row, by the even lane of its pair (as in k_kmeans_filter_b3)
+    const int q = r >> 1;
+    const int rt = (q & 3) + 8 * (q >> 2) + 4 * h;
+    const i64 grow = tile * 32 + rt;
+    const float b1 = lo[0], b2 = sec[0];
+    const int i1 = 32 * (int)(__builtin_bit_cast(unsigned int, b1) & 7u) + rmin;
+    const float p2f = __shfl(p2, rt, 64);
+    const double pp2 = (double)p2f * 1.001 + (double)D * 2e-45;
+    const double pn = sqrt(pp2) * 1.0001;
+    const double amax = cmax * cmax + 2.0 * pn * cmax;
+    const double e = 2.0 * eS * pn + 2.02 * u32 * (cmax * cmax + pn * cmax) +
+                     1e-28 * (double)D * (1.0 + cmax) * (1.0 + cmax) + 1e-8 * (pp2 + cmax * cmax) +
+                     8.0 * 1.1920928955078125e-07 * amax + 1e-300;
+    const bool live = grow < N && (r & 1) == 0;
+    const bool fin = isfinite(p2f) && isfinite(e) && pn * cmax < 1e36 && cmax * cmax < 1e36 &&
+                     isfinite(b1) && isfinite(b2);
+    const bool dec = fin && (double)b2 - (double)b1 > 2.0 * e;
+    if (live && dec) labels[grow] = i1;
+    if (live && !fin) full_list[atomicAdd(&counters[0], 1u)] = grow;
+    const bool needc = live && fin && !dec;
+    const unsigned long long und = __ballot(needc);
+    if (und) {  // wave-uniform: one slot range per wave
+      unsigned int base = 0;
+      if (lane == 0) base = atomicAdd(&counters[2], (unsigned int)__popcll(und));
+      base = __builtin_amdgcn_readfirstlane(base);
+      if (needc) und_list[base + (unsigned int)__popcll(und & ((1ull << lane) - 1ull))] = grow;
+    }
+  }
+}
+
+template <int NCT, int KS>
+static void ks_launch(hipStream_t s, i64 N, const float* P, i64 ldp, const __bf16* CBh, const __bf16* CBl,
+                      const float* cnf, const double* cmax, i64* labels, unsigned int* counters, i64* full_list,
+                      i64* und_list, int grid) {
+  const size_t lds = ks_lds_bytes(16 * KS, NCT);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_kmeans_filter_as<NCT, KS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)ks_lds_bytes(KB_DMAX, 8));
+    attr = true;
+  }
+  k_kmeans_filter_as<NCT, KS><<<grid, KS_WAVES * 64, lds, s>>>(N, P, ldp, CBh, CBl, cnf, cmax, labels, counters,
+                                                               full_list, und_list);
+}
+
+template <int NCT>
+static void ks_launch_d(hipStream_t s, i64 N, i64 D, const float* P, i64 ldp, const __bf16* CBh, const __bf16* CBl,
+                        const float* cnf, const double* cmax, i64* labels, unsigned int* counters, i64* full_list,
+                        i64* und_list, int grid) {
+  if (D == 64) ks_launch<NCT, 4>(s, N, P, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_list, grid);
+  else ks_launch<NCT, 8>(s, N, P, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_list, grid);
 }
 
 // Exact-order labels of the undecided points from their candidate masks
@@ -1723,6 +2033,14 @@ static void ka_grid(int dtype, i64 N, i64 D, i64 K, i64* G, i64* ndb, i64* ncb) 
 
 static i64 kf_kp(i64 K) { return (K + KF_BN - 1) / KF_BN * KF_BN; }
 
+// SPX_KMEANS_FILTER=b3 selects the single all-accumulator filter pass (A/B
+// timing and the bit-exactness cross-check in the GPU tests); default: the
+// A-stationary pass + list-mode candidates
+static int kmeans_filter_mode() {
+  const char* v = getenv("SPX_KMEANS_FILTER");
+  return (v && strcmp(v, "b3") == 0) ? 1 : 0;
+}
+
 static int kf_persistent_grid(i64 N) {
   const i64 g = (N + 255) / 256;
   return (int)(g < 2048 ? (g < 1 ? 1 : g) : 2048);
@@ -1732,7 +2050,9 @@ extern "C" int64_t spx_kmeans_assign_workspace(int dtype, int64_t N, int64_t D, 
   if ((dtype != SPX_F32 && dtype != SPX_F64) || N < 0 || D < 1 || K < 1) return -1;
   const i64 Kp = kf_kp(K);
   // CT (D x Kp f32) | cn (Kp f64) | cmax | counters | full list (N i64) | candidate list (N KfCand, K <= 256)
-  return (D * Kp * 4 + 15) / 16 * 16 + Kp * 8 + 16 + 16 + N * 8 + (Kp == KF_BN ? N * (i64)sizeof(KfCand) : 0);
+  // | undecided-row list (N i64, K <= 256)
+  return (D * Kp * 4 + 15) / 16 * 16 + Kp * 8 + 16 + 16 + N * 8 +
+         (Kp == KF_BN ? N * (i64)sizeof(KfCand) + N * 8 : 0);
 }
 
 extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
@@ -1770,7 +2090,9 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
   i64* full_list = (i64*)ws;
   ws += N * 8;
   KfCand* cand_list = (KfCand*)ws;
-  HIP_TRY(hipMemsetAsync(counters, 0, 2 * sizeof(unsigned int), S(stream)));
+  i64* und_list = (i64*)(ws + (Kp == KF_BN ? N * (i64)sizeof(KfCand) : 0));
+  // counters: [0] full-list rows, [1] candidate rows, [2] undecided rows
+  HIP_TRY(hipMemsetAsync(counters, 0, 4 * sizeof(unsigned int), S(stream)));
   const int gp = kf_persistent_grid(N);
   if (dtype == SPX_F32 && Kp == KF_BN && D % 64 == 0 && D <= KB_DMAX && ldp % 4 == 0 &&
       ((uintptr_t)points % 16) == 0) {
@@ -1788,16 +2110,39 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
       HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     }
     const i64 ntiles = (N + 31) / 32;
-    const i64 need_blocks = (ntiles + KB_WAVES - 1) / KB_WAVES;
-    const int grid = (int)(need_blocks < ncu ? need_blocks : ncu);
     const float* Pf = (const float*)points;
-    switch (nct) {
-      case 1: kb_launch<1>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, grid); break;
-      case 2: kb_launch<2>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, grid); break;
-      case 4: kb_launch<4>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, grid); break;
-      default: kb_launch<8>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, grid); break;
+    if (kmeans_filter_mode() == 0) {
+      // A-stationary first pass over every point, then the all-accumulator
+      // filter in list mode over its undecided rows (candidate masks)
+      const i64 need_as = (ntiles + KS_WAVES - 1) / KS_WAVES;
+      const int grid_as = (int)(need_as < ncu ? need_as : ncu);
+      switch (nct) {
+        case 1: ks_launch_d<1>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_list, grid_as); break;
+        case 2: ks_launch_d<2>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_list, grid_as); break;
+        case 4: ks_launch_d<4>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_list, grid_as); break;
+        default: ks_launch_d<8>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_list, grid_as); break;
+      }
+      LAUNCH_CHECK("spx_kmeans_assign(filter A-stationary)");
+      const i64* rin = und_list;
+      const unsigned int* nin = counters + 2;
+      switch (nct) {
+        case 1: kb_launch<1>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, ncu, rin, nin); break;
+        case 2: kb_launch<2>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, ncu, rin, nin); break;
+        case 4: kb_launch<4>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, ncu, rin, nin); break;
+        default: kb_launch<8>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, ncu, rin, nin); break;
+      }
+      LAUNCH_CHECK("spx_kmeans_assign(filter bf16x3, undecided rows)");
+    } else {
+      const i64 need_blocks = (ntiles + KB_WAVES - 1) / KB_WAVES;
+      const int grid = (int)(need_blocks < ncu ? need_blocks : ncu);
+      switch (nct) {
+        case 1: kb_launch<1>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, grid); break;
+        case 2: kb_launch<2>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, grid); break;
+        case 4: kb_launch<4>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, grid); break;
+        default: kb_launch<8>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, grid); break;
+      }
+      LAUNCH_CHECK("spx_kmeans_assign(filter bf16x3)");
     }
-    LAUNCH_CHECK("spx_kmeans_assign(filter bf16x3)");
     k_kmeans_cand<float, true><<<gp, 256, 0, S(stream)>>>(D, Pf, ldp, centers, labels, counters, cand_list);
     LAUNCH_CHECK("spx_kmeans_assign(candidates)");
     k_kmeans_assign<float><<<gp, 256, 0, S(stream)>>>(N, D, K, Pf, ldp, centers, labels, nullptr, full_list,

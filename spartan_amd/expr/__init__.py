@@ -1,6 +1,6 @@
 """spartan_amd.expr -- the spartan.expr API (spartan/expr/__init__.py:26-53)
 on the MI355X tile-execution backend."""
-from .base import (Expr, NotShapeable, as_array, eager, evaluate, force, glom, lazify,
+from .base import (Expr, NotShapeable, as_array, eager, evaluate, force, glom, lazify, newaxis,
                    optimized_dag)
 from .builtins import (abs, add, arange, argmax, argmin, astype, bincount, concatenate, count_nonzero,
                        count_zero, exp,
@@ -17,6 +17,7 @@ from .slice import slice_expr
 from .transpose import transpose
 from .write_array import from_file, from_numpy, write
 
+Expr.outer = outer
 Expr.sum = sum
 Expr.mean = mean
 Expr.astype = astype

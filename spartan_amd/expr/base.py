@@ -23,6 +23,11 @@ from ..util import log
 _ids = itertools.count()
 
 
+class newaxis(object):
+  """Marks a new unit dimension in ``x[...]`` (reference base.py:23-26;
+  NumPy's ``None`` / ``np.newaxis`` is accepted too)."""
+
+
 class NotShapeable(Exception):
   pass
 
@@ -196,8 +201,27 @@ class Expr:
   def __xor__(self, o): return _map(self, o, fn=np.logical_xor)
 
   def __getitem__(self, idx):
-    from .slice import slice_expr
-    return slice_expr(self, idx)
+    """Basic indexing (reference base.py:388-430): slices give a zero-copy
+    slice view; an int index drops its dimension and ``newaxis`` inserts a
+    unit dimension -- the reference's ReshapeExpr over the SliceExpr, here a
+    zero-copy UnitDims view."""
+    from .slice import slice_expr, unit_dims
+    items = idx if isinstance(idx, tuple) else (idx,)
+    if not any(_is_newaxis(i) or isinstance(i, (int, np.integer)) for i in items):
+      return slice_expr(self, idx)
+    core = tuple(i for i in items if not _is_newaxis(i))
+    sl = slice_expr(self, core) if core else self
+    kept = iter(sl.shape)
+    new_shape = []
+    for i in items:
+      if _is_newaxis(i):
+        new_shape.append(1)
+      elif isinstance(i, (int, np.integer)):
+        next(kept)  # an int index drops its (length-1) dimension
+      else:
+        new_shape.append(next(kept))
+    new_shape.extend(kept)  # trailing dims the index did not name
+    return unit_dims(sl, tuple(new_shape))
 
   @property
   def T(self):
@@ -210,6 +234,10 @@ class Expr:
   def reshape(self, new_shape):
     from .reshape import reshape
     return reshape(self, new_shape)
+
+
+def _is_newaxis(i):
+  return i is None or i is newaxis
 
 
 def _map(*args, fn):

@@ -43,3 +43,34 @@ def slice_expr(src, idx):
   e = SliceExpr(src=src)
   e.idx = idx
   return e
+
+
+class UnitDimsExpr(Expr):
+  """Drop / insert length-1 dims of ``array`` without a copy (the reference
+  wraps int / newaxis indexing in a ReshapeExpr, base.py:402-430)."""
+  _members = ('array',)
+
+  def compute_shape(self):
+    return self.new_shape
+
+  def compute_dtype(self):
+    return self.array.dtype
+
+  def pretty_str(self):
+    return 'UnitDims[%d](%s, %s)' % (self.expr_id, self.array, self.new_shape)
+
+  def _evaluate(self, deps):
+    from ..array.distarray import LocalWrapper, ReplicatedArray
+    from ..array.views import unit_dims_of
+    a = deps['array']
+    if isinstance(a, ReplicatedArray):
+      return ReplicatedArray(a.device_data().reshape(self.new_shape))
+    if isinstance(a, LocalWrapper):
+      return LocalWrapper(np.asarray(a.value).reshape(self.new_shape))
+    return unit_dims_of(a, self.new_shape)
+
+
+def unit_dims(array, new_shape):
+  e = UnitDimsExpr(array=array)
+  e.new_shape = tuple(int(s) for s in new_shape)
+  return e

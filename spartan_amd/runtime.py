@@ -6,8 +6,9 @@ execution model: ONE process per GPU, launched by torchrun, all processes
 running the same (SPMD) program.  A tile *worker* index (the reference's
 ``TileId.worker``, spartan/core.pyx:16-41) is owned by rank ``worker % world``.
 Every rank computes the same tile plan, runs the kernels for the tiles it owns
-on its own GPU, and exchanges data only through torch.distributed collectives
-(backend "nccl" == RCCL over xGMI on ROCm; "gloo" for CPU-only tests).
+on its own GPU, and exchanges data only through RCCL collectives over xGMI
+issued through libspx.so's C ABI (comm.py); torch.distributed (gloo) is the
+host control plane, and gloo alone carries the CPU-only tests.
 """
 import os
 
@@ -17,15 +18,24 @@ _ctx = None
 
 
 class Context:
-  def __init__(self, rank, world_size, local_rank, device, dist_backend):
+  def __init__(self, rank, world_size, local_rank, device, dist_backend, rccl=None):
     self.rank = rank
     self.world_size = world_size
     self.local_rank = local_rank
     self.device = device
-    self.dist_backend = dist_backend
+    self.dist_backend = dist_backend   # data plane: 'rccl' (libspx), 'gloo' (tests / rehearsal), 'nccl' (torch)
+    self.rccl = rccl                   # libspx RCCL communicator handle when dist_backend == 'rccl'
+    self._comm_stream = None
     self.num_workers = int(FLAGS.num_workers or world_size)
     if self.num_workers < 1:
       raise ValueError('num_workers must be >= 1')
+
+  def comm_stream(self):
+    """Side HIP stream for collectives that overlap compute (dot slab reduces)."""
+    if self._comm_stream is None:
+      import torch
+      self._comm_stream = torch.cuda.Stream(device=self.device)
+    return self._comm_stream
 
   # reference blob_ctx.BlobCtx.num_workers semantics
   def owner(self, worker):
@@ -49,10 +59,16 @@ class Context:
 def initialize(argv=None, device=None):
   """Bring up this rank (reference spartan.initialize, spartan/__init__.py:42-56).
 
-  Reads RANK / WORLD_SIZE / LOCAL_RANK from the torchrun environment, selects
-  cuda:LOCAL_RANK, and initialises torch.distributed (nccl on GPU) when the
-  world has more than one rank.  ``device`` overrides the device (tests run
-  the host logic on 'cpu' with a test backend and gloo)."""
+  Reads RANK / WORLD_SIZE / LOCAL_RANK from the torchrun environment and
+  selects cuda:LOCAL_RANK.  With more than one rank on GPUs the data plane is
+  an RCCL communicator created through libspx.so (spx_comm_init; every device
+  collective is a C-ABI call, comm.py) and torch.distributed runs gloo as the
+  host control plane (the unique-id hand-off, barriers, host maxima).
+  ``SPARTAN_DIST_BACKEND=gloo`` rehearses N ranks on fewer GPUs (device
+  tensors staged through the host); ``SPARTAN_COMM=torch`` uses
+  torch.distributed's own RCCL group instead of libspx's.  ``device``
+  overrides the device (tests run the host logic on 'cpu' with a test
+  backend and gloo)."""
   global _ctx
   import torch
   if argv is not None:
@@ -67,19 +83,25 @@ def initialize(argv=None, device=None):
     torch.cuda.set_device(device)
   device = torch.device(device)
   backend = None
+  rccl = None
   if world > 1:
     import torch.distributed as dist
-    backend = 'nccl' if device.type == 'cuda' else 'gloo'
-    # SPARTAN_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (device
-    # tensors staged through the host by comm.py); RCCL otherwise
-    backend = os.environ.get('SPARTAN_DIST_BACKEND', backend)
+    backend = os.environ.get('SPARTAN_DIST_BACKEND', 'rccl' if device.type == 'cuda' else 'gloo')
+    if backend == 'nccl' or (backend == 'rccl' and os.environ.get('SPARTAN_COMM') == 'torch'):
+      backend = 'nccl'
+    pg = 'nccl' if backend == 'nccl' else 'gloo'   # torch.distributed: control plane (or the torch RCCL path)
     if not dist.is_initialized():
       os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
       kw = {}
-      if device.type == 'cuda' and backend == 'nccl':
+      if device.type == 'cuda' and pg == 'nccl':
         kw['device_id'] = device
-      dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
-  _ctx = Context(rank, world, local_rank, device, backend)
+      dist.init_process_group(backend=pg, rank=rank, world_size=world, **kw)
+    if backend == 'rccl':
+      from . import comm
+      obj = [comm.rccl_unique_id() if rank == 0 else None]
+      dist.broadcast_object_list(obj, src=0)
+      rccl = comm.rccl_init(rank, world, obj[0])
+  _ctx = Context(rank, world, local_rank, device, backend, rccl)
   return _ctx
 
 
@@ -87,6 +109,12 @@ def shutdown():
   global _ctx
   if _ctx is not None and _ctx.distributed:
     import torch.distributed as dist
+    if _ctx.rccl is not None:
+      import torch
+      from . import comm
+      torch.cuda.synchronize(_ctx.device)
+      comm.rccl_destroy(_ctx.rccl)
+      _ctx.rccl = None
     if dist.is_initialized():
       dist.barrier()
       dist.destroy_process_group()

@@ -19,7 +19,9 @@ def test_header_lists_the_boundary():
   names = declared()
   for n in ['spx_abi_version', 'spx_last_error', 'spx_module_load', 'spx_module_function', 'spx_launch',
             'spx_fill', 'spx_reduce_finalize', 'spx_merge', 'spx_copy_region', 'spx_gemm',
-            'spx_argreduce_combine', 'spx_module_unload']:
+            'spx_argreduce_combine', 'spx_module_unload', 'spx_comm_load', 'spx_comm_unique_id',
+            'spx_comm_init', 'spx_comm_destroy', 'spx_allreduce', 'spx_reduce_scatter', 'spx_allgather',
+            'spx_broadcast', 'spx_reduce', 'spx_sendrecv']:
     assert n in names
 
 
@@ -57,3 +59,31 @@ def test_argument_validation_without_gpu():
                     ctypes.c_int64(4), None, ctypes.c_int64(4), None, ctypes.c_int64(4),
                     ctypes.c_double(1), ctypes.c_double(0), None)
   assert rc == -1 and b'leading dimension' in lib.spx_last_error()
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason='libspx.so not built')
+def test_collectives_boundary_without_gpu():
+  """RCCL is opened at run time: before spx_comm_load every collective
+  refuses; after it (PyTorch's own RCCL) a unique id can be made without a
+  device; bad dtypes / ops are rejected before RCCL sees them."""
+  import subprocess
+  import sys
+  code = r'''
+import ctypes, sys
+sys.path.insert(0, %r)
+from spartan_amd import backend, comm
+lib = backend.load_library()
+assert lib.spx_allreduce(None, None, None, 4, 3, 0, None) == -1
+assert b'spx_comm_load' in lib.spx_last_error()
+uid = comm.rccl_unique_id()
+assert len(uid) == 128 and any(uid)
+assert lib.spx_allreduce(ctypes.c_void_p(1), None, None, 4, 9, 0, None) == -1
+assert b'dtype' in lib.spx_last_error()
+assert lib.spx_reduce_scatter(ctypes.c_void_p(1), None, None, 4, 3, 4, None) == -1
+assert b'op' in lib.spx_last_error()
+assert lib.spx_comm_init(uid, 128, 2, 2, ctypes.byref(ctypes.c_void_p())) == -1
+assert lib.spx_comm_load(b'/nonexistent/librccl.so') == 0  # already loaded: a no-op
+print('ok')
+''' % ROOT
+  r = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, timeout=120)
+  assert r.returncode == 0 and r.stdout.strip().endswith('ok'), r.stderr[-2000:]

@@ -210,6 +210,48 @@ def test_gemm_random(ex, dtype, rtol, shape, W):
   check_fp(got, cpu, exact, rtol)
 
 
+@pytest.mark.parametrize('dtype,rtol', [(np.float32, 1e-5), (np.float64, 1e-12)])
+def test_dot_cfg4_full_size(ex, dtype, rtol):
+  """configs[3] at its BASELINE size, 32768^2 (K = 32768 accumulation depth),
+  through the same expr.dot the bench times.  Size-independent properties
+  checked in fp64 on the device: row sums of C equal A . (B 1) and column
+  sums equal (1^T A) . B; plus spot elements against an fp64 host dot of
+  the generator's own values, under the CPU-or-closer rule (rtol 1e-5 fp32,
+  1e-12 fp64; reference dot.py:238-283)."""
+  expr, setw = ex
+  setw(1)
+  S = 32768
+  f64 = np.float64
+  A = expr.rand(S, S, dtype=dtype, seed=31).force()
+  B = expr.rand(S, S, dtype=dtype, seed=32).force()
+  Ae, Be = expr.lazify(A), expr.lazify(B)
+  C = expr.dot(Ae, Be).force()
+  Ce = expr.lazify(C)
+  # row sums: sum_j C[i, j] = A[i, :] . rowsum(B)
+  b1 = expr.sum(expr.astype(Be, f64), axis=1).glom()
+  want_rows = expr.dot(expr.astype(Ae, f64), b1).glom()
+  got_rows = expr.sum(expr.astype(Ce, f64), axis=1).glom()
+  a0 = expr.sum(expr.astype(Ae, f64), axis=0).glom()
+  want_cols = expr.dot(expr.transpose(expr.astype(Be, f64)), a0).glom()
+  got_cols = expr.sum(expr.astype(Ce, f64), axis=0).glom()
+  for got, want in ((got_rows, want_rows), (got_cols, want_cols)):
+    rel = np.abs(got - want) / np.abs(want)
+    assert rel.max() <= rtol, 'max rel err %g' % rel.max()
+  # spot elements vs the generator's values on the host
+  rows = [0, 1, 4097, 16383, 20000, 32767]
+  cols = [0, 5, 8191, 16384, 30001, 32767]
+  k = np.arange(S, dtype=np.uint64)
+  for r in rows:
+    crow = Ce[r:r + 1, :].glom().reshape(S)
+    arow = rng.uniform_values(np.uint64(r * S) + k, 31, 0.0, 1.0, dtype)
+    for c in cols:
+      bcol = rng.uniform_values(k * np.uint64(S) + np.uint64(c), 32, 0.0, 1.0, dtype)
+      cpu = np.dot(arow, bcol)
+      exact = np.dot(arow.astype(f64), bcol.astype(f64))
+      check_fp(np.array([crow[c]]), np.array([cpu]), np.array([exact]), rtol)
+  del A, B, C, Ae, Be, Ce
+
+
 def test_gemm_layout_asymmetric(ex):
   """A = I with an asymmetric B catches a transposed C write."""
   expr, setw = ex
@@ -833,3 +875,47 @@ def test_map_forced_operands_gpu(ex, W):
   got = expr.sum(expr.map(a, np.sqrt), axis=0).optimized().glom()
   mapped = np.sqrt(na)
   check_fp(got, O.sum_tiles(mapped, 0, W), mapped.astype(np.float64).sum(0), 1e-5)
+
+
+def test_rccl_single_rank_collectives(ex):
+  """Every libspx collective on a one-rank RCCL communicator (the only
+  communicator one GPU can hold): dtype / op mapping, stream order, in-place
+  and out-of-place buffers, grouped point-to-point to self.  The N-rank
+  decomposition logic above it is the gloo world-2 tests' (same comm.py
+  call sites)."""
+  import ctypes
+  import torch
+  from spartan_amd import comm
+  lib = comm._lib()
+  uid = comm.rccl_unique_id()
+  c = comm.rccl_init(0, 1, uid)
+  try:
+    dev = torch.device('cuda', torch.cuda.current_device())
+    st = comm._stream()
+    for dt in (torch.float32, torch.float64, torch.int64, torch.int32):
+      x = (torch.arange(1000, device=dev) * 3 - 7).to(dt)
+      y = torch.empty_like(x)
+      for op in (0, 1, 2):
+        assert lib.spx_allreduce(c, comm._p(x), comm._p(y), x.numel(), comm._dt(x), op, st) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(x, y)
+      assert lib.spx_reduce_scatter(c, comm._p(x), comm._p(y), x.numel(), comm._dt(x), 0, st) == 0
+      g = torch.empty((1, 1000), dtype=dt, device=dev)
+      assert lib.spx_allgather(c, comm._p(x), comm._p(g), x.numel(), comm._dt(x), st) == 0
+      z = x.clone()
+      assert lib.spx_broadcast(c, comm._p(z), comm._p(z), z.numel(), comm._dt(z), 0, st) == 0
+      r = torch.empty_like(x)
+      assert lib.spx_reduce(c, comm._p(x), comm._p(r), x.numel(), comm._dt(x), 0, 0, st) == 0
+      torch.cuda.synchronize()
+      assert torch.equal(y, x) and torch.equal(g[0], x) and torch.equal(z, x) and torch.equal(r, x)
+    a = torch.arange(257, dtype=torch.float64, device=dev)
+    b = torch.zeros_like(a)
+    VP, I64, I32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+    rc = lib.spx_sendrecv(c, 1, (VP * 1)(a.data_ptr()), (I64 * 1)(a.numel() * 8), (I32 * 1)(0),
+                          1, (VP * 1)(b.data_ptr()), (I64 * 1)(b.numel() * 8), (I32 * 1)(0), st)
+    assert rc == 0, lib.spx_last_error()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+  finally:
+    torch.cuda.synchronize()
+    comm.rccl_destroy(c)

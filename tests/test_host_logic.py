@@ -250,3 +250,18 @@ def test_map_forced_operands(host_ctx):
   np.testing.assert_array_equal(expr.map((a, a), np.add).glom(), na + na)
   np.testing.assert_array_equal(expr.astype(a, np.float32).glom(), na.astype(np.float32))
   np.testing.assert_allclose(expr.std(a, 0).glom(), na.std(0), rtol=1e-12)
+
+
+def test_expr_method_surface(host_ctx):
+  """Methods the reference attaches to Expr (spartan/expr/__init__.py:47-53)
+  and the newaxis marker (base.py:23-26)."""
+  host_ctx(2)
+  from spartan_amd import expr
+  from spartan_amd.expr import join
+  for name in ('outer', 'sum', 'mean', 'astype', 'argmin', 'argmax'):
+    assert callable(getattr(expr.Expr, name)), name
+  assert expr.Expr.outer is join.outer
+  x = expr.arange((6, 4))
+  assert x[expr.newaxis, :, 1:3].shape == (1, 6, 2)
+  assert x[:, None].shape == (6, 1, 4)
+  assert x[2, None].shape == (1, 4)

@@ -53,6 +53,14 @@ def _views_cases(expr):
   cases.append(('reshape_dot', expr.dot(expr.reshape(expr.from_numpy(q1), (45, 7)), expr.from_numpy(q2)),
                 q1.reshape(45, 7) @ q2))                                                 # :95-121
   cases.append(('reshape_transpose', expr.reshape(expr.transpose(t1), (13 * 37,)), t2.T.reshape(-1)))
+  # newaxis indexing (reference base.py:23-30, 402-430) and Expr.outer (expr/__init__.py:47)
+  na_ = expr.newaxis
+  cases.append(('newaxis_front', x[na_, 2:5], nx[None, 2:5]))
+  cases.append(('newaxis_mid', x[:, na_], nx[:, None]))
+  cases.append(('newaxis_int', x[3, na_], nx[3, None]))
+  cases.append(('newaxis_none', x[1:4, None, 2:6], nx[1:4, None, 2:6]))
+  cases.append(('newaxis_bcast', (x[:, na_, 0:3] * x3[0:10, 0:1, 0:3]).sum(1),
+                (nx[:, None, 0:3] * nx3[0:10, 0:1, 0:3]).sum(1)))
   return cases
 
 
