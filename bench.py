@@ -200,12 +200,25 @@ def main():
   if args.workloads:
     result['lreg'] = leg(bench_lreg, args.lreg_points, ctx, expr, comm, sync)
     result['kmeans'] = leg(bench_kmeans, args.km_points, ctx, expr, comm, sync)
+    result['kmeans_api'] = leg(bench_kmeans_api, args.km_points, ctx, expr, comm, sync)
 
   if args.cpu_baseline and N == 1 and ctx.rank == 0:
-    from oracle.cpu_baseline import cfg2_cpu_baseline
-    cb = cfg2_cpu_baseline(rows=min(args.cpu_rows, S), cols=S, reps=5)
-    result['cpu_baseline'] = {k: cb[k] for k in ('value', 'unit', 'cores', 'kind', 'sample')}
-    result['cpu_baseline']['value'] = round(cb['value'], 3)
+    # the reference's multi-worker CPU model on this box's host cores
+    # (oracle/cpu_baseline.py; bounded samples, about 30 s in all)
+    from oracle import cpu_baseline as CB
+    cb = CB.cfg2_cpu_baseline(rows=min(args.cpu_rows, S), cols=S, reps=5)
+    out = {k: cb[k] for k in ('value', 'unit', 'cores', 'kind', 'sample', 'single_process', 'host')}
+    out['value'] = round(cb['value'], 3)
+    legs = {}
+    for name, fn, kw in (('dot', CB.dot_cpu_baseline, {'S': 4096}),
+                         ('lreg', CB.lreg_cpu_baseline, {'N': 20_000_000}),
+                         ('kmeans', CB.kmeans_cpu_baseline, {'N': 1_000_000})):
+      try:
+        legs[name] = fn(**kw)
+      except Exception as e:  # noqa: BLE001  (a failing side leg is reported, not fatal)
+        legs[name] = {'error': '%s: %s' % (type(e).__name__, str(e)[:200])}
+    out['legs'] = legs
+    result['cpu_baseline'] = out
   if ctx.rank == 0:
     print(json.dumps(result), flush=True)
   spartan_amd.shutdown()
@@ -282,6 +295,33 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
                    'assign = bf16x3-MFMA certified filter + exact-order fp64 recompute of undecided points '
                    '(bit-exact labels), fp64 centroid sums' % (npts, D, K, K)}
   del X, labels
+  torch.cuda.empty_cache()
+  return out
+
+
+def bench_kmeans_api(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
+  """configs[2] through the drop-in API: the reference's KMeans.fit loop
+  (k_means_.py:125-152) -- expr.outer + expr.argmin (fused into the certified
+  assignment), map2 bincount, map2 centre sums, host divide -- on the same
+  points and initial centres as the direct-kernel leg."""
+  import torch
+  from spartan_amd.array import distarray, extent as ext
+  from spartan_amd.examples.kmeans import KMeans
+  X = expr.rand(npts * ctx.world_size, D, dtype=np.float32, seed=21).force()
+  c0 = distarray.glom_region(X, ext.create((0, 0), (K, D), X.shape)).astype(np.float64)
+  KMeans(K, 1).fit(X, c0)  # warm-up
+  sync()
+  comm.barrier()
+  t0 = time.perf_counter()
+  KMeans(K, iters).fit(X, c0)
+  sync()
+  comm.barrier()
+  el = comm.max_over_ranks(time.perf_counter() - t0) / iters
+  n = npts * ctx.world_size
+  out = {'ms_per_iter': round(el * 1e3, 3), 'points_per_s': round(n / el, 1),
+         'config': 'cfg3 via examples.kmeans.KMeans(%d, %d).fit(X, first %d points): outer + argmin '
+                   '(OuterArgminFusion -> certified assignment), map2 bincount, map2 centre sums' % (K, iters, K)}
+  del X
   torch.cuda.empty_cache()
   return out
 

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SPX_ABI_VERSION 1
+#define SPX_ABI_VERSION 2  /* 2: spx_kmeans_assign dist_dtype; collectives */
 
 /* error codes */
 #define SPX_OK 0
@@ -160,11 +160,17 @@ int spx_argreduce_combine(int op, int dtype, const void* vals, const int64_t* id
  * only the remaining points run the exact-order kernel.  The labels are the
  * same bits either way.  With mindist != NULL (receives the fp64 distance)
  * or workspace == NULL every point takes the exact-order kernel.
+ * dist_dtype SPX_F64: argmin of the fp64 distances; SPX_F32: argmin of the
+ * distances rounded to fp32, first index on equal rounded values -- the
+ * outer product's target is fp32 when the points are (map2 / outer dtype
+ * None -> arrays[0].dtype, k_means_.py:126-127), and the reference rounds the
+ * cdist values into it before argmin.  The certified gap then also covers
+ * the rounding (exact distances more than 2 fp32 ulps apart).
  */
 int64_t spx_kmeans_assign_workspace(int dtype, int64_t N, int64_t D, int64_t K);
 int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
                       const double* centers, int64_t* labels, double* mindist, void* workspace,
-                      size_t workspace_bytes, void* stream);
+                      size_t workspace_bytes, int dist_dtype, void* stream);
 /* Per-centre sums (fp64, K x D) and counts (K) of the points carrying each
  * label (labels outside [0, K) are skipped), ADDED into sums/counts (which are
  * overwritten instead when zero_first != 0): replaces kmeans_center_mapper /

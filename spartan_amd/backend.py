@@ -88,7 +88,7 @@ _SIGS = {
                                      ctypes.c_int64),
     'spx_kmeans_assign': ([ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                            ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                           ctypes.c_size_t, ctypes.c_void_p], ctypes.c_int),
+                           ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
     'spx_kmeans_accumulate_workspace': ([ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64],
                                          ctypes.c_int64),
     'spx_kmeans_accumulate': ([ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
@@ -593,10 +593,11 @@ class HipBackend:
 
 
   # --------------------------------------------------------------- k-means
-  def kmeans_assign(self, points, centers, labels, mindist=None, exact_only=False):
-    """labels[p] = first argmin_c cdist(points[p], centers[c]) (exact fp64 order).
-    Default: MFMA-certified fast path + exact-order kernel for the undecided
-    points; exact_only=True (or mindist) runs every point exactly."""
+  def kmeans_assign(self, points, centers, labels, mindist=None, exact_only=False, dist_dtype=np.float64):
+    """labels[p] = first argmin_c cdist(points[p], centers[c]) (exact fp64
+    order; dist_dtype float32: of the distances rounded to fp32).  Default:
+    MFMA-certified fast path + exact-order kernel for the undecided points;
+    exact_only=True (or mindist) runs every point exactly."""
     N, D = points.shape
     K = centers.shape[0]
     assert centers.dtype == self._f64() and tuple(centers.shape) == (K, D) and labels.shape[0] == N
@@ -612,7 +613,7 @@ class HipBackend:
                                       ctypes.c_void_p(centers.data_ptr()), ctypes.c_void_p(labels.data_ptr()),
                                       ctypes.c_void_p(mindist.data_ptr() if mindist is not None else 0),
                                       ctypes.c_void_p(ws.data_ptr() if ws is not None else 0), nws,
-                                      self.stream()), 'spx_kmeans_assign')
+                                      spx_dtype(dist_dtype), self.stream()), 'spx_kmeans_assign')
 
   def kmeans_accumulate(self, points, labels, sums, counts, zero_first=True):
     N, D = points.shape

@@ -96,6 +96,7 @@ FLAGS.add('opt_auto_tiling', True, bool, 'row / column partitioning chosen by th
 FLAGS.add('opt_outer_argmin_fusion', True, bool,
           'argmin(outer(X, C, registered distance mapper), axis=1) -> one fused assignment kernel')
 FLAGS.add('opt_expression_cache', True, bool)
+FLAGS.add('opt_plan_cache', True, bool, 'replay the optimised DAG of a structure seen before (expr/plan_cache.py)')
 FLAGS.add('dot_overlap', True, bool, 'multi-rank dot: reduce each output row slab while the next one computes')
 FLAGS.add('rng_seed', 0x5EED, int, 'base seed of the counter-based rand()')
 FLAGS.add('kernel_cache_dir', '', str, 'override the JIT code-object cache directory')

@@ -712,9 +712,11 @@ template <typename TP>
 __global__ __launch_bounds__(256) void k_kmeans_assign(i64 N, i64 D, i64 K, const TP* __restrict__ P, i64 ldp,
                                                        const double* __restrict__ C, i64* __restrict__ labels,
                                                        double* __restrict__ mind, const i64* __restrict__ rows,
-                                                       const unsigned int* __restrict__ nrows) {
+                                                       const unsigned int* __restrict__ nrows, int r32) {
   // rows != NULL: only the *nrows points rows[0..*nrows) (the filter's
-  // undecided points); the grid is sized for the worst case.
+  // undecided points); the grid is sized for the worst case.  r32: the
+  // distances are rounded to fp32 before the argmin (an outer product whose
+  // target is fp32 stores them so: the reference's target.update casts).
   __shared__ double Cs[KM_CC][KM_DC];
   const i64 n = rows ? (i64)*nrows : N;
   for (i64 base = (i64)blockIdx.x * 256; base < n; base += (i64)gridDim.x * 256) {  // block-uniform
@@ -753,6 +755,7 @@ __global__ __launch_bounds__(256) void k_kmeans_assign(i64 N, i64 D, i64 K, cons
     for (int cc = 0; cc < KM_CC; ++cc) {
       if (c0 + cc < K) {
         double dist = sqrt(s[cc]);
+        if (r32) dist = (double)(float)dist;
         if (bi < 0 || dist < best || (dist != dist && best == best)) {
           best = dist;
           bi = c0 + cc;
@@ -854,7 +857,11 @@ __global__ __launch_bounds__(BM * 4, MINW) void k_kmeans_filter(i64 N, i64 D, i6
     si[i] = -1;
     bad[i] = false;
   }
-  const double cmax = *cmax_p;
+  const double cmax = cmax_p[0];
+  // fp32 target: two exact distances whose squares differ by more than
+  // 2^-21 (|p| + |c|)^2 are more than 2 fp32 ulps apart, so they cannot
+  // round to one value; the margin is folded into e (gap > 2e + margin)
+  const double mcoef = cmax_p[1];
   const double u32 = 5.9604644775390625e-08;
   V ra, rb[LB];
   for (i64 c0 = 0; c0 < Kp; c0 += BN) {
@@ -971,7 +978,7 @@ __global__ __launch_bounds__(BM * 4, MINW) void k_kmeans_filter(i64 N, i64 D, i6
       const double pnorm = sqrt(p2) * 1.0001;
       const double e = 2.0 * (double)(D + 3) * 1.01 * u32 * pnorm * cmax +
                        2.02 * u32 * (cmax * cmax + pnorm * cmax) + 4.0 * (double)D * 1.2e-38 * (1.0 + cmax) +
-                       1e-8 * (p2 + cmax * cmax) + 1e-300;
+                       1e-8 * (p2 + cmax * cmax) + 0.5 * mcoef * (pnorm + cmax) * (pnorm + cmax) + 1e-300;
       const bool fin = !bad[i] && isfinite(s1[i]) && isfinite(e);
       if (fin && (double)s2[i] - (double)s1[i] > 2.0 * e) {
         if (sub == 0) labels[row] = si[i];
@@ -1060,7 +1067,8 @@ typedef float kb_f4 __attribute__((ext_vector_type(4)));
 // (float)|C[c]|^2 (+inf past K); *cmax = max_c |C[c]| (one block).
 __global__ __launch_bounds__(256) void k_kmeans_prep_b3(i64 D, i64 K, i64 Kp, const double* __restrict__ C,
                                                         __bf16* __restrict__ CBh, __bf16* __restrict__ CBl,
-                                                        float* __restrict__ cnf, double* __restrict__ cmax) {
+                                                        float* __restrict__ cnf, double* __restrict__ cmax,
+                                                        double mcoef) {
   __shared__ double red[256];
   double mx = 0.0;
   for (i64 c = threadIdx.x; c < Kp; c += 256) {
@@ -1088,7 +1096,10 @@ __global__ __launch_bounds__(256) void k_kmeans_prep_b3(i64 D, i64 K, i64 Kp, co
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) *cmax = sqrt(red[0]) * 1.001;
+  if (threadIdx.x == 0) {
+    cmax[0] = sqrt(red[0]) * 1.001;
+    cmax[1] = mcoef;  // fp32 tie margin coefficient (0: fp64 distances), read by the filters
+  }
 }
 
 static size_t kb_lds_bytes(i64 D, int nct) { return (size_t)2 * 32 * nct * (D + 8) * 2 + (size_t)32 * nct * 4; }
@@ -1194,7 +1205,11 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
   float cnr[NCT];  // |c|^2 of this lane's centre in every tile
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct) cnr[ct] = cns[ct * 32 + r];
-  const double cmax = *cmax_p;
+  const double cmax = cmax_p[0];
+  // fp32 target: two exact distances whose squares differ by more than
+  // 2^-21 (|p| + |c|)^2 are more than 2 fp32 ulps apart, so they cannot
+  // round to one value; the margin is folded into e (gap > 2e + margin)
+  const double mcoef = cmax_p[1];
   const double u32 = 5.9604644775390625e-08;
   const int KS = (int)D / 16;
   // chain length of one accumulator: 48 KB_GRP products then KS / KB_GRP
@@ -1358,7 +1373,7 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
     const double amax = cmax * cmax + 2.0 * pn * cmax;
     const double e = 2.0 * eS * pn + 2.02 * u32 * (cmax * cmax + pn * cmax) +
                      1e-28 * (double)D * (1.0 + cmax) * (1.0 + cmax) + 1e-8 * (pp2 + cmax * cmax) +
-                     8.0 * 1.1920928955078125e-07 * amax + 1e-300;
+                     8.0 * 1.1920928955078125e-07 * amax + 0.5 * mcoef * (pn + cmax) * (pn + cmax) + 1e-300;
     const bool live = gslot < nslots && (r & 1) == 0;
     // finite point, no overflow possible in S or a' (every a' then finite)
     const bool fin = isfinite(p2f) && isfinite(e) && pn * cmax < 1e36 && cmax * cmax < 1e36 &&
@@ -1551,7 +1566,11 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
     for (int i = t; i < NC; i += KS_WAVES * 64) cns[i] = cnf[i];
   }
   __syncthreads();
-  const double cmax = *cmax_p;
+  const double cmax = cmax_p[0];
+  // fp32 target: two exact distances whose squares differ by more than
+  // 2^-21 (|p| + |c|)^2 are more than 2 fp32 ulps apart, so they cannot
+  // round to one value; the margin is folded into e (gap > 2e + margin)
+  const double mcoef = cmax_p[1];
   const double u32 = 5.9604644775390625e-08;
   // each accumulator chain: 48 products per k-step over KS / 2 k-steps, then
   // one add of the two chains
@@ -1669,7 +1688,7 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
     const double amax = cmax * cmax + 2.0 * pn * cmax;
     const double e = 2.0 * eS * pn + 2.02 * u32 * (cmax * cmax + pn * cmax) +
                      1e-28 * (double)D * (1.0 + cmax) * (1.0 + cmax) + 1e-8 * (pp2 + cmax * cmax) +
-                     8.0 * 1.1920928955078125e-07 * amax + 1e-300;
+                     8.0 * 1.1920928955078125e-07 * amax + 0.5 * mcoef * (pn + cmax) * (pn + cmax) + 1e-300;
     const bool live = grow < N && (r & 1) == 0;
     const bool fin = isfinite(p2f) && isfinite(e) && pn * cmax < 1e36 && cmax * cmax < 1e36 &&
                      isfinite(b1) && isfinite(b2);
@@ -1754,7 +1773,7 @@ template <typename TP, bool NATURAL>
 __global__ __launch_bounds__(256) void k_kmeans_cand(i64 D, const TP* __restrict__ P, i64 ldp,
                                                      const double* __restrict__ C, i64* __restrict__ labels,
                                                      const unsigned int* __restrict__ counters,
-                                                     const KfCand* __restrict__ cand_list) {
+                                                     const KfCand* __restrict__ cand_list, int r32) {
   const i64 n = counters[1];
   const int sub = threadIdx.x % KC_LPP;
   const i64 step = ((i64)gridDim.x * 256) / KC_LPP;
@@ -1813,7 +1832,8 @@ __global__ __launch_bounds__(256) void k_kmeans_cand(i64 D, const TP* __restrict
         const double sq = df * df;
         acc = acc + sq;
       }
-      const double dist = sqrt(acc);
+      double dist = sqrt(acc);
+      if (r32) dist = (double)(float)dist;  // fp32-rounded distances: equal values tie, first index wins
       if (c >= 0 && (bi < 0 || dist < best || (dist == best && c < bi))) {
         best = dist;
         bi = c;
@@ -1836,7 +1856,7 @@ __global__ __launch_bounds__(256) void k_kmeans_cand(i64 D, const TP* __restrict
 // fp64 (+inf for padding), *cmax = max_c |C[c]| (one block).
 __global__ __launch_bounds__(256) void k_kmeans_prep(i64 D, i64 K, i64 Kp, const double* __restrict__ C,
                                                      float* __restrict__ CT, double* __restrict__ cn,
-                                                     double* __restrict__ cmax) {
+                                                     double* __restrict__ cmax, double mcoef) {
   __shared__ double red[256];
   double mx = 0.0;
   for (i64 c = threadIdx.x; c < Kp; c += 256) {
@@ -1858,7 +1878,10 @@ __global__ __launch_bounds__(256) void k_kmeans_prep(i64 D, i64 K, i64 Kp, const
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) *cmax = sqrt(red[0]) * 1.001;
+  if (threadIdx.x == 0) {
+    cmax[0] = sqrt(red[0]) * 1.001;
+    cmax[1] = mcoef;
+  }
 }
 
 // Accumulation: sums[c][:] += P[p][:] and counts[c] += 1 for labels[p] == c,
@@ -2057,20 +2080,24 @@ extern "C" int64_t spx_kmeans_assign_workspace(int dtype, int64_t N, int64_t D, 
 
 extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
                                  const double* centers, int64_t* labels, double* mindist, void* workspace,
-                                 size_t workspace_bytes, void* stream) {
+                                 size_t workspace_bytes, int dist_dtype, void* stream) {
   if (dtype != SPX_F32 && dtype != SPX_F64) return set_err(SPX_ENOTSUP, "spx_kmeans_assign: points must be F32/F64");
   if (N < 0 || D < 1 || K < 1 || (N > 0 && ldp < D)) return set_err(SPX_EINVAL, "spx_kmeans_assign: bad N/D/K/ldp");
+  if (dist_dtype != SPX_F64 && dist_dtype != SPX_F32)
+    return set_err(SPX_EINVAL, "spx_kmeans_assign: dist_dtype must be F64 or F32");
   if (N == 0) return SPX_OK;
   if (!points || !centers || !labels) return set_err(SPX_EINVAL, "spx_kmeans_assign: null pointer");
+  const int r32 = dist_dtype == SPX_F32;
+  const double mcoef = r32 ? 4.76837158203125e-07 : 0.0;  // 2^-21
   const i64 g = (N + 255) / 256;
   if (g > 0x7fffffffLL) return set_err(SPX_EINVAL, "spx_kmeans_assign: too many points");
   if (mindist || !workspace) {  // all points through the exact-order kernel
     if (dtype == SPX_F32)
       k_kmeans_assign<float><<<(unsigned)g, 256, 0, S(stream)>>>(N, D, K, (const float*)points, ldp, centers, labels,
-                                                                  mindist, nullptr, nullptr);
+                                                                  mindist, nullptr, nullptr, r32);
     else
       k_kmeans_assign<double><<<(unsigned)g, 256, 0, S(stream)>>>(N, D, K, (const double*)points, ldp, centers,
-                                                                   labels, mindist, nullptr, nullptr);
+                                                                   labels, mindist, nullptr, nullptr, r32);
     LAUNCH_CHECK("spx_kmeans_assign");
     return SPX_OK;
   }
@@ -2101,7 +2128,7 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
     __bf16* CBh = (__bf16*)CT;
     __bf16* CBl = CBh + (i64)32 * nct * D;
     float* cnf = (float*)cn;
-    k_kmeans_prep_b3<<<1, 256, 0, S(stream)>>>(D, K, 32 * nct, centers, CBh, CBl, cnf, cmax);
+    k_kmeans_prep_b3<<<1, 256, 0, S(stream)>>>(D, K, 32 * nct, centers, CBh, CBl, cnf, cmax, mcoef);
     LAUNCH_CHECK("spx_kmeans_assign(prep)");
     static int ncu = 0;
     if (!ncu) {
@@ -2143,14 +2170,14 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
       }
       LAUNCH_CHECK("spx_kmeans_assign(filter bf16x3)");
     }
-    k_kmeans_cand<float, true><<<gp, 256, 0, S(stream)>>>(D, Pf, ldp, centers, labels, counters, cand_list);
+    k_kmeans_cand<float, true><<<gp, 256, 0, S(stream)>>>(D, Pf, ldp, centers, labels, counters, cand_list, r32);
     LAUNCH_CHECK("spx_kmeans_assign(candidates)");
     k_kmeans_assign<float><<<gp, 256, 0, S(stream)>>>(N, D, K, Pf, ldp, centers, labels, nullptr, full_list,
-                                                       counters);
+                                                       counters, r32);
     LAUNCH_CHECK("spx_kmeans_assign(exact)");
     return SPX_OK;
   }
-  k_kmeans_prep<<<1, 256, 0, S(stream)>>>(D, K, Kp, centers, CT, cn, cmax);
+  k_kmeans_prep<<<1, 256, 0, S(stream)>>>(D, K, Kp, centers, CT, cn, cmax, mcoef);
   LAUNCH_CHECK("spx_kmeans_assign(prep)");
   const i64 gf = (N + KfProd::BM - 1) / KfProd::BM;
   const bool al = D % KF_BK == 0 && ldp % 4 == 0 && ((uintptr_t)points % 16) == 0;
@@ -2167,18 +2194,18 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
   if (Kp == KF_BN) {
     if (dtype == SPX_F32)
       k_kmeans_cand<float, false><<<gp, 256, 0, S(stream)>>>(D, (const float*)points, ldp, centers, labels, counters,
-                                                       cand_list);
+                                                       cand_list, r32);
     else
       k_kmeans_cand<double, false><<<gp, 256, 0, S(stream)>>>(D, (const double*)points, ldp, centers, labels, counters,
-                                                        cand_list);
+                                                        cand_list, r32);
     LAUNCH_CHECK("spx_kmeans_assign(candidates)");
   }
   if (dtype == SPX_F32)
     k_kmeans_assign<float><<<gp, 256, 0, S(stream)>>>(N, D, K, (const float*)points, ldp, centers, labels, nullptr,
-                                                       full_list, counters);
+                                                       full_list, counters, r32);
   else
     k_kmeans_assign<double><<<gp, 256, 0, S(stream)>>>(N, D, K, (const double*)points, ldp, centers, labels,
-                                                        nullptr, full_list, counters);
+                                                        nullptr, full_list, counters, r32);
   LAUNCH_CHECK("spx_kmeans_assign(exact)");
   return SPX_OK;
 }

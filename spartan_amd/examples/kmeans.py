@@ -9,9 +9,10 @@ are registered joins (expr/join.py), so each runs as device work:
   kmeans_dist_mapper    outer((X, C), (0, 0))  -> spx_cdist: exact-order fp64
                         distances (N, K), rounded to the target dtype;
   argmin(outer(...), axis=1)                   -> fused by OuterArgminFusion
-                        (expr/optimize.py) into spx_kmeans_assign when the
-                        distances are fp64: certified bf16x3-MFMA filter +
-                        exact recompute, no (N, K) matrix (204.8 GB at cfg3);
+                        (expr/optimize.py) into spx_kmeans_assign for fp64
+                        or fp32 distances (the argmin of the values rounded to
+                        the target dtype): certified bf16x3-MFMA filter +
+                        exact recompute, no (N, K) matrix (102-205 GB at cfg3);
   kmeans_count_mapper   map2(labels, 0)        -> spx_bincount per label tile
                         + RCCL all-reduce;
   kmeans_center_mapper  map2((X, labels), (0, 0)) -> spx_kmeans_accumulate
@@ -151,10 +152,12 @@ def _center_join(kind, arrays, axes, fn_kw, target):
   _deliver_full(target, sums)
 
 
-def _assign_fused(arrays, fn_kw, target):
-  """argmin(outer((X, C), (0, 0), kmeans_dist_mapper), axis=1) for fp64
-  distances: spx_kmeans_assign per X row block (labels bit-exact with the
-  argmin of the materialised cdist, first index on ties, first NaN wins)."""
+def _assign_fused(arrays, fn_kw, target, dist_dtype):
+  """argmin(outer((X, C), (0, 0), kmeans_dist_mapper), axis=1): the outer's
+  target holds the cdist values rounded to its dtype (fp64, or fp32 for fp32
+  points: map2 / outer dtype None -> arrays[0].dtype); spx_kmeans_assign per
+  X row block gives the argmin of exactly those values (first index on
+  ties, first NaN wins) without materialising them."""
   import torch
   from ..expr.join import _scatter_updates
   X, C = arrays
@@ -172,13 +175,13 @@ def _assign_fused(arrays, fn_kw, target):
       if pts.stride(-1) != 1:
         pts = be.contiguous(pts)
       lab = torch.empty((tex.shape[0],), dtype=torch.int64, device=ctx.device)
-      be.kmeans_assign(pts, c, lab)
+      be.kmeans_assign(pts, c, lab, dist_dtype=dist_dtype)
     updates.append((qi, tex, src, lab))
   _scatter_updates(target, updates)
 
 
 register_join(kmeans_dist_mapper, _dist_join)
-register_argmin_fusion(kmeans_dist_mapper, _assign_fused)
+register_argmin_fusion(kmeans_dist_mapper, _assign_fused, dtypes=(np.float64, np.float32))
 register_join(kmeans_count_mapper, _count_join)
 register_join(kmeans_center_mapper, _center_join)
 

@@ -23,6 +23,10 @@ from ..util import log
 _ids = itertools.count()
 
 
+def _new_id():
+  return next(_ids)
+
+
 class newaxis(object):
   """Marks a new unit dimension in ``x[...]`` (reference base.py:23-26;
   NumPy's ``None`` / ``np.newaxis`` is accepted too)."""

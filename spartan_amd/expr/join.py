@@ -72,9 +72,10 @@ _ARGMIN_FUSIONS = {}
 
 def register_argmin_fusion(fn, impl, dtypes=(np.float64,)):
   """``argmin(outer(arrays, (0, 0), fn), axis=1)`` may run as
-  ``impl(arrays, fn_kw, labels_target)`` without materialising the outer
-  product, when the outer's result dtype is one of ``dtypes`` (the fused
-  kernel must give the argmin of exactly those values)."""
+  ``impl(arrays, fn_kw, labels_target, dist_dtype)`` without materialising
+  the outer product, when the outer's result dtype is one of ``dtypes`` (the
+  fused kernel must give the argmin of exactly those values, i.e. of the
+  mapper's values rounded to ``dist_dtype``)."""
   _ARGMIN_FUSIONS[fn] = (impl, tuple(np.dtype(d) for d in dtypes))
 
 
@@ -103,7 +104,7 @@ class ArgminJoinExpr(Expr):
   def _evaluate(self, deps):
     arrays = [distarray.as_array(a) for a in deps['arrays']]
     target = distarray.create(self.compute_shape(), np.int64, reducer=np.minimum, tile_hint=self.tile_hint)
-    self.impl(arrays, dict(self.outer.fn_kw or {}), target)
+    self.impl(arrays, dict(self.outer.fn_kw or {}), target, self.outer.compute_dtype())
     return target
 
 

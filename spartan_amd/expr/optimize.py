@@ -519,10 +519,17 @@ PASSES = [CollapsedCachedExpressions, AutomaticTiling, MapMapFusion, ReduceMapFu
           OuterArgminFusion]
 
 
-def optimize(dag):
-  if not FLAGS.optimization:
-    return dag
+def _run_passes(dag):
   for p in PASSES:
     if getattr(FLAGS, 'opt_' + p.name):
       dag = p().visit(dag)
   return dag
+
+
+def optimize(dag):
+  if not FLAGS.optimization:
+    return dag
+  if FLAGS.opt_plan_cache:
+    from . import plan_cache
+    return plan_cache.optimize_cached(dag, _run_passes)
+  return _run_passes(dag)

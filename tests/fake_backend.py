@@ -184,9 +184,9 @@ class FakeBackend:
       r = r + beta * _np(C)
     C.copy_(torch.as_tensor(np.ascontiguousarray(r.astype(_np(C).dtype))))
 
-  def kmeans_assign(self, points, centers, labels, mindist=None, exact_only=False):
+  def kmeans_assign(self, points, centers, labels, mindist=None, exact_only=False, dist_dtype=np.float64):
     from scipy.spatial.distance import cdist
-    d = cdist(_np(points).astype(np.float64), _np(centers))
+    d = cdist(_np(points).astype(np.float64), _np(centers)).astype(dist_dtype)
     labels.copy_(torch.as_tensor(d.argmin(1).astype(np.int64)))
 
   def cdist(self, points, centers, out):

@@ -15,6 +15,8 @@ import numpy as np  # noqa: E402
 
 
 def main():
+  import faulthandler
+  faulthandler.dump_traceback_later(150, exit=True)  # a hang names its stack instead of timing out silently
   import spartan_amd
   from spartan_amd import expr
   from spartan_amd.config import FLAGS

@@ -594,29 +594,39 @@ def _assign_case(kind, dt):
   elif kind == 'nonfinite':
     C = g.random((30, 16)); pts = g.random((3000, 16)).astype(dt)
     pts[5, 3] = np.nan; pts[9, 0] = np.inf; pts[13, :] = -np.inf
+  elif kind == 'ties32':                    # centres 1e-9 apart: distinct in fp64, equal once rounded to fp32
+    C = g.random((256, 128)); C[200] = C[7]; C[200, 5] += 1e-9; C[31] = C[250]; C[250, 0] -= 1e-9
+    pts = g.random((40000, 128)).astype(dt)
+    pts[::5] = (C[7] + 0.01 * g.standard_normal((len(pts[::5]), 128))).astype(dt)
+    pts[1::5] = (C[250] + 0.01 * g.standard_normal((len(pts[1::5]), 128))).astype(dt)
   return np.ascontiguousarray(pts), np.ascontiguousarray(C)
 
 
+@pytest.mark.parametrize('ddt', [np.float64, np.float32])
 @pytest.mark.parametrize('dt', [np.float32, np.float64])
-@pytest.mark.parametrize('kind', ['uniform', 'ties', 'offset', 'clusters', 'k1', 'nonfinite'])
-def test_kmeans_assign_certified_bit_exact(ex, kind, dt):
+@pytest.mark.parametrize('kind', ['uniform', 'ties', 'offset', 'clusters', 'k1', 'nonfinite', 'ties32'])
+def test_kmeans_assign_certified_bit_exact(ex, kind, dt, ddt):
   """The MFMA-certified fast path must give argmin(scipy cdist) bit for bit
   (first index on ties, NaN rows -> first NaN = 0), identical to the
-  all-exact kernel."""
+  all-exact kernel; with ddt float32 the argmin of the distances rounded to
+  fp32 (an fp32 outer-product target), whose ties the rounding creates."""
   import torch
-  from oracle import workloads as OW
+  from scipy.spatial.distance import cdist
   from spartan_amd import backend
   be = backend.get()
   pts, C = _assign_case(kind, dt)
-  want = OW.kmeans_assign(pts, C)
+  want = cdist(pts.astype(np.float64), C).astype(ddt).argmin(1)
   P = torch.as_tensor(pts).cuda()
   Cd = torch.as_tensor(C).cuda()
   fast = torch.empty(len(pts), dtype=torch.int64, device='cuda')
   slow = torch.empty_like(fast)
-  be.kmeans_assign(P, Cd, fast)
-  be.kmeans_assign(P, Cd, slow, exact_only=True)
+  be.kmeans_assign(P, Cd, fast, dist_dtype=ddt)
+  be.kmeans_assign(P, Cd, slow, exact_only=True, dist_dtype=ddt)
   np.testing.assert_array_equal(slow.cpu().numpy(), want)
   np.testing.assert_array_equal(fast.cpu().numpy(), want)
+  if kind == 'ties32':  # the case is only a test if the two orders differ
+    want64 = cdist(pts.astype(np.float64), C).argmin(1)
+    assert (want64 != cdist(pts.astype(np.float64), C).astype(np.float32).argmin(1)).any()
 
 
 @pytest.mark.parametrize('D', [64, 128])

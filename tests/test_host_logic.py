@@ -265,3 +265,74 @@ def test_expr_method_surface(host_ctx):
   assert x[expr.newaxis, :, 1:3].shape == (1, 6, 2)
   assert x[:, None].shape == (6, 1, 4)
   assert x[2, None].shape == (1, 4)
+
+
+def test_plan_cache_replays_structures(host_ctx):
+  """expr/plan_cache.py: the second optimisation of an identical structure
+  is a replay (no passes) with the new host values substituted, and gives
+  the same results as a fresh optimisation; a different structure or
+  different flags misses."""
+  host_ctx(3)
+  from spartan_amd import expr, workloads
+  from spartan_amd.config import FLAGS
+  from spartan_amd.expr import plan_cache
+  from oracle import rng
+  from oracle import workloads as OW
+  Xn = rng.rand((300, 16), 41, np.float32)
+  Yn = rng.rand((300, 1), 42, np.float32)
+  w0 = rng.rand((16, 1), 43, np.float32)
+  X, Y = expr.lazify(expr.from_numpy(Xn).force()), expr.lazify(expr.from_numpy(Yn).force())
+  plan_cache.clear()
+  h0 = plan_cache.STATS['hits']
+  w_cached = workloads.sgd_train(X, Y, w0, 1e-3, 6)
+  assert plan_cache.STATS['hits'] - h0 >= 5
+  FLAGS.opt_plan_cache = False
+  try:
+    w_plain = workloads.sgd_train(X, Y, w0, 1e-3, 6)
+  finally:
+    FLAGS.opt_plan_cache = True
+  np.testing.assert_array_equal(w_cached, w_plain)
+  w = w0
+  for _ in range(6):
+    w = OW.linear_regression_update(Xn, Yn, w, 1e-3, 3)
+  np.testing.assert_allclose(w_cached, w, rtol=1e-5)
+  # same structure over other arrays / values: results follow the new leaves
+  Zn = rng.rand((300, 16), 44, np.float32)
+  Z = expr.lazify(expr.from_numpy(Zn).force())
+  for a, an in ((X, Xn), (Z, Zn), (X, Xn)):
+    for v in (w0, w0 * 2):
+      got = expr.sum(a * (expr.dot(a, v) - Y), axis=0).optimized().glom()
+      want = (an * (an @ v - Yn)).sum(0)
+      np.testing.assert_allclose(got, want, rtol=1e-5)
+  # a different reduction axis is a different structure
+  m0 = plan_cache.STATS['misses']
+  expr.sum(X * 2.0, axis=1).optimized().glom()
+  expr.sum(X * 2.0, axis=0).optimized().glom()
+  assert plan_cache.STATS['misses'] == m0 + 2
+  np.testing.assert_allclose(expr.sum(X * 3.0, axis=0).optimized().glom(), (Xn * 3.0).sum(0), rtol=1e-5)
+
+
+def test_plan_cache_keeps_shared_node_ids(host_ctx):
+  """The reference's KMeans loop forces ``labels`` through ``counts`` and
+  reuses the cached value for the centres (k_means_.py:129-136): with the
+  plan cache replaying later iterations, the assignment still runs once per
+  iteration (replayed nodes keep the ids of the nodes they stand for)."""
+  host_ctx(1)
+  from spartan_amd import backend, expr
+  from spartan_amd.examples.kmeans import KMeans
+  from spartan_amd.expr import plan_cache
+  from oracle import rng
+  pts = rng.rand((400, 8), 21, np.float32)
+  X = expr.from_numpy(pts).force()
+  be = backend.get()
+  calls = []
+  orig = be.kmeans_assign  # fp32 points: argmin(outer) fused with fp32-rounded distances
+  be.kmeans_assign = lambda *a, **k: (calls.append(k.get('dist_dtype')), orig(*a, **k))[1]
+  try:
+    plan_cache.clear()
+    h0 = plan_cache.STATS['hits']
+    KMeans(5, 4).fit(X, pts[:5].astype(np.float64))
+  finally:
+    be.kmeans_assign = orig
+  assert plan_cache.STATS['hits'] > h0
+  assert calls == [np.float32] * 4
