@@ -587,7 +587,7 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
   act = ctype(adt)
   arg = op in ('argmin', 'argmax')
   L = [PRELUDE, _ocml_decls(ocml), fn, _comb_fns(op, adt)]
-  if rds:
+  if rds or kind == 'rows':
     L.append(SHFL)
     L.append(ROW_ALLSUM)
 
@@ -649,25 +649,38 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
         L.append('  if (better(acc%d, acci%d, accv, acci)) { accv = acc%d; acci = acci%d; }' % (j, j, j, j))
       else:
         L.append('  accv = comb(accv, acc%d);' % j)
-    L.append('  SHARED %s sv[256];' % act)
-    if arg:
-      L.append('  SHARED i64 si[256];')
+    # wave level first: DPP within each 16-lane row (quad_perm [1,0,3,2],
+    # [2,3,0,1], row_half_mirror, row_mirror -- each lane meets a partner
+    # holding its mirror group's partial, and comb / better are symmetric, so
+    # every lane ends with the wave's value), ds_bpermute across rows; then
+    # the 4 wave results through LDS with one barrier (was an 8-barrier tree)
     L.append('  const u32 t = tid();')
-    L.append('  sv[t] = accv;' + (' si[t] = acci;' if arg else ''))
+    steps = ['dpp_mov<0xB1>(%s)', 'dpp_mov<0x4E>(%s)', 'dpp_mov<0x141>(%s)', 'dpp_mov<0x140>(%s)',
+             'shfl_xor(%s, 16)', 'shfl_xor(%s, 32)']
+    for st in steps:
+      if arg:
+        L.append('  { %s ov = %s; i64 oi = %s;' % (act, st % 'accv', st % 'acci'))
+        L.append('    if (better(ov, oi, accv, acci)) { accv = ov; acci = oi; } }')
+      else:
+        L.append('  accv = comb(accv, %s);' % (st % 'accv'))
+    L.append('  SHARED %s sv[4];' % act)
+    if arg:
+      L.append('  SHARED i64 si[4];')
+    L.append('  if ((t & 63) == 0) { sv[t >> 6] = accv;' + (' si[t >> 6] = acci;' if arg else '') + ' }')
     L.append('  bsync();')
-    L.append('  for (u32 s = 128; s > 0; s >>= 1) {')
-    L.append('    if (t < s) {')
-    if arg:
-      L.append('      if (better(sv[t + s], si[t + s], sv[t], si[t])) { sv[t] = sv[t + s]; si[t] = si[t + s]; }')
-    else:
-      L.append('      sv[t] = comb(sv[t], sv[t + s]);')
-    L.append('    }')
-    L.append('    bsync();')
-    L.append('  }')
     L.append('  if (t == 0) {')
-    L.append('    ((GLOBAL %s*)a.out0)[p * O + o] = sv[0];' % act)
+    L.append('    %s v = sv[0];' % act)
     if arg:
-      L.append('    ((GLOBAL i64*)a.out1)[p * O + o] = si[0];')
+      L.append('    i64 vi = si[0];')
+    L.append('    for (int k = 1; k < 4; ++k) {')
+    if arg:
+      L.append('      if (better(sv[k], si[k], v, vi)) { v = sv[k]; vi = si[k]; }')
+    else:
+      L.append('      v = comb(v, sv[k]);')
+    L.append('    }')
+    L.append('    ((GLOBAL %s*)a.out0)[p * O + o] = v;' % act)
+    if arg:
+      L.append('    ((GLOBAL i64*)a.out1)[p * O + o] = vi;')
     L.append('  }')
     L.append('}')
   elif kind == 'rowsp':
