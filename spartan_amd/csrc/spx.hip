@@ -1063,28 +1063,45 @@ typedef __bf16 kb_bf8 __attribute__((ext_vector_type(8)));
 typedef float kb_acc __attribute__((ext_vector_type(16)));
 typedef float kb_f4 __attribute__((ext_vector_type(4)));
 
-// CBh / CBl[c][d]: bf16 split of (float)C[c][d] (zero past K); cnf[c] =
-// (float)|C[c]|^2 (+inf past K); *cmax = max_c |C[c]| (one block).
+// Centred centres for the bf16x3 filters.  mu = fp32 mean of the centres;
+// c' = C[c] - mu.  For every point x
+//   |x - C[c]|^2 = |x - mu|^2 + (|c'|^2 + 2 mu.c' - 2 x.c'),
+// and the first term does not depend on c, so the filters rank the centres
+// by a'(x, c) = cc[c] - 2 x.c' with cc[c] = |c'|^2 + 2 mu.c'.  The bf16x3
+// error of x.c' scales with |x| |c'| instead of |x| |c|: for points far from
+// the origin (U[0,1)^128: |c| ~ 6.5, |c'| ~ 1.5-3.7) the certified bound e
+// shrinks 2-4x and so does the share of undecided rows the exact path has to
+// recompute (cfg3: 1.0 / 3.1 % -> 0.5 / 0.8 %).
+// CBh / CBl[c][d]: bf16 split of (float)c'[d] (zero past K); cnf[c] =
+// (float)cc[c] (huge past K); cmax[0] = max_c |c'|, cmax[2] = |mu| (one block).
 __global__ __launch_bounds__(256) void k_kmeans_prep_b3(i64 D, i64 K, i64 Kp, const double* __restrict__ C,
                                                         __bf16* __restrict__ CBh, __bf16* __restrict__ CBl,
                                                         float* __restrict__ cnf, double* __restrict__ cmax,
                                                         double mcoef) {
   __shared__ double red[256];
+  __shared__ float mus[KB_DMAX];
+  for (i64 d = threadIdx.x; d < D; d += 256) {
+    double m = 0.0;
+    for (i64 c = 0; c < K; ++c) m += C[c * D + d];
+    mus[d] = (float)(m / (double)K);
+  }
+  __syncthreads();
   double mx = 0.0;
   for (i64 c = threadIdx.x; c < Kp; c += 256) {
-    double s = 0.0;
+    double s = 0.0, sm = 0.0;
     for (i64 d = 0; d < D; ++d) {
-      const double v = c < K ? C[c * D + d] : 0.0;
+      const double v = c < K ? C[c * D + d] - (double)mus[d] : 0.0;
       const float v32 = (float)v;
       const __bf16 hi = (__bf16)v32;
       CBh[c * D + d] = hi;
       CBl[c * D + d] = (__bf16)(v32 - (float)hi);
       s += v * v;
+      sm += (double)mus[d] * v;
     }
-    // padding centres: a huge FINITE |c|^2 (the filter tags a' mantissa bits,
+    // padding centres: a huge FINITE cc (the filter tags a' mantissa bits,
     // which would turn +inf into NaN); they never win, and a lone real centre
     // is certified against them
-    cnf[c] = c < K ? (float)s : 3.0e38f;
+    cnf[c] = c < K ? (float)(s + 2.0 * sm) : 3.0e38f;
     if (c < K) mx = (s > mx || s != s) ? s : mx;
   }
   red[threadIdx.x] = mx;
@@ -1097,9 +1114,28 @@ __global__ __launch_bounds__(256) void k_kmeans_prep_b3(i64 D, i64 K, i64 Kp, co
     __syncthreads();
   }
   if (threadIdx.x == 0) {
+    double mn = 0.0;
+    for (i64 d = 0; d < D; ++d) mn += (double)mus[d] * (double)mus[d];
     cmax[0] = sqrt(red[0]) * 1.001;
     cmax[1] = mcoef;  // fp32 tie margin coefficient (0: fp64 distances), read by the filters
+    cmax[2] = sqrt(mn) * 1.001;
   }
+}
+
+// The certified gap bound e of one point for the bf16x3 filters (a point is
+// labelled iff b2 - b1 > 2e).  eS |p|: the bf16x3 product error of x.c'
+// (split residuals, fp32 accumulation chains); 2.02 u (cmax^2 + 2|mu| cmax +
+// |p| cmax): rounding of c' to fp32 (in x.c' and in |c'|^2) and of cc to
+// fp32; the 1e-28 / 1e-8 terms: bf16 underflow and slack; 8 eps amax: the fp32
+// fma a' = cc - 2S and the 3-bit tile tag; mcoef: the fp32-target tie margin
+// over |x - c| <= |p| + |mu| + cmax.
+__device__ __forceinline__ double kc_bound(double eS, double pn, double cmax, double mun, double pp2, double amax,
+                                           double mcoef, i64 D) {
+  const double u32 = 5.9604644775390625e-08;
+  const double dm = pn + mun + cmax;
+  return 2.0 * eS * pn + 2.02 * u32 * (cmax * cmax + 2.0 * mun * cmax + pn * cmax) +
+         1e-28 * (double)D * (1.0 + cmax) * (1.0 + cmax) + 1e-8 * (pp2 + cmax * cmax + mun * mun) +
+         8.0 * 1.1920928955078125e-07 * amax + 0.5 * mcoef * dm * dm + 1e-300;
 }
 
 static size_t kb_lds_bytes(i64 D, int nct) { return (size_t)2 * 32 * nct * (D + 8) * 2 + (size_t)32 * nct * 4; }
@@ -1209,7 +1245,7 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
   // fp32 target: two exact distances whose squares differ by more than
   // 2^-21 (|p| + |c|)^2 are more than 2 fp32 ulps apart, so they cannot
   // round to one value; the margin is folded into e (gap > 2e + margin)
-  const double mcoef = cmax_p[1];
+  const double mcoef = cmax_p[1], mun = cmax_p[2];
   const double u32 = 5.9604644775390625e-08;
   const int KS = (int)D / 16;
   // chain length of one accumulator: 48 KB_GRP products then KS / KB_GRP
@@ -1368,16 +1404,14 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
     const float p2f = __shfl(p2, rt, 64);
     const double pp2 = (double)p2f * 1.001 + (double)D * 2e-45;
     const double pn = sqrt(pp2) * 1.0001;
-    // a' magnitudes are at most cmax^2 + 2 |p| cmax: the 7-ulp index tag adds
-    // 2 * 8 * 2^-23 of that to the gap test
-    const double amax = cmax * cmax + 2.0 * pn * cmax;
-    const double e = 2.0 * eS * pn + 2.02 * u32 * (cmax * cmax + pn * cmax) +
-                     1e-28 * (double)D * (1.0 + cmax) * (1.0 + cmax) + 1e-8 * (pp2 + cmax * cmax) +
-                     8.0 * 1.1920928955078125e-07 * amax + 0.5 * mcoef * (pn + cmax) * (pn + cmax) + 1e-300;
+    // |a'| <= amax = cmax^2 + 2 |mu| cmax + 2 |p| cmax: the 7-ulp index tag
+    // adds 2 * 8 * 2^-23 of that to the gap test
+    const double amax = cmax * cmax + 2.0 * mun * cmax + 2.0 * pn * cmax;
+    const double e = kc_bound(eS, pn, cmax, mun, pp2, amax, mcoef, D);
     const bool live = gslot < nslots && (r & 1) == 0;
     // finite point, no overflow possible in S or a' (every a' then finite)
     const bool fin = isfinite(p2f) && isfinite(e) && pn * cmax < 1e36 && cmax * cmax < 1e36 &&
-                     isfinite(b1) && isfinite(b2);
+                     mun * cmax < 1e36 && isfinite(b1) && isfinite(b2);
     const bool dec = fin && (double)b2 - (double)b1 > 2.0 * e;
     if (live && dec) labels[grow] = i1;
     if (live && !fin) full_list[atomicAdd(&counters[0], 1u)] = grow;
@@ -1570,7 +1604,7 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
   // fp32 target: two exact distances whose squares differ by more than
   // 2^-21 (|p| + |c|)^2 are more than 2 fp32 ulps apart, so they cannot
   // round to one value; the margin is folded into e (gap > 2e + margin)
-  const double mcoef = cmax_p[1];
+  const double mcoef = cmax_p[1], mun = cmax_p[2];
   const double u32 = 5.9604644775390625e-08;
   // each accumulator chain: 48 products per k-step over KS / 2 k-steps, then
   // one add of the two chains
@@ -1685,13 +1719,11 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
     const float p2f = __shfl(p2, rt, 64);
     const double pp2 = (double)p2f * 1.001 + (double)D * 2e-45;
     const double pn = sqrt(pp2) * 1.0001;
-    const double amax = cmax * cmax + 2.0 * pn * cmax;
-    const double e = 2.0 * eS * pn + 2.02 * u32 * (cmax * cmax + pn * cmax) +
-                     1e-28 * (double)D * (1.0 + cmax) * (1.0 + cmax) + 1e-8 * (pp2 + cmax * cmax) +
-                     8.0 * 1.1920928955078125e-07 * amax + 0.5 * mcoef * (pn + cmax) * (pn + cmax) + 1e-300;
+    const double amax = cmax * cmax + 2.0 * mun * cmax + 2.0 * pn * cmax;
+    const double e = kc_bound(eS, pn, cmax, mun, pp2, amax, mcoef, D);
     const bool live = grow < N && (r & 1) == 0;
     const bool fin = isfinite(p2f) && isfinite(e) && pn * cmax < 1e36 && cmax * cmax < 1e36 &&
-                     isfinite(b1) && isfinite(b2);
+                     mun * cmax < 1e36 && isfinite(b1) && isfinite(b2);
     const bool dec = fin && (double)b2 - (double)b1 > 2.0 * e;
     if (live && dec) labels[grow] = i1;
     if (live && !fin) full_list[atomicAdd(&counters[0], 1u)] = grow;
@@ -1881,6 +1913,7 @@ __global__ __launch_bounds__(256) void k_kmeans_prep(i64 D, i64 K, i64 Kp, const
   if (threadIdx.x == 0) {
     cmax[0] = sqrt(red[0]) * 1.001;
     cmax[1] = mcoef;
+    cmax[2] = 0.0;  // uncentred
   }
 }
 
@@ -2074,7 +2107,7 @@ extern "C" int64_t spx_kmeans_assign_workspace(int dtype, int64_t N, int64_t D, 
   const i64 Kp = kf_kp(K);
   // CT (D x Kp f32) | cn (Kp f64) | cmax | counters | full list (N i64) | candidate list (N KfCand, K <= 256)
   // | undecided-row list (N i64, K <= 256)
-  return (D * Kp * 4 + 15) / 16 * 16 + Kp * 8 + 16 + 16 + N * 8 +
+  return (D * Kp * 4 + 15) / 16 * 16 + Kp * 8 + 32 + 16 + N * 8 +
          (Kp == KF_BN ? N * (i64)sizeof(KfCand) + N * 8 : 0);
 }
 
@@ -2110,8 +2143,8 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
   ws += (D * Kp * 4 + 15) / 16 * 16;
   double* cn = (double*)ws;
   ws += Kp * 8;
-  double* cmax = (double*)ws;
-  ws += 16;
+  double* cmax = (double*)ws;  // [0] max |c'|, [1] fp32 tie margin coefficient, [2] |mu|
+  ws += 32;
   unsigned int* counters = (unsigned int*)ws;
   ws += 16;
   i64* full_list = (i64*)ws;

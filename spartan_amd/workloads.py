@@ -8,10 +8,11 @@ linear_regression_update -- LinearRegression.update
       diff = x * (yp - y)
       grad = sum(diff, axis=0).optimized().glom().reshape((d, 1))
       w    = w - grad * alpha          # host update
-  Here ``dot(x, w)`` is a skinny GEMV (generated multiply + packed row-sum) and
-  ReduceMapFusion fuses ``x * (yp - y)`` into the axis-0 reduction: one
-  generated kernel reading x once more.  Across GPUs the (d,) partials are
-  combined with one RCCL all-reduce.
+  Here ReduceMapFusion fuses ``x * (yp - y)`` into the axis-0 reduction and
+  DotReduceFusion folds ``dot(x, w)`` into the same kernel as a per-row dot
+  product (``rowdot``), so one generated kernel reads x and y once; the
+  optimised plan is replayed across iterations (expr/plan_cache.py).  Across
+  GPUs the (d,) partials are combined with one RCCL all-reduce (spx_allreduce).
 """
 import numpy as np
 

@@ -11,6 +11,8 @@ reference CPU result is.
 import os
 import sys
 
+import zlib
+
 import numpy as np
 import pytest
 
@@ -573,7 +575,7 @@ def test_kmeans_accumulate_direct(ex, dt, N, D, K):
 
 
 def _assign_case(kind, dt):
-  g = np.random.default_rng(hash(kind) % 2**32)
+  g = np.random.default_rng(zlib.crc32(kind.encode()))  # hash() of a str varies per process
   if kind == 'uniform':
     pts = g.random((20000, 128)).astype(dt); C = pts[:256].astype(np.float64)
   elif kind == 'ties':                      # duplicate centres + exact midpoints
@@ -662,6 +664,44 @@ def test_kmeans_bf16x3_filter_bit_exact(ex, D, K):
   np.testing.assert_array_equal(f, e)
   ok = np.isfinite(pts).all(1)
   np.testing.assert_array_equal(f[ok][:3000], OW.kmeans_assign(pts[ok][:3000], centers))
+
+
+@pytest.mark.parametrize('mode', ['as', 'b3'])
+@pytest.mark.parametrize('ddt', [np.float64, np.float32])
+@pytest.mark.parametrize('kind', ['offset128', 'means', 'clusters64', 'negative'])
+def test_kmeans_centred_filters_bit_exact(ex, kind, ddt, mode, monkeypatch):
+  """Both bf16x3 filters rank centres by cc - 2 x.c' with c' = c - mean(c)
+  (spx.hip k_kmeans_prep_b3): labels stay bit-identical to argmin(cdist) for
+  data far from the origin (the case centring is for), second-iteration
+  centres (cluster means, the tight-gap case), tight clusters and negative
+  coordinates, in both filter modes and both distance dtypes."""
+  import torch
+  from scipy.spatial.distance import cdist
+  from spartan_amd import backend
+  be = backend.get()
+  g = np.random.default_rng(zlib.crc32(kind.encode()))
+  if kind == 'offset128':
+    pts = (1e3 + g.random((30011, 128))).astype(np.float32)
+    C = pts[:256].astype(np.float64)
+  elif kind == 'means':
+    pts = g.random((30011, 128)).astype(np.float32)
+    C0 = pts[:256].astype(np.float64)
+    lab = cdist(pts.astype(np.float64), C0).argmin(1)
+    C = np.stack([pts[lab == k].astype(np.float64).mean(0) if (lab == k).any() else C0[k] for k in range(256)])
+  elif kind == 'clusters64':
+    ctr = g.random((40, 64)) * 5
+    pts = (ctr[g.integers(0, 40, 20000)] + 1e-2 * g.standard_normal((20000, 64))).astype(np.float32)
+    C = ctr[g.integers(0, 40, 200)] + 1e-2 * g.standard_normal((200, 64))
+  else:
+    pts = (g.standard_normal((20000, 128)) * 3 - 7).astype(np.float32)
+    C = pts[g.choice(20000, 97, replace=False)].astype(np.float64)
+  want = cdist(pts.astype(np.float64), C).astype(ddt).argmin(1)
+  monkeypatch.setenv('SPX_KMEANS_FILTER', 'b3' if mode == 'b3' else '')
+  P = torch.as_tensor(pts).cuda()
+  Cd = torch.as_tensor(np.ascontiguousarray(C)).cuda()
+  fast = torch.empty(len(pts), dtype=torch.int64, device='cuda')
+  be.kmeans_assign(P, Cd, fast, dist_dtype=ddt)
+  np.testing.assert_array_equal(fast.cpu().numpy(), want)
 
 
 # ---------------------------------------------- views: slice / transpose / reshape
