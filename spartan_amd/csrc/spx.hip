@@ -1138,6 +1138,21 @@ __device__ __forceinline__ double kc_bound(double eS, double pn, double cmax, do
          8.0 * 1.1920928955078125e-07 * amax + 0.5 * mcoef * dm * dm + 1e-300;
 }
 
+// kc_bound as e(|p|) = k0 + k1 |p| + k2 |p|^2 (|p|^2 >= pp2), coefficients
+// rounded up to fp32, for a per-row evaluation in fp32.
+__device__ __forceinline__ void kc_coef(double eS, double cmax, double mun, double mcoef, i64 D, float (&k)[3]) {
+  const double u32 = 5.9604644775390625e-08, eps = 1.1920928955078125e-07;
+  const double cm2 = cmax * cmax + 2.0 * mun * cmax, m = mun + cmax;
+  const double k0 = 2.02 * u32 * cm2 + 1e-28 * (double)D * (1.0 + cmax) * (1.0 + cmax) +
+                    1e-8 * (cmax * cmax + mun * mun) + 8.0 * eps * cm2 + 0.5 * mcoef * m * m + 1e-30;
+  const double k1 = 2.0 * eS + 2.02 * u32 * cmax + 16.0 * eps * cmax + mcoef * m;
+  const double k2 = 1e-8 + 0.5 * mcoef;
+  const double up = 1.0 + 2.384185791015625e-07;  // 2^-22: covers the rounding to fp32
+  k[0] = (float)(k0 * up);
+  k[1] = (float)(k1 * up);
+  k[2] = (float)(k2 * up);
+}
+
 static size_t kb_lds_bytes(i64 D, int nct) { return (size_t)2 * 32 * nct * (D + 8) * 2 + (size_t)32 * nct * 4; }
 
 // Step (B) of the bf16x3 filter epilogue, as a function (tools/perm_probe.hip
@@ -1499,6 +1514,9 @@ constexpr int KS_WAVES = KS_WAVES_CFG;
 #ifndef KS_PREFETCH
 #define KS_PREFETCH 0  // 1: next tile's loads in flight during the sweep (+64 registers: spills at 2 waves/SIMD)
 #endif
+#ifndef KS_PIPE
+#define KS_PIPE 0  // 1: tile ct's top-2 fold interleaved with tile ct+1's MFMAs (two accumulator sets)
+#endif
 // LDS row of centre c: [hi: D bf16][lo: D bf16][48-byte pad]; the row stride
 // is 4 D + 48 bytes = 12 (mod 64) banks, so the 16-lane groups of a
 // ds_read_b128 (rows 0-3, 12-15, 20-27 ...) hit 16 distinct 4-bank quads,
@@ -1610,6 +1628,11 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
   // one add of the two chains
   const double chain = KS_CHAINS == 2 ? 48.0 * (double)(KS / 2) + 1.0 : 48.0 * (double)KS;
   const double eS = (u32 + 3.1 * 3.814697265625e-06 + 2.0 * (chain + 3.0) * u32) * 1.01 * cmax;
+  float kq[3];
+  kc_coef(eS, cmax, mun, mcoef, D, kq);
+  // no overflow in S or a' (every a' finite): |p| cmax, cmax^2, |mu| cmax < 1e36
+  const bool cok = cmax * cmax < 1e36 && mun * cmax < 1e36;
+  const float pn_lim = (float)(cmax > 0.0 ? 1e36 / cmax : 1e36);
   const i64 ntiles = (N + 31) / 32;
   const i64 stride = (i64)gridDim.x * KS_WAVES;
   i64 tile = (i64)blockIdx.x * KS_WAVES + w;
@@ -1660,9 +1683,10 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
       sec[q] = INFINITY;
     }
     const unsigned char* rowp = kb_lds + r * RB + 16 * h;
-#pragma unroll 1
-    for (int ct = 0; ct < NCT; ++ct) {  // rolled: bounds the scheduler's window (and the LDS reads it hoists)
-      kb_acc c0 = (kb_acc){}, c1 = (kb_acc){};
+    // one centre tile: 3 KS MFMAs into two chains of KS / 2 k-steps each
+    auto chain = [&](int ct, kb_acc& c0, kb_acc& c1) {
+      c0 = (kb_acc){};
+      c1 = (kb_acc){};
       const unsigned char* rp = rowp + ct * 32 * RB;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -1678,7 +1702,9 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bl, c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ks], bh, c, 0, 0, 0);
       }
-      const float cc = cns[ct * 32 + r];
+    };
+    // fold tile ct's a' = fl(cc - 2S), tagged with ct, into the running top-2
+    auto fold = [&](int ct, const kb_acc& c0, const kb_acc& c1, float cc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const float sq = KS_CHAINS == 2 ? c0[q] + c1[q] : c0[q];
@@ -1690,7 +1716,38 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
         lo[q] = ks_min(lo[q], v);
 #endif
       }
+    };
+#if KS_PIPE
+    // software pipeline: tile ct's fold (VALU) is independent of tile ct+1's
+    // MFMAs, so one wave fills the MFMA gaps with it
+    {
+      kb_acc a0, a1, b0, b1;
+      chain(0, a0, a1);
+      float cca = cns[r];
+      if constexpr (NCT == 1) {
+        fold(0, a0, a1, cca);
+      } else {
+#pragma unroll 1
+        for (int cp = 0; cp < NCT; cp += 2) {
+          chain(cp + 1, b0, b1);
+          const float ccb = cns[(cp + 1) * 32 + r];
+          fold(cp, a0, a1, cca);
+          if (cp + 2 < NCT) {
+            chain(cp + 2, a0, a1);
+            cca = cns[(cp + 2) * 32 + r];
+          }
+          fold(cp + 1, b0, b1, ccb);
+        }
+      }
     }
+#else
+#pragma unroll 1
+    for (int ct = 0; ct < NCT; ++ct) {  // rolled: bounds the scheduler's window (and the LDS reads it hoists)
+      kb_acc c0, c1;
+      chain(ct, c0, c1);
+      fold(ct, c0, c1, cns[ct * 32 + r]);
+    }
+#endif
     float lo0[16];  // this lane's minimum per register (its centre r over all tiles)
 #pragma unroll
     for (int q = 0; q < 16; ++q) lo0[q] = lo[q];
@@ -1717,14 +1774,14 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
     const float b1 = lo[0], b2 = sec[0];
     const int i1 = 32 * (int)(__builtin_bit_cast(unsigned int, b1) & 7u) + rmin;
     const float p2f = __shfl(p2, rt, 64);
-    const double pp2 = (double)p2f * 1.001 + (double)D * 2e-45;
-    const double pn = sqrt(pp2) * 1.0001;
-    const double amax = cmax * cmax + 2.0 * mun * cmax + 2.0 * pn * cmax;
-    const double e = kc_bound(eS, pn, cmax, mun, pp2, amax, mcoef, D);
+    // the bound in fp32 (kc_coef): |p| from the fp32 sum of squares with
+    // slack for its rounding and for underflowed squares, e(|p|) by two fmas,
+    // each rounding priced by the 1.0001 factors
+    const float pn = sqrtf(__builtin_fmaf(p2f, 1.001f, 1e-37f)) * 1.0001f;
+    const float e = __builtin_fmaf(__builtin_fmaf(kq[2], pn, kq[1]), pn, kq[0]) * 1.0001f;
     const bool live = grow < N && (r & 1) == 0;
-    const bool fin = isfinite(p2f) && isfinite(e) && pn * cmax < 1e36 && cmax * cmax < 1e36 &&
-                     mun * cmax < 1e36 && isfinite(b1) && isfinite(b2);
-    const bool dec = fin && (double)b2 - (double)b1 > 2.0 * e;
+    const bool fin = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim && isfinite(b1) && isfinite(b2);
+    const bool dec = fin && b2 - b1 > 2.0f * 1.0001f * e;
     if (live && dec) labels[grow] = i1;
     if (live && !fin) full_list[atomicAdd(&counters[0], 1u)] = grow;
     const bool needc = live && fin && !dec;
@@ -1940,7 +1997,10 @@ __global__ __launch_bounds__(256) void k_kmeans_prep(i64 D, i64 K, i64 Kp, const
 //   k_kmeans_reduce   out[i] (+)= sum over g of part[g][i]: four fixed g
 //                     slices per output, combined in a fixed order.
 constexpr int KA_THREADS = 1024;
-constexpr int KA_DB = 64;                  // columns per tile = lanes per wave
+#ifndef KA_CPL
+#define KA_CPL 2                           // columns per lane: 2 -> every point is visited once per wave at D = 128
+#endif
+constexpr int KA_DB = 64 * KA_CPL;         // columns per tile
 constexpr int KA_WAVES = KA_THREADS / 64;  // centre owners per tile
 constexpr int KA_CPW = 16;                 // centres per wave (register sums)
 constexpr int KA_CB = KA_WAVES * KA_CPW;   // centres per tile
@@ -1948,7 +2008,7 @@ constexpr int KA_CB = KA_WAVES * KA_CPW;   // centres per tile
 #define KA_STAGES 3                        // register prefetch ring depth (chunks per barrier): 3 -> 10.1 ms, 2 -> 10.2, 4 -> 10.7, 1 -> 11.8 at cfg3 (profiles/r01_ka_variants.txt)
 #endif
 #ifndef KA_BPC
-#define KA_BPC 1                           // resident blocks per CU (LDS: 2 KA_STAGES x 16 KiB per block)
+#define KA_BPC 1                          // resident blocks per CU (LDS: 2 KA_STAGES x 16 KiB per block)
 #endif
 
 template <typename TP>
@@ -1960,7 +2020,7 @@ __global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(4 * 
   constexpr int LPR = KA_DB / VE;                         // lanes per row slice
   constexpr int ST = KA_STAGES;
   typedef TP V __attribute__((ext_vector_type(VE)));
-  __shared__ TP xs[2][ST][CH * KA_DB];
+  __shared__ __attribute__((aligned(16))) TP xs[2][ST][CH * KA_DB];
   __shared__ int lab_s[2][ST][CH];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int cb = blockIdx.y / ndb, db = blockIdx.y % ndb;
@@ -1970,9 +2030,13 @@ __global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(4 * 
   const int lp = t / LPR, lc = (t % LPR) * VE;
   // 16-byte loads need the slice inside the row and aligned; else per element
   const bool vec = d0 + lc + VE <= D && (ldp % VE) == 0 && ((uintptr_t)P % 16) == 0;
-  double acc[KA_CPW];
+  static_assert(KA_CPL == 1 || KA_CPL == 2, "one or two columns per lane");
+  typedef TP XV __attribute__((ext_vector_type(2)));
+  // one flat register array per column (a vector-of-pairs array indexed at
+  // run time is not promoted to registers: it went to scratch)
+  double acc0[KA_CPW], acc1[KA_CPW];
 #pragma unroll
-  for (int j = 0; j < KA_CPW; ++j) acc[j] = 0.0;
+  for (int j = 0; j < KA_CPW; ++j) acc0[j] = acc1[j] = 0.0;
   // counts: integer LDS atomics at staging time (order-free, hence exact and
   // deterministic), kept by the db == 0 blocks
   __shared__ unsigned int cnt_s[KA_CB];
@@ -2035,16 +2099,26 @@ __global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(4 * 
         const int p = __ffsll((long long)m) - 1;
         m &= m - 1;
         const int j = __builtin_amdgcn_readlane(jl, p);
-        acc[j] += (double)xs[buf][s][p * KA_DB + lane];
+        if constexpr (KA_CPL == 2) {
+          const XV x = *(const XV*)&xs[buf][s][p * KA_DB + 2 * lane];
+          acc0[j] += (double)x[0];
+          acc1[j] += (double)x[1];
+        } else {
+          acc0[j] += (double)xs[buf][s][p * KA_DB + lane];
+        }
       }
     }
     buf ^= 1;
   }
-  const i64 g = blockIdx.x, d = d0 + lane;
+  const i64 g = blockIdx.x;
 #pragma unroll
   for (int j = 0; j < KA_CPW; ++j) {
     const i64 c = c0 + (i64)j * KA_WAVES + w;
-    if (c < K && d < D) psum[(g * K + c) * D + d] = acc[j];
+#pragma unroll
+    for (int cc = 0; cc < KA_CPL; ++cc) {
+      const i64 d = d0 + KA_CPL * lane + cc;
+      if (c < K && d < D) psum[(g * K + c) * D + d] = cc ? acc1[j] : acc0[j];
+    }
   }
   __syncthreads();
   if (db == 0)
@@ -2077,7 +2151,7 @@ __global__ __launch_bounds__(256) void k_kmeans_reduce(i64 n, i64 G, const T* __
 
 // Grid of the accumulation for (N, D, K): x = G point-chunk streams, y = tiles.
 static void ka_grid(int dtype, i64 N, i64 D, i64 K, i64* G, i64* ndb, i64* ncb) {
-  const i64 ch = dtype == SPX_F32 ? 64 : 32;  // points per chunk (k_kmeans_accum CH)
+  const i64 ch = KA_THREADS * (dtype == SPX_F32 ? 4 : 2) / KA_DB;  // points per chunk (k_kmeans_accum CH)
   *ndb = (D + KA_DB - 1) / KA_DB;
   *ncb = (K + KA_CB - 1) / KA_CB;
   const i64 nch = (N + ch - 1) / ch;
