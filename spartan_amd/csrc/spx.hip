@@ -1508,15 +1508,16 @@ static void kb_launch(hipStream_t s, i64 N, i64 D, const float* P, i64 ldp, cons
 #define KS_WAVES_CFG 8  // waves per block (one block per CU): 8 = two per SIMD (<= 256 registers), 4 = one (<= 512)
 #endif
 #ifndef KS_CHAINS
-#define KS_CHAINS 2  // accumulator chains per centre tile (2: the fresh-accumulator bound, one add per value)
+#define KS_CHAINS 1  // accumulator chains per centre tile (1: one 48 KS-product chain; 2: two chains + one add per value, a tighter bound but 32 more registers)
 #endif
 constexpr int KS_WAVES = KS_WAVES_CFG;
 #ifndef KS_PREFETCH
 #define KS_PREFETCH 0  // 1: next tile's loads in flight during the sweep (+64 registers: spills at 2 waves/SIMD)
 #endif
 #ifndef KS_PIPE
-#define KS_PIPE 0  // 1: tile ct's top-2 fold interleaved with tile ct+1's MFMAs (two accumulator sets)
+#define KS_PIPE 1  // 1: tile ct's top-2 fold interleaved with tile ct+1's MFMAs (two accumulator sets)
 #endif
+
 // LDS row of centre c: [hi: D bf16][lo: D bf16][48-byte pad]; the row stride
 // is 4 D + 48 bytes = 12 (mod 64) banks, so the 16-lane groups of a
 // ds_read_b128 (rows 0-3, 12-15, 20-27 ...) hit 16 distinct 4-bank quads,
@@ -1719,25 +1720,48 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
     };
 #if KS_PIPE
     // software pipeline: tile ct's fold (VALU) is independent of tile ct+1's
-    // MFMAs, so one wave fills the MFMA gaps with it
+    // MFMAs, so each wave fills its own MFMA gaps with it: the fold of the
+    // previous tile is written into the k-loop of the next tile's chain (16 / KS
+    // values per k-step) and the sched barriers keep each region to one chain
+    // + one fold (the scheduler otherwise hoists both tiles' B reads: spills).
+    auto chain_fold = [&](int ct, kb_acc& c0, kb_acc& c1, int pct, const kb_acc& p0, const kb_acc& p1, float pcc) {
+      c0 = (kb_acc){};
+      c1 = (kb_acc){};
+      const unsigned char* rp = rowp + ct * 32 * RB;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const kb_bf8 bh = *(const kb_bf8*)(rp + 32 * ks);
+        const kb_bf8 bl = *(const kb_bf8*)(rp + 2 * D + 32 * ks);
+        kb_acc& c = (KS_CHAINS == 2 && ks >= KS / 2) ? c1 : c0;
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bl, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ks], bh, c, 0, 0, 0);
+#pragma unroll
+        for (int qq = 0; qq < 16 / KS; ++qq) {
+          const int q = ks * (16 / KS) + qq;
+          const float sq = KS_CHAINS == 2 ? p0[q] + p1[q] : p0[q];
+          const float v = ks_tag(__builtin_fmaf(-2.f, sq, pcc), (unsigned int)pct);
+          sec[q] = ks_med3(v, lo[q], sec[q]);
+          lo[q] = ks_min(lo[q], v);
+        }
+      }
+    };
     {
       kb_acc a0, a1, b0, b1;
       chain(0, a0, a1);
-      float cca = cns[r];
       if constexpr (NCT == 1) {
-        fold(0, a0, a1, cca);
+        fold(0, a0, a1, cns[r]);
       } else {
 #pragma unroll 1
-        for (int cp = 0; cp < NCT; cp += 2) {
-          chain(cp + 1, b0, b1);
-          const float ccb = cns[(cp + 1) * 32 + r];
-          fold(cp, a0, a1, cca);
-          if (cp + 2 < NCT) {
-            chain(cp + 2, a0, a1);
-            cca = cns[(cp + 2) * 32 + r];
-          }
-          fold(cp + 1, b0, b1, ccb);
+        for (int cp = 0; cp < NCT - 2; cp += 2) {
+          chain_fold(cp + 1, b0, b1, cp, a0, a1, cns[cp * 32 + r]);
+          __builtin_amdgcn_sched_barrier(0);
+          chain_fold(cp + 2, a0, a1, cp + 1, b0, b1, cns[(cp + 1) * 32 + r]);
+          __builtin_amdgcn_sched_barrier(0);
         }
+        chain_fold(NCT - 1, b0, b1, NCT - 2, a0, a1, cns[(NCT - 2) * 32 + r]);
+        __builtin_amdgcn_sched_barrier(0);
+        fold(NCT - 1, b0, b1, cns[(NCT - 1) * 32 + r]);
       }
     }
 #else
