@@ -326,7 +326,7 @@ def bench_kmeans_api(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
   return out
 
 
-def bench_lreg(npts, ctx, expr, comm, sync, D=64, iters=10):
+def bench_lreg(npts, ctx, expr, comm, sync, D=64, iters=30):
   """configs[4]: linear-regression gradient step X^T(Xw - y) + all-reduce."""
   import torch
   from spartan_amd import workloads

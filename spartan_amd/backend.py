@@ -237,6 +237,9 @@ def compile_code_object(src):
   return img
 
 
+_REPLAY_PLANS = os.environ.get('SPX_REDUCE_PLANS', '1') != '0'  # dev A/B switch
+
+
 class HipBackend:
   """Launches libspx.so / generated kernels on the current HIP stream."""
   name = 'hip'
@@ -250,6 +253,7 @@ class HipBackend:
     self.kernel_events = None  # optional list of (name, start, end) HIP events (bench)
     self._names = {}
     self._sig_fns = {}
+    self._reduce_plans = {}  # backend.reduce launch plans (see reduce)
 
   # ---------------------------------------------------------------- utils
   def stream(self):
@@ -346,6 +350,16 @@ class HipBackend:
     out_shape and out_dtype; for argmin/argmax a (values, int64 indices) pair."""
     import torch
     slots = sorted(inputs)
+    # launch plan of an identical call (same IR signature, operand layouts and
+    # shapes: an iterative driver's replayed DAG): everything below up to the
+    # kernel arguments is a function of this key
+    pkey = (root.sig(), op, tuple((s, inputs[s].dtype, tuple(inputs[s].shape), inputs[s].stride(),
+                                   inputs[s].data_ptr() % 16 == 0) for s in slots),
+            tuple(in_shape), axis, tuple(out_shape), np.dtype(out_dtype).str,
+            None if idx_geom is None else repr(sorted(idx_geom.items())))
+    plan = self._reduce_plans.get(pkey) if _REPLAY_PLANS else None
+    if plan is not None:
+      return self._replay_reduce(plan, root, inputs, slots, out_shape, out_dtype)
     ins = [(s, np_dtype(inputs[s].dtype)) for s in slots]
     strides = [broadcast_strides(tuple(inputs[s].shape), in_shape, inputs[s].stride()) for s in slots]
     view = reduce_view(in_shape, strides, axis)
@@ -487,6 +501,39 @@ class HipBackend:
     if not direct:
       _check(self.lib.spx_reduce_finalize(
           OP_CODE[op], spx_dtype(adt), spx_dtype(np.int64 if arg else out_dtype),
+          ctypes.c_void_p(part_v.data_ptr()), ctypes.c_void_p(part_i.data_ptr() if arg else 0), P, n_out,
+          ctypes.c_void_p(result.data_ptr()), ctypes.c_void_p(res_v.data_ptr() if arg else 0),
+          self.stream()), 'spx_reduce_finalize')
+    if len(self._reduce_plans) >= 512:
+      self._reduce_plans.clear()
+    self._reduce_plans[pkey] = (fn, nblk, bytes(args), arg, direct, adt, P, n_out, dev, OP_CODE[op])
+    return (res_v, result) if arg else result
+
+  def _replay_reduce(self, plan, root, inputs, slots, out_shape, out_dtype):
+    """backend.reduce from a recorded launch plan: the same kernel, grid and
+    argument block, with this call's scalars, pointers and output buffers."""
+    import torch
+    fn, nblk, blob, arg, direct, adt, P, n_out, dev, opc = plan
+    args = codegen.KArgs.from_buffer_copy(blob)
+    _scalars_into(root, args)
+    for s in slots:
+      args.ptr[s] = inputs[s].data_ptr()
+    if arg:
+      res_v = torch.empty(tuple(out_shape), dtype=torch_dtype(adt), device=dev)
+      result = torch.empty(tuple(out_shape), dtype=torch.int64, device=dev)
+      part_v = res_v if direct else torch.empty((P * n_out,), dtype=torch_dtype(adt), device=dev)
+      part_i = result if direct else torch.empty((P * n_out,), dtype=torch.int64, device=dev)
+    else:
+      result = torch.empty(tuple(out_shape), dtype=torch_dtype(out_dtype), device=dev)
+      part_v = result if direct else torch.empty((P * n_out,), dtype=torch_dtype(adt), device=dev)
+      part_i = None
+    args.out0 = part_v.data_ptr()
+    args.out1 = part_i.data_ptr() if arg else 0
+    self.launch(fn, nblk, args)
+    if not direct:
+      _check(self.lib.spx_reduce_finalize(
+          opc, spx_dtype(adt),
+          spx_dtype(np.int64 if arg else out_dtype),
           ctypes.c_void_p(part_v.data_ptr()), ctypes.c_void_p(part_i.data_ptr() if arg else 0), P, n_out,
           ctypes.c_void_p(result.data_ptr()), ctypes.c_void_p(res_v.data_ptr() if arg else 0),
           self.stream()), 'spx_reduce_finalize')

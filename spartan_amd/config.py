@@ -31,11 +31,13 @@ class Flags:
   def __init__(self):
     object.__setattr__(self, '_flags', {})
     object.__setattr__(self, '_vals', {})
+    object.__setattr__(self, 'version', 0)  # bumped on every change (plan-cache keys read it)
 
   def add(self, name, default, typ=None, help=''):
     typ = typ or type(default)
     self._flags[name] = _Flag(name, default, typ, help)
     self._vals.setdefault(name, default)
+    object.__setattr__(self, 'version', self.version + 1)
 
   def __getattr__(self, name):
     vals = object.__getattribute__(self, '_vals')
@@ -47,10 +49,12 @@ class Flags:
     if name not in self._flags:
       raise AttributeError('unknown flag %s' % name)
     self._vals[name] = value
+    object.__setattr__(self, 'version', self.version + 1)
 
   def reset(self):
     for k, f in self._flags.items():
       self._vals[k] = f.default
+    object.__setattr__(self, 'version', self.version + 1)
 
   def parse(self, argv):
     """Consume ``--name=value`` / ``--name value`` tokens for known flags.
@@ -74,6 +78,7 @@ class Flags:
               i += 1
               v = argv[i]
           self._vals[k] = self._flags[k].parse(v)
+          object.__setattr__(self, 'version', self.version + 1)
           i += 1
           continue
       rest.append(tok)

@@ -37,11 +37,38 @@ def _scalar_value(child):
   return None
 
 
+_BIND_MEMO = {}
+
+
 def bind(children, child_to_var, op, extent=None):
   """Lower ``op`` with children bound to IR leaves (``extent``: the tile, for
   trees holding a location map).
 
-  Returns (root, array_slots {slot: child index}, pres [Pre leaves])."""
+  Returns (root, array_slots {slot: child index}, pres [Pre leaves]).
+
+  A LocalExpr tree that a replayed plan shares between iterations
+  (plan_cache marks it ``_tpl_pure``) is lowered once per binding pattern
+  (which children are host scalars, their values, the array dtypes); the
+  entry holds the tree, so its id cannot be reused while the entry lives."""
+  key = None
+  if extent is None and op.__dict__.get('_tpl_pure'):
+    desc = []
+    for child in children:
+      sv = _scalar_value(child)
+      desc.append(('a', child.dtype.str) if sv is None else (type(sv), sv))
+    key = (id(op), tuple(child_to_var), tuple(desc))
+    hit = _BIND_MEMO.get(key)
+    if hit is not None:
+      return hit[1]
+  out = _bind(children, child_to_var, op, extent)
+  if key is not None:
+    if len(_BIND_MEMO) >= 256:
+      _BIND_MEMO.clear()
+    _BIND_MEMO[key] = (op, out)
+  return out
+
+
+def _bind(children, child_to_var, op, extent=None):
   env = LowerEnv({}, extent)
   slots = {}
   for i, (child, var) in enumerate(zip(children, child_to_var)):

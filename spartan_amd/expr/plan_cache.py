@@ -133,11 +133,11 @@ class _Sig:
       cached = self.cache.cache.get(v.expr_id)
       if cached is not None:  # CollapsedCachedExpressions turns it into a Val of this value
         return ('cached', t, self.slot(cached) or self._obj_sig(cached))
-      d = v.__dict__
-      return (t,) + tuple([(a, self.walk(d[a])) for a in sorted(d) if a not in _SKIP])
+      # attributes in insertion order: a node built another way only misses
+      # (the names are part of the key), never collides
+      return (t,) + tuple([(a, self.walk(b)) for a, b in v.__dict__.items() if a not in _SKIP])
     if isinstance(v, self.LocalExpr):
-      d = v.__dict__
-      return (t,) + tuple([(a, self.walk(d[a])) for a in sorted(d)])
+      return (t,) + tuple([(a, self.walk(b)) for a, b in v.__dict__.items()])
     if t is np.ndarray:
       return self.slot(v) or ('np', v.shape, v.dtype.str, v.flags.c_contiguous)
     if isinstance(v, self.DistArray):
@@ -154,6 +154,18 @@ class _Sig:
     raise _Uncacheable(t.__name__)
 
   def _obj_sig(self, v):
+    # an array's layout never changes after it is built: memoised on the object
+    sig = getattr(v, '_plan_sig', None)
+    if sig is not None:
+      return sig
+    sig = self._obj_sig_new(v)
+    try:
+      v._plan_sig = sig
+    except AttributeError:
+      pass
+    return sig
+
+  def _obj_sig_new(self, v):
     from ..array.distarray import DistArrayImpl, LocalWrapper
     if not isinstance(v, (DistArrayImpl, LocalWrapper)):
       if isinstance(v, np.ndarray):
@@ -168,6 +180,17 @@ class _Sig:
             getattr(v, 'replicated', None))
 
 
+_FLAGS_KEY = [None, None]  # (FLAGS.version, key)
+
+
+def _flags_key():
+  if _FLAGS_KEY[0] != FLAGS.version:
+    _FLAGS_KEY[1] = tuple(sorted((k, repr(v)) for k, v in FLAGS.items().items()
+                                 if k.startswith('opt') or k == 'optimization'))
+    _FLAGS_KEY[0] = FLAGS.version
+  return _FLAGS_KEY[1]
+
+
 def signature(dag):
   """(key, walk state: .slots leaf objects, .nodes Expr nodes, .keep) of
   ``dag``, or (None, None) if it has a part the signature does not
@@ -179,8 +202,7 @@ def signature(dag):
   except _Uncacheable:
     return None, None
   ctx = runtime.get() if runtime._ctx is not None else None
-  flags = tuple(sorted((k, repr(v)) for k, v in FLAGS.items().items() if k.startswith('opt') or k == 'optimization'))
-  key = (body, flags, ctx.num_workers if ctx else None, ctx.world_size if ctx else None)
+  key = (body, _flags_key(), ctx.num_workers if ctx else None, ctx.world_size if ctx else None)
   return key, s
 
 
@@ -216,10 +238,30 @@ def _template(v, slot_ids, slots, memo, id2pos=None):
       new.__dict__[a] = _template(b, slot_ids, slots, memo, id2pos)
     if isinstance(v, Expr):
       new.__dict__['_tpl_pos'] = id2pos.get(v.expr_id)
+    elif _pure(new.__dict__):
+      # no slot, view or expression inside: every instantiation shares this
+      # tree object (engine.bind lowers it once per binding pattern)
+      new.__dict__['_tpl_pure'] = True
     return new
   if _is_leaf_obj(v):
     raise _Uncacheable('leaf object outside the input DAG')
   return v
+
+
+def _pure(v):
+  """True iff template value ``v`` holds no slot, view or expression node."""
+  from .base import Expr
+  from .local import LocalExpr
+  t = type(v)
+  if t is _Slot or t is _View or isinstance(v, Expr):
+    return False
+  if t in (list, tuple):
+    return all(_pure(e) for e in v)
+  if t is dict:
+    return all(_pure(e) for e in v.values())
+  if isinstance(v, LocalExpr):
+    return bool(v.__dict__.get('_tpl_pure'))
+  return True
 
 
 def _instantiate(v, slots, nodes):
@@ -247,6 +289,8 @@ class _Inst:
     if t is dict:
       return {a: self.run(b) for a, b in v.items()}
     if isinstance(v, (self.Expr, self.LocalExpr)):
+      if v.__dict__.get('_tpl_pure'):
+        return v
       k = id(v)
       new = self.memo.get(k)
       if new is not None:
