@@ -238,6 +238,15 @@ def compile_code_object(src):
 
 
 _REPLAY_PLANS = os.environ.get('SPX_REDUCE_PLANS', '1') != '0'  # dev A/B switch
+_NCU = []
+ROWS_GRID_PER_CU = 2  # rows reductions: 1.824 ms vs 1.836 uncapped at cfg2 axis 1 (profiles/r02_cfg2_grid.txt)
+
+
+def _num_cus():
+  if not _NCU:
+    import torch
+    _NCU.append(torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count)
+  return _NCU[0]
 
 
 class HipBackend:
@@ -441,6 +450,12 @@ class HipBackend:
       chunk = -(-chunk // per) * per
       P = -(-R // chunk)
       nblk = O * P
+      # grid-stride kernel: at most ROWS_GRID_PER_CU resident blocks per CU
+      # stream the segments (dev knob SPX_ROWS_GRID: blocks per CU, 0 = one
+      # block per segment)
+      gpc = int(os.environ.get('SPX_ROWS_GRID', ROWS_GRID_PER_CU))
+      if gpc > 0:
+        nblk = min(nblk, gpc * _num_cus())
       args.aux[0], args.aux[1] = P, chunk
     else:
       kind = 'cols'
@@ -458,8 +473,14 @@ class HipBackend:
       rows_per_step = 4 * (64 // lpr)
       base = CT * O
       P = 1
-      if base < target_blocks:
-        P = max(1, min(-(-target_blocks // base), -(-R // (rows_per_step * 4))))
+      # wide column reductions (several column tiles) stream best with
+      # exactly two resident blocks per CU (cfg2 axis 0: 512 blocks 1.80 ms,
+      # 1024 1.87, 2048 1.87, 4096 1.90); one narrow column tile (cfg5's 64
+      # columns) with eight (2048: 4.06 ms per lreg iteration, 512: 4.15)
+      # -- tools/cfg2_knobs.py, profiles/r02_cfg2_grid.txt
+      tb = int(os.environ.get('SPX_REDUCE_BLOCKS', 0)) or (2 if CT > 1 else 8) * _num_cus()
+      if base < tb:
+        P = max(1, min(-(-tb // base), -(-R // (rows_per_step * 4))))
       chunk = -(-R // P)
       P = -(-R // chunk)
       nblk = base * P

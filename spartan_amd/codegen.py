@@ -629,7 +629,9 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
 
     L.append('KERN void spx_reduce(KArgs a) {')
     L.append('  const i64 O = a.dim[0], R = a.dim[1], P = a.aux[0], chunk = a.aux[1];')
-    L.append('  const i64 blk = bidx(); const i64 o = blk / P, p = blk - o * P;')
+    # grid-stride over the O * P segments (the launch may cap the grid)
+    L.append('  for (i64 blk = bidx(); blk < O * P; blk += (i64)a.grid) {')
+    L.append('  const i64 o = blk / P, p = blk - o * P;')
     L.append('  const i64 r0 = p * chunk; i64 r1 = r0 + chunk; if (r1 > R) r1 = R;')
     for j in range(vec):
       L.append('  %s acc%d = %s;' % (act, j, _ident(op, adt)))
@@ -681,6 +683,8 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
     L.append('    ((GLOBAL %s*)a.out0)[p * O + o] = v;' % act)
     if arg:
       L.append('    ((GLOBAL i64*)a.out1)[p * O + o] = vi;')
+    L.append('  }')
+    L.append('  bsync();  // sv is rewritten by the next segment')
     L.append('  }')
     L.append('}')
   elif kind == 'rowsp':
