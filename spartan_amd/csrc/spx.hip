@@ -1074,22 +1074,34 @@ typedef float kb_f4 __attribute__((ext_vector_type(4)));
 // recompute (cfg3: 1.0 / 3.1 % -> 0.5 / 0.8 %).
 // CBh / CBl[c][d]: bf16 split of (float)c'[d] (zero past K); cnf[c] =
 // (float)cc[c] (huge past K); cmax[0] = max_c |c'|, cmax[2] = |mu| (one block).
-__global__ __launch_bounds__(256) void k_kmeans_prep_b3(i64 D, i64 K, i64 Kp, const double* __restrict__ C,
-                                                        __bf16* __restrict__ CBh, __bf16* __restrict__ CBl,
-                                                        float* __restrict__ cnf, double* __restrict__ cmax,
-                                                        double mcoef) {
-  __shared__ double red[256];
+// One block of 1024 threads: mu from 8 column partial sums per dimension
+// (combined in a fixed order), then one wave per centre (lane = dimension,
+// coalesced), wave-reduced |c'|^2 and mu.c' in a fixed shuffle order.
+__global__ __launch_bounds__(1024) void k_kmeans_prep_b3(i64 D, i64 K, i64 Kp, const double* __restrict__ C,
+                                                         __bf16* __restrict__ CBh, __bf16* __restrict__ CBl,
+                                                         float* __restrict__ cnf, double* __restrict__ cmax,
+                                                         double mcoef) {
+  __shared__ double part[8][KB_DMAX];
   __shared__ float mus[KB_DMAX];
-  for (i64 d = threadIdx.x; d < D; d += 256) {
+  __shared__ double red[16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  for (int i = t; i < 8 * (int)D; i += 1024) {
+    const int d = i % (int)D, g = i / (int)D;
     double m = 0.0;
-    for (i64 c = 0; c < K; ++c) m += C[c * D + d];
-    mus[d] = (float)(m / (double)K);
+    for (i64 c = g; c < K; c += 8) m += C[c * D + d];
+    part[g][d] = m;
+  }
+  __syncthreads();
+  if (t < D) {
+    double m = 0.0;
+    for (int g = 0; g < 8; ++g) m += part[g][t];
+    mus[t] = (float)(m / (double)K);
   }
   __syncthreads();
   double mx = 0.0;
-  for (i64 c = threadIdx.x; c < Kp; c += 256) {
+  for (i64 c = w; c < Kp; c += 16) {
     double s = 0.0, sm = 0.0;
-    for (i64 d = 0; d < D; ++d) {
+    for (int d = lane; d < D; d += 64) {
       const double v = c < K ? C[c * D + d] - (double)mus[d] : 0.0;
       const float v32 = (float)v;
       const __bf16 hi = (__bf16)v32;
@@ -1098,25 +1110,25 @@ __global__ __launch_bounds__(256) void k_kmeans_prep_b3(i64 D, i64 K, i64 Kp, co
       s += v * v;
       sm += (double)mus[d] * v;
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      s += __shfl_xor(s, o, 64);
+      sm += __shfl_xor(sm, o, 64);
+    }
     // padding centres: a huge FINITE cc (the filter tags a' mantissa bits,
     // which would turn +inf into NaN); they never win, and a lone real centre
     // is certified against them
-    cnf[c] = c < K ? (float)(s + 2.0 * sm) : 3.0e38f;
+    if (lane == 0) cnf[c] = c < K ? (float)(s + 2.0 * sm) : 3.0e38f;
     if (c < K) mx = (s > mx || s != s) ? s : mx;
   }
-  red[threadIdx.x] = mx;
+  if (lane == 0) red[w] = mx;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) {
-      const double a = red[threadIdx.x], b = red[threadIdx.x + o];
-      red[threadIdx.x] = (b > a || b != b) ? b : a;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
+  if (t == 0) {
+    double m = red[0];
+    for (int k = 1; k < 16; ++k) m = (red[k] > m || red[k] != red[k]) ? red[k] : m;
     double mn = 0.0;
     for (i64 d = 0; d < D; ++d) mn += (double)mus[d] * (double)mus[d];
-    cmax[0] = sqrt(red[0]) * 1.001;
+    cmax[0] = sqrt(m) * 1.001;
     cmax[1] = mcoef;  // fp32 tie margin coefficient (0: fp64 distances), read by the filters
     cmax[2] = sqrt(mn) * 1.001;
   }
@@ -2259,7 +2271,7 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
     __bf16* CBh = (__bf16*)CT;
     __bf16* CBl = CBh + (i64)32 * nct * D;
     float* cnf = (float*)cn;
-    k_kmeans_prep_b3<<<1, 256, 0, S(stream)>>>(D, K, 32 * nct, centers, CBh, CBl, cnf, cmax, mcoef);
+    k_kmeans_prep_b3<<<1, 1024, 0, S(stream)>>>(D, K, 32 * nct, centers, CBh, CBl, cnf, cmax, mcoef);
     LAUNCH_CHECK("spx_kmeans_assign(prep)");
     static int ncu = 0;
     if (!ncu) {

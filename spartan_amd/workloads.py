@@ -72,8 +72,10 @@ def kmeans_fit(X, n_clusters, n_iter, centers=None, seed=0):
   label_tiles = {}
   for it in range(n_iter):
     cdev = torch.as_tensor(centers).to(ctx.device)
-    sums = torch.empty((K, D), dtype=torch.float64, device=ctx.device)
-    counts = torch.empty((K,), dtype=torch.int64, device=ctx.device)
+    # sums and counts share one buffer: one D2H per iteration
+    buf = torch.empty((K * D + K,), dtype=torch.float64, device=ctx.device)
+    sums = buf[:K * D].view(K, D)
+    counts = buf[K * D:].view(torch.int64)
     first = True
     for ex, tile in Xa.local.items():
       lab = torch.empty((ex.shape[0],), dtype=torch.int64, device=ctx.device)
@@ -86,8 +88,9 @@ def kmeans_fit(X, n_clusters, n_iter, centers=None, seed=0):
       counts.zero_()
     comm.all_reduce(sums, 'sum')
     comm.all_reduce(counts, 'sum')
-    c_host = counts.cpu().numpy()
-    s_host = sums.cpu().numpy()
+    host = buf.cpu().numpy()
+    c_host = host[K * D:].view(np.int64)
+    s_host = host[:K * D].reshape(K, D)
     empty = c_host == 0
     if np.any(empty):
       c_host = c_host.copy()
