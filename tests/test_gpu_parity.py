@@ -458,6 +458,41 @@ def test_lreg_cfg5_small(ex, W):
   check_fp(g, cpu, exact, 1e-5)
 
 
+@pytest.mark.parametrize('W', [1, 3])
+def test_replayed_plans_follow_new_values(ex, W):
+  """An iterative driver's DAG is replayed (plan cache), its LocalExpr tree
+  lowered once (engine bind memo) and its reduction relaunched from a
+  recorded launch plan (backend.reduce): every iteration must still see its
+  own host vector, scalars and arrays -- checked against NumPy per step,
+  with a shape change in between (a different plan, then back)."""
+  from spartan_amd import backend
+  expr, setw = ex
+  setw(W)
+  n, d = 3000, 64
+  X = rng.rand((n, d), 41, np.float32)
+  Yv = rng.rand((n, 1), 42, np.float32)
+  x = expr.lazify(expr.rand(n, d, dtype=np.float32, seed=41).force())
+  y = expr.lazify(expr.rand(n, 1, dtype=np.float32, seed=42).force())
+  be = backend.get()
+  g = np.random.default_rng(5)
+  for it in range(6):
+    w = g.random((d, 1)).astype(np.float32) - 0.5
+    a = float(g.random()) * 4 - 2
+    got = expr.sum(x * (expr.dot(x, w) - y), axis=0).optimized().glom()
+    exact = (X.astype(np.float64) * (X.astype(np.float64) @ w.astype(np.float64) - Yv)).sum(0)
+    check_fp(got, (X * (X @ w - Yv)).sum(0), exact, 1e-5)
+    got2 = expr.sum(x * a + 1.5, axis=1).optimized().glom()
+    exact2 = (X.astype(np.float64) * a + 1.5).sum(1)
+    check_fp(got2, (X * np.float32(a) + np.float32(1.5)).sum(1), exact2, 1e-5)
+    if it == 2:  # another shape, then the first one again
+      xs = expr.rand(n // 2, d, dtype=np.float32, seed=41)
+      got3 = expr.sum(xs * (expr.dot(xs, w) - 1.0), axis=0).optimized().glom()
+      Xs = X[:n // 2]  # counter-based generator: same flat indices
+      e3 = (Xs.astype(np.float64) * (Xs.astype(np.float64) @ w.astype(np.float64) - 1.0)).sum(0)
+      check_fp(got3, (Xs * (Xs @ w - np.float32(1.0))).sum(0), e3, 1e-5)
+  assert be._reduce_plans  # the replay path was taken
+
+
 @pytest.mark.parametrize('K,dt', [(64, np.float32), (48, np.float32), (5, np.float32), (2, np.float32),
                                   (64, np.float64), (33, np.float64)])
 @pytest.mark.parametrize('W', [1, 3])
