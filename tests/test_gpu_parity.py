@@ -429,6 +429,65 @@ def test_full_size_checksums(ex):
              np.array([row.astype(np.float64).sum()]), 1e-5)
 
 
+def test_lreg_cfg5_full_size(ex):
+  """cfg5 at its BASELINE size (X 1e8 x 64 fp32): the fused one-pass
+  gradient equals an fp64 restatement computed chunk by chunk on the device
+  (X^T (X w - y) with torch fp64 matmuls) within the fp32 rule."""
+  import torch
+  expr, setw = ex
+  setw(1)
+  n, d = 100_000_000, 64
+  X = expr.rand(n, d, dtype=np.float32, seed=41).force()
+  Y = expr.rand(n, 1, dtype=np.float32, seed=42).force()
+  w = (np.random.default_rng(43).random((d, 1)) - 0.5).astype(np.float32)
+  got = expr.sum(expr.lazify(X) * (expr.dot(expr.lazify(X), w) - expr.lazify(Y)), axis=0).optimized().glom()
+  xt = next(iter(X.local.values())).data
+  yt = next(iter(Y.local.values())).data
+  wd = torch.as_tensor(w, dtype=torch.float64, device=xt.device)
+  acc = torch.zeros((d,), dtype=torch.float64, device=xt.device)
+  for r0 in range(0, n, 10_000_000):
+    xc = xt[r0:r0 + 10_000_000].to(torch.float64)
+    acc += (xc * (xc @ wd - yt[r0:r0 + 10_000_000].to(torch.float64))).sum(0)
+  exact = acc.cpu().numpy()
+  np.testing.assert_allclose(np.asarray(got, np.float64), exact, rtol=1e-5, atol=1e-5 * np.abs(exact).max())
+
+
+def test_kmeans_cfg3_full_size(ex):
+  """cfg3 at its BASELINE size (1e8 x 128 fp32, k = 256, second-iteration
+  centres): the certified assignment equals the all-exact kernel on a 2M-row
+  prefix and on 2M rows at the end; the fp64 centroid sums and counts equal a
+  chunked torch index_add restatement (counts exact, sums within 1e-12)."""
+  import torch
+  from spartan_amd import backend
+  expr, setw = ex
+  setw(1)
+  be = backend.get()
+  N, D, K = 100_000_000, 128, 256
+  dev = torch.device('cuda:0')
+  pts = torch.empty((N, D), dtype=torch.float32, device=dev)
+  be.fill(pts, backend.FILL_UNIFORM, 0.0, 1.0, 21, (0, 0), (N, D))
+  lab = torch.empty((N,), dtype=torch.int64, device=dev)
+  sums = torch.empty((K, D), dtype=torch.float64, device=dev)
+  cnt = torch.empty((K,), dtype=torch.int64, device=dev)
+  be.kmeans_assign(pts, pts[:K].to(torch.float64).contiguous(), lab)
+  be.kmeans_accumulate(pts, lab, sums, cnt)
+  cen = (sums / cnt.clamp(min=1).to(torch.float64).reshape(K, 1)).contiguous()
+  be.kmeans_assign(pts, cen, lab)
+  for a, b in ((0, 2_000_000), (N - 2_000_000, N)):
+    ref = torch.empty((b - a,), dtype=torch.int64, device=dev)
+    be.kmeans_assign(pts[a:b], cen, ref, exact_only=True)
+    assert torch.equal(lab[a:b], ref)
+  be.kmeans_accumulate(pts, lab, sums, cnt)
+  s2 = torch.zeros((K, D), dtype=torch.float64, device=dev)
+  c2 = torch.zeros((K,), dtype=torch.int64, device=dev)
+  for r0 in range(0, N, 10_000_000):
+    li = lab[r0:r0 + 10_000_000]
+    s2.index_add_(0, li, pts[r0:r0 + 10_000_000].to(torch.float64))
+    c2 += torch.bincount(li, minlength=K)
+  assert torch.equal(cnt, c2) and int(cnt.sum()) == N
+  torch.testing.assert_close(sums, s2, rtol=1e-12, atol=1e-9)
+
+
 # ------------------------------------------------------ cfg5: lreg gradient
 @pytest.mark.parametrize('W', [1, 3])
 def test_lreg_cfg5_small(ex, W):
