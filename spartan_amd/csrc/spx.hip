@@ -1462,6 +1462,9 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
           const double tq = __shfl(thr, 2 * qq + 32 * h, 64);
           const unsigned int s0 = __builtin_amdgcn_readlane(myslot, 2 * qq);
           const unsigned int s1 = __builtin_amdgcn_readlane(myslot, 32 + 2 * qq);
+          // the 8 mask words of both rows are moved into lanes 0-7 / 32-39
+          // and written by ONE store (was 16 single-lane stores per register)
+          unsigned int mw = 0;
 #pragma unroll
           for (int ct = 0; ct < 8; ++ct) {
             unsigned long long m = 0;
@@ -1469,9 +1472,9 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
               const float a = __builtin_fmaf(-2.f, acc[ct < NCT ? ct : 0][qq], cnr[ct < NCT ? ct : 0]);
               m = __ballot((double)a <= tq);
             }
-            if (n0 && lane == ct) cand_list[s0].mask[ct] = (unsigned int)m;
-            if (n1 && lane == 32 + ct) cand_list[s1].mask[ct] = (unsigned int)(m >> 32);
+            mw = lane == ct ? (unsigned int)m : lane == 32 + ct ? (unsigned int)(m >> 32) : mw;
           }
+          if ((r < 8) && (h ? n1 : n0)) cand_list[h ? s1 : s0].mask[r] = mw;
         }
       }
     }
