@@ -1685,6 +1685,10 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
         al[ks][j] = (__bf16)(x - (float)ah[ks][j]);
       }
     }
+    // (the compiler sinks the 64 |p|^2 fmas to the decision, keeping the raw
+    // tile live through the sweep; pinning them here frees 47 registers but
+    // measured 2 % slower, and the freed registers buy a next-tile prefetch
+    // that only wins that back: 20.3 / 20.7 / 20.5 ms, gpurun_out ksv4)
 #if KS_PREFETCH
     // the split above must finish reading ra before the next tile's loads
     // land in it: without this fence the scheduler hoists the loads above
