@@ -428,6 +428,27 @@ def _call_expr(inputs, j, name='fexpr', n_rd=0, sfx=''):
                         ''.join(', rd%d%s' % (k, sfx) for k in range(n_rd)))
 
 
+_NAME_RE = None
+
+
+def _suffix_names(line, sfx):
+  """Rename the per-load identifiers of a _load_vec / loads() line."""
+  global _NAME_RE
+  import re
+  if _NAME_RE is None:
+    _NAME_RE = re.compile(r'\b(off\d+|s\d+_in|vt\d+|xv\d+|x\d+_\d+)\b')
+  return _NAME_RE.sub(lambda m: m.group(1) + sfx, line)
+
+
+def rows_unroll(inputs, classes):
+  """Unrolled steps of the row-reduce loop: 4 for one streamed input, 2 for
+  two, 1 from three on (cfg2's x*y+exp(z) already streams 3 KiB per wave)."""
+  if os.environ.get('SPX_ROWS_UNROLL'):  # dev knob (tools/, experiments only)
+    return int(os.environ['SPX_ROWS_UNROLL'])
+  streamed = sum(1 for c in classes if c != 'b')
+  return 4 if streamed <= 1 else 2 if streamed == 2 else 1
+
+
 def cols_unroll(inputs, classes, vec, row_strides=None):
   """Rows per lane group per iteration of the column-reduce loop: enough that
   each wave keeps >= ~3 KiB of streamed loads in flight (Little's law at
@@ -618,9 +639,28 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
 }''')
 
   if kind == 'rows':
+    # U steps of the block's row loop per iteration, every load first: with
+    # one or two streamed inputs a single vector load per lane cannot keep
+    # enough bytes in flight (x.sum(axis=1) at cfg2 size: 4.1 TB/s with U=1).
+    # Each accumulator still takes its elements in the same order: results
+    # are unchanged.
+    U = rows_unroll(inputs, classes)
+
     def body(V):
       b = []
-      b.append('for (i64 r = r0 + (i64)tid() * %d; r < r1; r += 256 * %d) {' % (V, V))
+      b.append('i64 r = r0 + (i64)tid() * %d;' % V)
+      if U > 1:
+        b.append('for (; r + %d * 256 * %d < r1; r += %d * 256 * %d) {' % (U - 1, V, U, V))
+        for u in range(U):
+          step = '(r + %d * 256 * %d)' % (u, V)
+          lines = loads(V, lambda s: 'o * a.str[%d][0] + %s * a.str[%d][1]' % (s, step, s), 1)
+          b += ['  ' + _suffix_names(x, '_u%d' % u) for x in lines]
+        for u in range(U):
+          for j in range(V):
+            call = '(%s)%s' % (act, _call_expr(inputs, j, n_rd=len(rds), sfx='_u%d' % u))
+            b.append('  ' + _acc_update(op, j, call, gidx('r + %d * 256 * %d + %d' % (u, V, j))))
+        b.append('}')
+      b.append('for (; r < r1; r += 256 * %d) {' % V)
       b += ['  ' + x for x in loads(V, lambda s: 'o * a.str[%d][0] + r * a.str[%d][1]' % (s, s), 1)]
       for j in range(V):
         b.append('  ' + _acc_update(op, j, val_j(j), gidx('r + %d' % j)))

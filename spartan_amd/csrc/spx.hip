@@ -1759,7 +1759,13 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
         for (int qq = 0; qq < 16 / KS; ++qq) {
           const int q = ks * (16 / KS) + qq;
           const float sq = KS_CHAINS == 2 ? p0[q] + p1[q] : p0[q];
+#if defined(KS_DEV_NOFMA)  // timing split only; never set in the product build
+          const float v = ks_tag(sq, (unsigned int)pct);
+#elif defined(KS_DEV_NOTAG)  // timing split only; never set in the product build
+          const float v = __builtin_fmaf(-2.f, sq, pcc);
+#else
           const float v = ks_tag(__builtin_fmaf(-2.f, sq, pcc), (unsigned int)pct);
+#endif
           sec[q] = ks_med3(v, lo[q], sec[q]);
           lo[q] = ks_min(lo[q], v);
         }
