@@ -239,6 +239,7 @@ def compile_code_object(src):
 
 _REPLAY_PLANS = os.environ.get('SPX_REDUCE_PLANS', '1') != '0'  # dev A/B switch
 _NCU = []
+NT_STORE_BYTES = int(os.environ.get('SPX_NT_STORE_BYTES', 64 << 20))  # map outputs at least this large: non-temporal stores
 ROWS_GRID_PER_CU = 2  # rows reductions: 1.824 ms vs 1.836 uncapped at cfg2 axis 1 (profiles/r02_cfg2_grid.txt)
 
 
@@ -345,10 +346,13 @@ class HipBackend:
       vec_ok = (cshape[-1] % V == 0) and out.data_ptr() % 16 == 0 and all(
           _vec_aligned(inputs[s], cstr[k], classes[k], V) for k, s in enumerate(slots))
     args.flags = 1 if (vec_ok and V > 1) else 0
-    sig = ('map', root.sig(), tuple(ins), tuple(classes), ndim, V, dense)
+    # streamed outputs: non-temporal stores (x*y+exp(z) map at 2^30 fp32:
+    # 2.75 -> 2.57 ms, profiles/r02_stream_ceiling_maps.txt)
+    nt = n * out.element_size() >= NT_STORE_BYTES
+    sig = ('map', root.sig(), tuple(ins), tuple(classes), ndim, V, dense, nt)
     fn = self._sig_fns.get(sig)
     if fn is None:
-      fn = self._sig_fns[sig] = self.kernel(codegen.gen_map(root, ins, classes, ndim, V, dense), 'spx_map')
+      fn = self._sig_fns[sig] = self.kernel(codegen.gen_map(root, ins, classes, ndim, V, dense, nt), 'spx_map')
     per = V if args.flags else 1
     grid = max(1, min(-(-n // (256 * per)), 256 * 16))
     self.launch(fn, grid, args)

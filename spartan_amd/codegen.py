@@ -36,6 +36,16 @@ MAX_DIM = 8
 NT_LOADS = os.environ.get('SPX_NT_LOADS', '1') != '0'
 
 
+def _vstore(vtype, ptr_expr, val, nt):
+  """Source of one contiguous vector store: non-temporal for large streamed
+  outputs (backend.map picks the variant by output size; a runtime branch
+  between the two forms is folded into one plain store by the compiler),
+  plain otherwise (a small output stays in L2 / MALL for its next reader)."""
+  if nt:
+    return '__builtin_nontemporal_store(%s, (GLOBAL %s*)(%s));' % (val, vtype, ptr_expr)
+  return '*(GLOBAL %s*)(%s) = %s;' % (vtype, ptr_expr, val)
+
+
 def _vload(vtype, ptr_expr):
   """Source of one contiguous vector load of type ``vtype`` at ``ptr_expr``."""
   if NT_LOADS:
@@ -470,7 +480,7 @@ def cols_unroll(inputs, classes, vec, row_strides=None):
 
 
 # ---------------------------------------------------------------- map
-def gen_map(root, inputs, classes, ndim, vec, dense):
+def gen_map(root, inputs, classes, ndim, vec, dense, nt_store=False):
   """Elementwise kernel.  inputs: [(slot, dtype)], classes: per-input 'c'/'b'/'g'.
 
   dense=True: every input is contiguous with the output's shape (flat index).
@@ -508,14 +518,33 @@ def gen_map(root, inputs, classes, ndim, vec, dense):
       b.append('vo r;')
       for j in range(V):
         b.append('r[%d] = %s;' % (j, _call_expr(inputs, j)))
-      b.append('*(GLOBAL vo*)(%s + e) = r;' % outp)
+      b.append(_vstore('vo', '%s + e' % outp, 'r', nt_store))
     return b
 
   L.append('KERN void spx_map(KArgs a) {')
   L.append('  const i64 n = a.n;')
   L.append('  if (a.flags & 1) {')
   L.append('    const i64 step = (i64)a.grid * 256 * %d;' % vec)
-  L.append('    for (i64 e = ((i64)bidx() * 256 + tid()) * %d; e < n; e += step) {' % vec)
+  L.append('    i64 e = ((i64)bidx() * 256 + tid()) * %d;' % vec)
+  # dense maps with one or two streamed inputs: U grid steps per iteration,
+  # all loads first (one 16-byte load per lane and step does not keep enough
+  # bytes in flight: x + 1 at 2^30 fp32 ran 4.5 TB/s read+write)
+  U = rows_unroll(inputs, ['c'] * len(inputs)) if dense and vec > 1 else 1
+  if U > 1:
+    L.append('    for (; e + %d * step < n; e += %d * step) {' % (U - 1, U))
+    lines = []
+    for u in range(U):
+      for s_, dt in inputs:
+        lines += [_suffix_names(x, '_u%d' % u) for x in _load_vec(s_, dt, 'c', '(e + %d * step)' % u, vec)]
+    lines.append('typedef %s __attribute__((ext_vector_type(%d))) vo;' % (out_ct, vec))
+    for u in range(U):
+      lines.append('{ vo r;')
+      for j in range(vec):
+        lines.append('  r[%d] = %s;' % (j, _call_expr(inputs, j, sfx='_u%d' % u)))
+      lines.append('  %s }' % _vstore('vo', '((GLOBAL %s*)a.out0) + (e + %d * step)' % (out_ct, u), 'r', nt_store))
+    L += ['      ' + x for x in lines]
+    L.append('    }')
+  L.append('    for (; e < n; e += step) {')
   L += ['      ' + x for x in body(vec, dense)]
   L.append('    }')
   L.append('  } else {')
