@@ -353,8 +353,11 @@ class HipBackend:
     fn = self._sig_fns.get(sig)
     if fn is None:
       fn = self._sig_fns[sig] = self.kernel(codegen.gen_map(root, ins, classes, ndim, V, dense, nt), 'spx_map')
-    per = V if args.flags else 1
-    grid = max(1, min(-(-n // (256 * per)), 256 * 16))
+    per = V if args.flags & 1 else 1
+    # one vector per lane and no grid-stride loop: x + 1 / x * y at 2^30 fp32
+    # 1.75 / 2.58 ms with a 4096-block grid-stride loop, 1.34 / 2.01 ms with
+    # the full grid (6.4 TB/s read+write; profiles/r02_map_grid.txt)
+    grid = max(1, min(-(-n // (256 * per)), int(os.environ.get('SPX_MAP_GRID', 0x7fffffff))))  # env: dev knob
     self.launch(fn, grid, args)
 
   # --------------------------------------------------------------- reduce

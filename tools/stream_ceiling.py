@@ -34,11 +34,11 @@ for name, f, nin in (cases if os.environ.get("SC_REDUCE", "1") == "1" else []):
 for name, f, nin in [('x*y+exp(z)', lambda: X * Y + expr.exp(Z), 3), ('x+1', lambda: X + 1.0, 1),
                      ('x*y', lambda: X * Y, 2)]:
   for _ in range(2):
-    f().force()
+    f().optimized().force()
   torch.cuda.synchronize()
   be.kernel_events = []
   for _ in range(10):
-    f().force()
+    f().optimized().force()
   torch.cuda.synchronize()
   t = [s.elapsed_time(e) for n, s, e in be.kernel_events if n == 'spx_map']
   be.kernel_events = None
