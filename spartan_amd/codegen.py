@@ -584,9 +584,12 @@ def _ident(op, dt):
     return '(%s)0' % ct
   if is_float(dt):
     return '(%s)__builtin_inf()' % ct if op in ('min', 'argmin') else '-(%s)__builtin_inf()' % ct
-  if op in ('min', 'argmin'):
-    return '(%s)0x7fffffffffffffffLL' % ct
-  return '(%s)(-0x7fffffffffffffffLL - 1)' % ct
+  # the value type's own extremes (a truncated int64 extreme would be -1 / 0)
+  ii = np.iinfo(dt)
+  v = int(ii.max) if op in ('min', 'argmin') else int(ii.min)
+  if v == -(1 << 63):
+    return '(%s)(-0x7fffffffffffffffLL - 1)' % ct
+  return '(%s)%dULL' % (ct, v) if v >= 0 else '(%s)(%dLL)' % (ct, v)
 
 
 def _comb_fns(op, adt):
@@ -602,20 +605,27 @@ def _comb_fns(op, adt):
               % (ct, ct, ct, c))
     return 'DEV %s comb(%s x, %s y) { return (y %s x) ? y : x; }' % (ct, ct, ct, c)
   c = '<' if op == 'argmin' else '>'
+  # better_seq: the in-loop form, for a thread's own elements in increasing
+  # index order -- a held NaN is never displaced and a tie only displaces the
+  # identity (acci still the sentinel), so no 64-bit index compare
   if fl:
     return ('DEV bool better(%s v, i64 vi, %s b, i64 bi) {\n'
             '  bool vn = v != v, bn = b != b;\n'
             '  if (vn || bn) { if (vn && !bn) return true; if (!vn && bn) return false; return vi < bi; }\n'
             '  if (v == b) return vi < bi;\n'
-            '  return v %s b;\n}' % (ct, ct, c))
-  return ('DEV bool better(%s v, i64 vi, %s b, i64 bi) { if (v == b) return vi < bi; return v %s b; }'
-          % (ct, ct, c))
+            '  return v %s b;\n}\n'
+            'DEV bool better_seq(%s v, %s b, i64 bi) {\n'
+            '  return (b == b) & ((v != v) | (v %s b) | ((v == b) & (bi == 0x7fffffffffffffffLL)));\n}'
+            % (ct, ct, c, ct, ct, c))
+  return ('DEV bool better(%s v, i64 vi, %s b, i64 bi) { if (v == b) return vi < bi; return v %s b; }\n'
+          'DEV bool better_seq(%s v, %s b, i64 bi) { return (v %s b) | ((v == b) & (bi == 0x7fffffffffffffffLL)); }'
+          % (ct, ct, c, ct, ct, c))
 
 
 def _acc_update(op, j, val, idx_expr):
   if op in ('argmin', 'argmax'):
-    return ('{ auto v_ = %s; i64 vi_ = %s; if (better(v_, vi_, acc%d, acci%d)) { acc%d = v_; acci%d = vi_; } }'
-            % (val, idx_expr, j, j, j, j))
+    return ('{ auto v_ = %s; if (better_seq(v_, acc%d, acci%d)) { acc%d = v_; acci%d = %s; } }'
+            % (val, j, j, j, j, idx_expr))
   return 'acc%d = comb(acc%d, %s);' % (j, j, val)
 
 
@@ -653,6 +663,10 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
       b += _load_vec(s, dt, cls, 'off%d' % s, V)
     return b
 
+  def to_global():
+    # tile-local indices of the per-thread arg accumulators -> global ones
+    return ['if (acci%d != 0x7fffffffffffffffLL) acci%d = %s;' % (j, j, gidx('acci%d' % j)) for j in range(vec)]
+
   def gidx(r_expr):
     # global index of element r along the reduced dim (axis) or flat (axis None)
     return ('(a.aux[5] ? gflat(a, %s) : a.aux[4] + %s)' % (r_expr, r_expr))
@@ -687,12 +701,12 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
         for u in range(U):
           for j in range(V):
             call = '(%s)%s' % (act, _call_expr(inputs, j, n_rd=len(rds), sfx='_u%d' % u))
-            b.append('  ' + _acc_update(op, j, call, gidx('r + %d * 256 * %d + %d' % (u, V, j))))
+            b.append('  ' + _acc_update(op, j, call, '(r + %d * 256 * %d + %d)' % (u, V, j)))
         b.append('}')
       b.append('for (; r < r1; r += 256 * %d) {' % V)
       b += ['  ' + x for x in loads(V, lambda s: 'o * a.str[%d][0] + r * a.str[%d][1]' % (s, s), 1)]
       for j in range(V):
-        b.append('  ' + _acc_update(op, j, val_j(j), gidx('r + %d' % j)))
+        b.append('  ' + _acc_update(op, j, val_j(j), '(r + %d)' % j))
       b.append('}')
       return b
 
@@ -711,6 +725,10 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
     L.append('  } else {')
     L += ['    ' + x for x in body(1)]
     L.append('  }')
+    # in the loop the indices are tile-local (monotonic in the global index,
+    # so first-occurrence ties resolve the same); converted once here
+    if arg:
+      L += ['  ' + x for x in to_global()]
     # fold the V slots in index order, then block tree
     L.append('  %s accv = acc0;' % act)
     if arg:
@@ -763,7 +781,7 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
       b.append('  for (i64 r = cl * %d; r < R; r += LPR * %d) {' % (V, V))
       b += ['    ' + x for x in loads(V, lambda s: 'o * a.str[%d][0] + r * a.str[%d][1]' % (s, s), 1)]
       for j in range(V):
-        b.append('    ' + _acc_update(op, j, val_j(j), gidx('r + %d' % j)))
+        b.append('    ' + _acc_update(op, j, val_j(j), '(r + %d)' % j))
       b.append('  }')
       b.append('}')
       return b
@@ -786,6 +804,8 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
     L.append('    } else {')
     L += ['      ' + x for x in body(1)]
     L.append('    }')
+    if arg:
+      L += ['    ' + x for x in to_global()]
     L.append('    %s accv = acc0;' % act)
     if arg:
       L.append('    i64 acci = acci0;')
@@ -841,7 +861,7 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
       upd = []
       for j in range(V):
         call = '(%s)%s' % (act, _call_expr(inputs, j, n_rd=len(rds), sfx=sfx))
-        upd.append(_acc_update(op, j, call, gidx(rv)))
+        upd.append(_acc_update(op, j, call, '(%s)' % rv))
       if masked:
         cp.append('if (colok) {')
         cp += ['  ' + x for x in upd]
@@ -925,6 +945,8 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
     L.append('  } else {')
     L += ['    ' + x for x in body(1)]
     L.append('  }')
+    if arg:
+      L += ['  ' + x for x in to_global()]
     # LDS combine over the 4*RPW row groups sharing a column, in row-group order
     L.append('  SHARED %s sv[256 * %d];' % (act, vec))
     if arg:

@@ -400,6 +400,25 @@ def test_int32_and_bool_semantics(ex):
   np.testing.assert_array_equal(m, n.sum(0) // 6)
 
 
+@pytest.mark.parametrize('dt', [np.int32, np.int64])
+def test_small_int_min_max_arg(ex, dt):
+  """min / max / argmin / argmax keep the value type: the identity is that
+  type's extreme (all-positive and all-negative inputs, ties at the extremes,
+  each of the rows / rowsp / cols skeletons)."""
+  expr, setw = ex
+  setw(3)
+  ii = np.iinfo(dt)
+  rng = np.random.default_rng(7)
+  for shape in [(6, 10), (7, 3000), (3000, 5)]:
+    for lo, hi in [(1, 100), (ii.min, ii.min // 2 if ii.min < 0 else 1), (ii.max - 3, ii.max)]:
+      n = rng.integers(lo, int(hi) + 1, size=shape, dtype=np.int64).astype(dt)
+      x = expr.from_numpy(n)
+      for axis in [None, 0, 1]:
+        for fe, fn in [(expr.min, np.min), (expr.max, np.max), (expr.argmin, np.argmin), (expr.argmax, np.argmax)]:
+          got = fe(x, axis=axis).glom()
+          np.testing.assert_array_equal(got, fn(n, axis=axis), err_msg='%s %s %s %s' % (dt, shape, axis, fn.__name__))
+
+
 def test_full_size_checksums(ex):
   """cfg2 at its BASELINE size (2^30 fp32): size-independent properties --
   the axis-0, axis-1 and full sums agree (checksum of checksums) and the
