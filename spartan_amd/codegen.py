@@ -601,7 +601,9 @@ def _comb_fns(op, adt):
   if op in ('min', 'max'):
     c = '<' if op == 'min' else '>'
     if fl:
-      return ('DEV %s comb(%s x, %s y) { if (x != x) return x; if (y != y) return y; return (y %s x) ? y : x; }'
+      # NaN-propagating: y wins if it is NaN or strictly better; a NaN x is
+      # never displaced by a number (one compare + one select fewer)
+      return ('DEV %s comb(%s x, %s y) { return ((y %s x) | (y != y)) ? y : x; }'
               % (ct, ct, ct, c))
     return 'DEV %s comb(%s x, %s y) { return (y %s x) ? y : x; }' % (ct, ct, ct, c)
   c = '<' if op == 'argmin' else '>'
