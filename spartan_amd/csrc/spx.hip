@@ -15,6 +15,7 @@
 #include <cstring>
 #include <string>
 #include <type_traits>
+#include <utility>
 
 #include "../../include/spx.h"
 
@@ -1152,12 +1153,13 @@ __device__ __forceinline__ double kc_bound(double eS, double pn, double cmax, do
 
 // kc_bound as e(|p|) = k0 + k1 |p| + k2 |p|^2 (|p|^2 >= pp2), coefficients
 // rounded up to fp32, for a per-row evaluation in fp32.
-__device__ __forceinline__ void kc_coef(double eS, double cmax, double mun, double mcoef, i64 D, float (&k)[3]) {
+__device__ __forceinline__ void kc_coef(double eS, double cmax, double mun, double mcoef, i64 D, float (&k)[3],
+                                        double xk1 = 0.0, double xk0 = 0.0) {
   const double u32 = 5.9604644775390625e-08, eps = 1.1920928955078125e-07;
   const double cm2 = cmax * cmax + 2.0 * mun * cmax, m = mun + cmax;
   const double k0 = 2.02 * u32 * cm2 + 1e-28 * (double)D * (1.0 + cmax) * (1.0 + cmax) +
-                    1e-8 * (cmax * cmax + mun * mun) + 8.0 * eps * cm2 + 0.5 * mcoef * m * m + 1e-30;
-  const double k1 = 2.0 * eS + 2.02 * u32 * cmax + 16.0 * eps * cmax + mcoef * m;
+                    1e-8 * (cmax * cmax + mun * mun) + 8.0 * eps * cm2 + 0.5 * mcoef * m * m + 1e-30 + xk0;
+  const double k1 = 2.0 * eS + 2.02 * u32 * cmax + 16.0 * eps * cmax + mcoef * m + xk1;
   const double k2 = 1e-8 + 0.5 * mcoef;
   const double up = 1.0 + 2.384185791015625e-07;  // 2^-22: covers the rounding to fp32
   k[0] = (float)(k0 * up);
@@ -1522,9 +1524,6 @@ static void kb_launch(hipStream_t s, i64 N, i64 D, const float* P, i64 ldp, cons
 #ifndef KS_WAVES_CFG
 #define KS_WAVES_CFG 8  // waves per block (one block per CU): 8 = two per SIMD (<= 256 registers), 4 = one (<= 512)
 #endif
-#ifndef KS_CHAINS
-#define KS_CHAINS 1  // accumulator chains per centre tile (1: one 48 KS-product chain; 2: two chains + one add per value, a tighter bound but 32 more registers)
-#endif
 constexpr int KS_WAVES = KS_WAVES_CFG;
 #ifndef KS_PREFETCH
 #define KS_PREFETCH 0  // 1: next tile's loads in flight during the sweep (+64 registers: spills at 2 waves/SIMD)
@@ -1533,42 +1532,48 @@ constexpr int KS_WAVES = KS_WAVES_CFG;
 #define KS_PIPE 1  // 1: tile ct's top-2 fold interleaved with tile ct+1's MFMAs (two accumulator sets)
 #endif
 
-// LDS row of centre c: [hi: D bf16][lo: D bf16][48-byte pad]; the row stride
-// is 4 D + 48 bytes = 12 (mod 64) banks, so the 16-lane groups of a
-// ds_read_b128 (rows 0-3, 12-15, 20-27 ...) hit 16 distinct 4-bank quads,
-// and every read of a tile's k-loop is one base register + an immediate.
+// LDS row of centre c: [hi: D bf16][lo: D bf16][-cc/2 as 3 bf16 + 5 zeros]
+// [8 zero bf16][16-byte pad]; the row stride is 4 D + 48 bytes = 12 (mod 64)
+// banks, so the 16-lane groups of a ds_read_b128 (rows 0-3, 12-15, 20-27 ...)
+// hit 16 distinct 4-bank quads, and every read of a tile's k-loop is one base
+// register + an immediate.
 __host__ __device__ constexpr int ks_row_bytes(int D) { return 4 * D + 48; }
-static size_t ks_lds_bytes(i64 D, int nct) { return (size_t)32 * nct * ks_row_bytes((int)D) + (size_t)32 * nct * 4; }
+static size_t ks_lds_bytes(i64 D, int nct) { return (size_t)32 * nct * ks_row_bytes((int)D); }
 
-// Plain v_min_f32 / v_med3_f32 / v_and_or_b32: fminf / fmed3 on values
-// built by bit operations make the compiler canonicalize every operand first
-// (a v_max_f32 x, x each), which doubled the per-value epilogue here.  The
-// operands are finite or +inf (non-finite points are routed by the |p|^2 /
-// cmax checks before any of these values is used).
-__device__ __forceinline__ float ks_min(float a, float b) {
-  float r;
-  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
+// Plain v_med3_f32 / v_max_f32: fmaxf / fmed3 on values built by bit
+// operations make the compiler canonicalize every operand first (a v_max_f32
+// x, x each), which doubled the per-value epilogue here.  The operands are
+// finite or -inf (non-finite points are routed by the |p|^2 / cmax checks
+// before any of these values is used) and never a fresh MFMA result (inline
+// asm gets no MFMA -> VALU wait states from the hazard recognizer).
 __device__ __forceinline__ float ks_med3(float a, float b, float c) {
   float r;
   asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
-__device__ __forceinline__ float ks_tag(float a, unsigned int ct) {  // (bits(a) & ~7) | ct
-  unsigned int r;
-  asm("v_and_or_b32 %0, %1, -8, %2" : "=v"(r) : "v"(__builtin_bit_cast(unsigned int, a)), "v"(ct));
-  return __builtin_bit_cast(float, r);
+__device__ __forceinline__ float ks_max(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// (bits(a) & ~7) | ct.  Plain C, not inline asm: its operand comes straight
+// from an MFMA accumulator, and only compiler-generated instructions get the
+// MFMA -> VALU read wait states from the hazard recognizer (an asm
+// v_and_or_b32 there read stale accumulators: ~5 % wrong labels, caught by
+// the exact-kernel comparison).  An asm form placed three MFMAs after the
+// write measured no faster (tools/ks_variants.sh).
+__device__ __forceinline__ float ks_tag(float a, unsigned int ct) {
+  return __builtin_bit_cast(float, (__builtin_bit_cast(unsigned int, a) & ~7u) | (ct & 7u));
 }
 
-// Top-2 VALUES across the 32 lanes of each half (register halving as in
-// kb_top2_lanes, without carrying an index: the argmin lane is found
+// Top-2 (largest) VALUES across the 32 lanes of each half (register halving
+// as in kb_top2_lanes, without carrying an index: the best lane is found
 // afterwards by one ballot per row).  Lane (h, r) ends with register 0 =
 // row rt(r >> 1, h) over all 32 centres of every tile.
 __device__ __forceinline__ void ks_top2_vals(float (&lo)[16], float (&sec)[16], int lane) {
   auto comb = [](float a, float as, float b, float bs, float& l, float& s2) {
-    s2 = ks_med3(a, b, ks_min(as, bs));
-    l = ks_min(a, b);
+    s2 = ks_med3(a, b, ks_max(as, bs));
+    l = ks_max(a, b);
   };
   auto xor16 = [](float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x401F));
@@ -1604,6 +1609,12 @@ __device__ __forceinline__ void ks_top2_vals(float (&lo)[16], float (&sec)[16], 
   }
 }
 
+// f(integral_constant<int, Q>) for every Q of the sequence (compile-time Q)
+template <typename F, int... Q>
+__device__ __forceinline__ void ks_unroll(F&& f, std::integer_sequence<int, Q...>) {
+  (f(std::integral_constant<int, Q>{}), ...);
+}
+
 template <int NCT, int KS>
 __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const float* __restrict__ P, i64 ldp,
                                                                     const __bf16* __restrict__ CBh,
@@ -1615,8 +1626,6 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
                                                                     i64* __restrict__ und_list) {
   extern __shared__ __attribute__((aligned(16))) unsigned char kb_lds[];
   constexpr int NC = 32 * NCT, D = 16 * KS, RB = ks_row_bytes(D);
-  static_assert(KS % 2 == 0, "two accumulator chains");
-  float* cns = (float*)(kb_lds + NC * RB);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, h = lane >> 5;
   {
     // centre rows in the permuted k order of k_kmeans_filter_b3 (dim quads
@@ -1631,7 +1640,20 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
       *(kb_u2*)(row + 8 * pq) = *(const kb_u2*)&CBh[(i64)c * D + 4 * q];
       *(kb_u2*)(row + 2 * D + 8 * pq) = *(const kb_u2*)&CBl[(i64)c * D + 4 * q];
     }
-    for (int i = t; i < NC; i += KS_WAVES * 64) cns[i] = cnf[i];
+    // -cc/2 split exactly into three bf16 (8 + 8 + 8 significant bits of
+    // the fp32 value), for the k-step that adds it on the MFMA (lanes of the
+    // upper half read the zeros next to it)
+    for (int i = t; i < NC; i += KS_WAVES * 64) {
+      const float v = -0.5f * cnf[i];
+      const __bf16 b1 = (__bf16)v;
+      const float v1 = v - (float)b1;
+      const __bf16 b2 = (__bf16)v1;
+      const __bf16 b3 = (__bf16)(v1 - (float)b2);
+      const __bf16 z = (__bf16)0.f;
+      unsigned char* row = kb_lds + i * RB;
+      *(kb_bf8*)(row + 4 * D) = (kb_bf8){b1, b2, b3, z, z, z, z, z};
+      *(kb_bf8*)(row + 4 * D + 16) = (kb_bf8){z, z, z, z, z, z, z, z};
+    }
   }
   __syncthreads();
   const double cmax = cmax_p[0];
@@ -1640,12 +1662,16 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
   // round to one value; the margin is folded into e (gap > 2e + margin)
   const double mcoef = cmax_p[1], mun = cmax_p[2];
   const double u32 = 5.9604644775390625e-08;
-  // each accumulator chain: 48 products per k-step over KS / 2 k-steps, then
-  // one add of the two chains
-  const double chain = KS_CHAINS == 2 ? 48.0 * (double)(KS / 2) + 1.0 : 48.0 * (double)KS;
+  // one accumulator chain: 48 products per k-step over KS k-steps
+  const double chain = 48.0 * (double)KS;
   const double eS = (u32 + 3.1 * 3.814697265625e-06 + 2.0 * (chain + 3.0) * u32) * 1.01 * cmax;
   float kq[3];
-  kc_coef(eS, cmax, mun, mcoef, D, kq);
+  // the chain ends with one MFMA that adds -cc/2 (three nonzero products):
+  // its roundings, at most 16 of <= 2u |S - cc/2 + ...| each, priced in a'
+  // units as 64u |p| cmax + 32u (cmax^2 + 2|mu| cmax); the fma a' = cc - 2S
+  // is gone, and the tile tag on the accumulator (7 ulp of |S - cc/2|, i.e.
+  // 14 eps (|p| cmax + cm2 / 2) in a' units) stays inside kc_coef's 8 eps amax
+  kc_coef(eS, cmax, mun, mcoef, D, kq, 64.0 * u32 * cmax, 32.0 * u32 * (cmax * cmax + 2.0 * mun * cmax));
   // no overflow in S or a' (every a' finite): |p| cmax, cmax^2, |mu| cmax < 1e36
   const bool cok = cmax * cmax < 1e36 && mun * cmax < 1e36;
   const float pn_lim = (float)(cmax > 0.0 ? 1e36 / cmax : 1e36);
@@ -1674,17 +1700,20 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
     load(tile);  // the partner wave's sweep covers the latency
 #endif
     kb_bf8 ah[KS], al[KS];
-    float p2 = 0.f;
+    // |p|^2 only feeds the bound (x 1.001 slack): four independent partial
+    // chains instead of one 64-deep dependent fma chain
+    float p2q[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float x = j < 4 ? ra[ks][0][j] : ra[ks][1][j - 4];
-        p2 = __builtin_fmaf(x, x, p2);  // |p|^2 only feeds the bound (x 1.001 slack)
+        p2q[j & 3] = __builtin_fmaf(x, x, p2q[j & 3]);
         ah[ks][j] = (__bf16)x;
         al[ks][j] = (__bf16)(x - (float)ah[ks][j]);
       }
     }
+    float p2 = (p2q[0] + p2q[1]) + (p2q[2] + p2q[3]);
     // (the compiler sinks the 64 |p|^2 fmas to the decision, keeping the raw
     // tile live through the sweep; pinning them here frees 47 registers but
     // measured 2 % slower, and the freed registers buy a next-tile prefetch
@@ -1696,17 +1725,24 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
     __builtin_amdgcn_sched_barrier(0);
     if (tile + stride < ntiles) load(tile + stride);  // lands during the sweep below
 #endif
+    // running top-2 of acc = S - cc/2 = -a'/2 (the best centre has the
+    // LARGEST acc); lo / sec keep their names from the a' form
     float lo[16], sec[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      lo[q] = INFINITY;
-      sec[q] = INFINITY;
+      lo[q] = -INFINITY;
+      sec[q] = -INFINITY;
     }
     const unsigned char* rowp = kb_lds + r * RB + 16 * h;
-    // one centre tile: 3 KS MFMAs into two chains of KS / 2 k-steps each
-    auto chain = [&](int ct, kb_acc& c0, kb_acc& c1) {
+    // A operand of the -cc/2 k-step: all ones against the three bf16 pieces
+    // and zeros (the step's sum is the pieces' sum whatever the k order of the
+    // fragment; every product is exact)
+    const __bf16 one = (__bf16)1.f;
+    const kb_bf8 a_one = (kb_bf8){one, one, one, one, one, one, one, one};
+    // one centre tile: 3 KS MFMAs of x.c' in one chain, then the -cc/2 step
+    // LAST (so only its own roundings see |cc|: the bound in kc_coef)
+    auto chain = [&](int ct, kb_acc& c0) {
       c0 = (kb_acc){};
-      c1 = (kb_acc){};
       const unsigned char* rp = rowp + ct * 32 * RB;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -1717,25 +1753,27 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
         const kb_bf8 bh = *(const kb_bf8*)(rp + 32 * ks);
         const kb_bf8 bl = *(const kb_bf8*)(rp + 2 * D + 32 * ks);
 #endif
-        kb_acc& c = (KS_CHAINS == 2 && ks >= KS / 2) ? c1 : c0;
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bh, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bl, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ks], bh, c, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bh, c0, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bl, c0, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ks], bh, c0, 0, 0, 0);
       }
-    };
-    // fold tile ct's a' = fl(cc - 2S), tagged with ct, into the running top-2
-    auto fold = [&](int ct, const kb_acc& c0, const kb_acc& c1, float cc) {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const float sq = KS_CHAINS == 2 ? c0[q] + c1[q] : c0[q];
-#ifdef KS_DEV_NOEPI  // timing split only; never set in the product build
-        lo[q] = ks_min(lo[q], sq);
-#else
-        const float v = ks_tag(__builtin_fmaf(-2.f, sq, cc), (unsigned int)ct);
-        sec[q] = ks_med3(v, lo[q], sec[q]);
-        lo[q] = ks_min(lo[q], v);
+#ifndef KS_DEV_CCVALU
+      c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, *(const kb_bf8*)(rp + 4 * D), c0, 0, 0, 0);
 #endif
-      }
+    };
+    // fold tile ct's acc, tagged with ct, into the running top-2 (3 VALU per
+    // value: the a' = cc - 2S fma of the earlier form is the MFMA step above)
+    auto fold1 = [&](int q, int ct, float acc) {
+#ifdef KS_DEV_CCVALU  // dev A/B only: -cc/2 added on the VALU instead of the MFMA step
+      acc = acc + -0.5f * cnf[ct * 32 + r];
+#endif
+      const float v = ks_tag(acc, (unsigned int)ct);
+      sec[q] = ks_med3(v, lo[q], sec[q]);
+      lo[q] = ks_max(lo[q], v);
+    };
+    auto fold = [&](int ct, const kb_acc& c0) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) fold1(q, ct, c0[q]);
     };
 #if KS_PIPE
     // software pipeline: tile ct's fold (VALU) is independent of tile ct+1's
@@ -1743,78 +1781,75 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
     // previous tile is written into the k-loop of the next tile's chain (16 / KS
     // values per k-step) and the sched barriers keep each region to one chain
     // + one fold (the scheduler otherwise hoists both tiles' B reads: spills).
-    auto chain_fold = [&](int ct, kb_acc& c0, kb_acc& c1, int pct, const kb_acc& p0, const kb_acc& p1, float pcc) {
+    auto chain_fold = [&](int ct, kb_acc& c0, int pct, const kb_acc& p0) {
       c0 = (kb_acc){};
-      c1 = (kb_acc){};
       const unsigned char* rp = rowp + ct * 32 * RB;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         const kb_bf8 bh = *(const kb_bf8*)(rp + 32 * ks);
         const kb_bf8 bl = *(const kb_bf8*)(rp + 2 * D + 32 * ks);
-        kb_acc& c = (KS_CHAINS == 2 && ks >= KS / 2) ? c1 : c0;
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bh, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bl, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ks], bh, c, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bh, c0, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bl, c0, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ks], bh, c0, 0, 0, 0);
 #pragma unroll
-        for (int qq = 0; qq < 16 / KS; ++qq) {
-          const int q = ks * (16 / KS) + qq;
-          const float sq = KS_CHAINS == 2 ? p0[q] + p1[q] : p0[q];
-#if defined(KS_DEV_NOFMA)  // timing split only; never set in the product build
-          const float v = ks_tag(sq, (unsigned int)pct);
-#elif defined(KS_DEV_NOTAG)  // timing split only; never set in the product build
-          const float v = __builtin_fmaf(-2.f, sq, pcc);
-#else
-          const float v = ks_tag(__builtin_fmaf(-2.f, sq, pcc), (unsigned int)pct);
-#endif
-          sec[q] = ks_med3(v, lo[q], sec[q]);
-          lo[q] = ks_min(lo[q], v);
-        }
+        for (int qq = 0; qq < 16 / KS; ++qq) fold1(ks * (16 / KS) + qq, pct, p0[ks * (16 / KS) + qq]);
       }
+#ifndef KS_DEV_CCVALU
+      c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, *(const kb_bf8*)(rp + 4 * D), c0, 0, 0, 0);
+#endif
     };
     {
-      kb_acc a0, a1, b0, b1;
-      chain(0, a0, a1);
+      kb_acc a0, b0;
+      chain(0, a0);
       if constexpr (NCT == 1) {
-        fold(0, a0, a1, cns[r]);
+        fold(0, a0);
       } else {
 #pragma unroll 1
         for (int cp = 0; cp < NCT - 2; cp += 2) {
-          chain_fold(cp + 1, b0, b1, cp, a0, a1, cns[cp * 32 + r]);
+          chain_fold(cp + 1, b0, cp, a0);
           __builtin_amdgcn_sched_barrier(0);
-          chain_fold(cp + 2, a0, a1, cp + 1, b0, b1, cns[(cp + 1) * 32 + r]);
+          chain_fold(cp + 2, a0, cp + 1, b0);
           __builtin_amdgcn_sched_barrier(0);
         }
-        chain_fold(NCT - 1, b0, b1, NCT - 2, a0, a1, cns[(NCT - 2) * 32 + r]);
+        chain_fold(NCT - 1, b0, NCT - 2, a0);
         __builtin_amdgcn_sched_barrier(0);
-        fold(NCT - 1, b0, b1, cns[(NCT - 1) * 32 + r]);
+        fold(NCT - 1, b0);
       }
     }
 #else
 #pragma unroll 1
     for (int ct = 0; ct < NCT; ++ct) {  // rolled: bounds the scheduler's window (and the LDS reads it hoists)
-      kb_acc c0, c1;
-      chain(ct, c0, c1);
-      fold(ct, c0, c1, cns[ct * 32 + r]);
+      kb_acc c0;
+      chain(ct, c0);
+      fold(ct, c0);
     }
 #endif
-    float lo0[16];  // this lane's minimum per register (its centre r over all tiles)
+    float lo0[16];  // this lane's best per register (its centre r over all tiles)
 #pragma unroll
     for (int q = 0; q < 16; ++q) lo0[q] = lo[q];
     ks_top2_vals(lo, sec, lane);
-    // the centre of each row's minimum: lane (h, 2q) holds row rt(q, h)'s
-    // b1; the lowest lane of that half whose own minimum equals it is the
+    // the centre of each row's best: lane (h, 2q) holds row rt(q, h)'s
+    // b1; the lowest lane of that half whose own best equals it is the
     // centre r (ties in the tagged value share the tile, so the lowest r is
     // the lowest centre index, the first occurrence)
+    // (branch-free: the ballot's first set bit goes straight into lane 2q /
+    // 32 + 2q by writelane; a row always matches in its own half, so the
+    // empty-mask case never decides a label)
     int rmin = 0;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
+    auto rmin_q = [&](auto qc) {
+      constexpr int q = decltype(qc)::value;
       const float b0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lo[0]), 2 * q));
       const float b1h = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lo[0]), 32 + 2 * q));
       const unsigned long long m = __ballot(lo0[q] == (h ? b1h : b0));
-      const unsigned int m0 = (unsigned int)m, m1 = (unsigned int)(m >> 32);
-      const int r0 = m0 ? __builtin_ctz(m0) : 0, r1 = m1 ? __builtin_ctz(m1) : 0;
-      if (r == 2 * q) rmin = h ? r1 : r0;
-    }
+      const int r0 = __builtin_ctz((unsigned int)m | 0x80000000u);
+      const int r1 = __builtin_ctz((unsigned int)(m >> 32) | 0x80000000u);
+      // lane selects are inline constants (no SGPR lane-select hazard)
+      int v = rmin;
+      asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(r0), "n"(2 * q));
+      asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(r1), "n"(32 + 2 * q));
+      rmin = v;
+    };
+    ks_unroll(rmin_q, std::make_integer_sequence<int, 16>{});
     p2 += __shfl_xor(p2, 32, 64);  // row r's |p|^2 in lanes r and r + 32
     // one decision per row, by the even lane of its pair (as in k_kmeans_filter_b3)
     const int q = r >> 1;
@@ -1826,11 +1861,14 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
     // the bound in fp32 (kc_coef): |p| from the fp32 sum of squares with
     // slack for its rounding and for underflowed squares, e(|p|) by two fmas,
     // each rounding priced by the 1.0001 factors
-    const float pn = sqrtf(__builtin_fmaf(p2f, 1.001f, 1e-37f)) * 1.0001f;
+    // (v_sqrt_f32 directly: its ~1 ulp is inside the 1.0001 slack, and the
+    // argument is >= 1e-37, a normal number)
+    const float pn = __builtin_amdgcn_sqrtf(__builtin_fmaf(p2f, 1.001f, 1e-37f)) * 1.0001f;
     const float e = __builtin_fmaf(__builtin_fmaf(kq[2], pn, kq[1]), pn, kq[0]) * 1.0001f;
     const bool live = grow < N && (r & 1) == 0;
     const bool fin = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim && isfinite(b1) && isfinite(b2);
-    const bool dec = fin && b2 - b1 > 2.0f * 1.0001f * e;
+    // acc = -a'/2: a' gap > 2e  <=>  acc gap b1 - b2 > e
+    const bool dec = fin && b1 - b2 > 1.0001f * e;
     if (live && dec) labels[grow] = i1;
     if (live && !fin) full_list[atomicAdd(&counters[0], 1u)] = grow;
     const bool needc = live && fin && !dec;
