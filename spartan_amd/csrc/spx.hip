@@ -1078,13 +1078,17 @@ typedef float kb_f4 __attribute__((ext_vector_type(4)));
 // One block of 1024 threads: mu from 8 column partial sums per dimension
 // (combined in a fixed order), then one wave per centre (lane = dimension,
 // coalesced), wave-reduced |c'|^2 and mu.c' in a fixed shuffle order.
+// For the fp16 screen (k_kmeans_filter_as MODE 1, which centres the points as
+// well): cnf2[c] = (float)|c'|^2, muf = mu, cmax[3] = max_c |c' - fp16(hi + lo)|
+// (the screen's own rounding of each centre, measured exactly).
 __global__ __launch_bounds__(1024) void k_kmeans_prep_b3(i64 D, i64 K, i64 Kp, const double* __restrict__ C,
                                                          __bf16* __restrict__ CBh, __bf16* __restrict__ CBl,
                                                          float* __restrict__ cnf, double* __restrict__ cmax,
-                                                         double mcoef) {
+                                                         double mcoef, float* __restrict__ cnf2,
+                                                         float* __restrict__ muf) {
   __shared__ double part[8][KB_DMAX];
   __shared__ float mus[KB_DMAX];
-  __shared__ double red[16];
+  __shared__ double red[16], redc[16];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   for (int i = t; i < 8 * (int)D; i += 1024) {
     const int d = i % (int)D, g = i / (int)D;
@@ -1097,34 +1101,46 @@ __global__ __launch_bounds__(1024) void k_kmeans_prep_b3(i64 D, i64 K, i64 Kp, c
     double m = 0.0;
     for (int g = 0; g < 8; ++g) m += part[g][t];
     mus[t] = (float)(m / (double)K);
+    muf[t] = mus[t];
   }
   __syncthreads();
-  double mx = 0.0;
+  double mx = 0.0, mdc = 0.0;
   for (i64 c = w; c < Kp; c += 16) {
-    double s = 0.0, sm = 0.0;
+    double s = 0.0, sm = 0.0, dc = 0.0;
     for (int d = lane; d < D; d += 64) {
       const double v = c < K ? C[c * D + d] - (double)mus[d] : 0.0;
       const float v32 = (float)v;
       const __bf16 hi = (__bf16)v32;
+      const __bf16 lo = (__bf16)(v32 - (float)hi);
       CBh[c * D + d] = hi;
-      CBl[c * D + d] = (__bf16)(v32 - (float)hi);
+      CBl[c * D + d] = lo;
+      // the screen's fp16 centre (staged as fp16(hi + lo)) against the fp32 c'
+      const double e16 = (double)v32 - (double)(float)(_Float16)((float)hi + (float)lo);
       s += v * v;
       sm += (double)mus[d] * v;
+      dc += e16 * e16;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       s += __shfl_xor(s, o, 64);
       sm += __shfl_xor(sm, o, 64);
+      dc += __shfl_xor(dc, o, 64);
     }
     // padding centres: a huge FINITE cc (the filter tags a' mantissa bits,
     // which would turn +inf into NaN); they never win, and a lone real centre
     // is certified against them
     if (lane == 0) cnf[c] = c < K ? (float)(s + 2.0 * sm) : 3.0e38f;
+    if (lane == 0) cnf2[c] = c < K ? (float)s : 3.0e38f;
     if (c < K) mx = (s > mx || s != s) ? s : mx;
+    if (c < K) mdc = (dc > mdc || dc != dc) ? dc : mdc;
   }
   if (lane == 0) red[w] = mx;
+  if (lane == 0) redc[w] = mdc;
   __syncthreads();
   if (t == 0) {
+    double mc = redc[0];
+    for (int k = 1; k < 16; ++k) mc = (redc[k] > mc || redc[k] != redc[k]) ? redc[k] : mc;
+    cmax[3] = sqrt(mc) * 1.001;
     double m = red[0];
     for (int k = 1; k < 16; ++k) m = (red[k] > m || red[k] != red[k]) ? red[k] : m;
     double mn = 0.0;
@@ -1537,8 +1553,15 @@ constexpr int KS_WAVES = KS_WAVES_CFG;
 // banks, so the 16-lane groups of a ds_read_b128 (rows 0-3, 12-15, 20-27 ...)
 // hit 16 distinct 4-bank quads, and every read of a tile's k-loop is one base
 // register + an immediate.
-__host__ __device__ constexpr int ks_row_bytes(int D) { return 4 * D + 48; }
-static size_t ks_lds_bytes(i64 D, int nct) { return (size_t)32 * nct * ks_row_bytes((int)D); }
+// MODE 1 (the fp16 screen below): [hi: D fp16][-cc/2 as 3 bf16 + 5 zeros][8
+// zero bf16][16-byte pad], 2 D + 48 bytes: also an odd multiple of 4 banks
+// for D = 64 and 128, so conflict-free the same way.
+__host__ __device__ constexpr int ks_row_bytes(int D, int mode = 0) { return (mode == 0 ? 4 : 2) * D + 48; }
+// (MODE 1 adds the D fp32 centre mean after the rows)
+static size_t ks_lds_bytes(i64 D, int nct, int mode = 0) {
+  return (size_t)32 * nct * ks_row_bytes((int)D, mode) + (mode == 1 ? 4 * D : 0);
+}
+typedef _Float16 kh_f8 __attribute__((ext_vector_type(8)));
 
 // Plain v_med3_f32 / v_max_f32: fmaxf / fmed3 on values built by bit
 // operations make the compiler canonicalize every operand first (a v_max_f32
@@ -1615,7 +1638,21 @@ __device__ __forceinline__ void ks_unroll(F&& f, std::integer_sequence<int, Q...
   (f(std::integral_constant<int, Q>{}), ...);
 }
 
-template <int NCT, int KS>
+// MODE 0: the bf16x3 filter described above.  MODE 1: the fp16 screen -- the
+// same sweep with ONE v_mfma_f32_32x32x16_f16 per k-step, a third of the
+// MFMAs and no lo split.  The screen centres the points too: it ranks by
+// a'' = |c'|^2 - 2 x'.c' with x' = fl(x - mu) (= |x - c|^2 - |x - mu|^2 up
+// to the roundings priced below), so its error scales with |x - mu| instead
+// of |x|; x' and c' are rounded to fp16 (11 significant bits): x' within
+// 2^-11 |x'| (+ 2^-25 per component below the fp16 normal range), c' within
+// the measured dcmax = max_c |c' - fp16(c')| (k_kmeans_prep_b3).  Its bound
+// is still several times bf16x3's, so a few % of cfg3's rows stay
+// undecided; they go to a row list that the MODE 0 kernel re-runs in list
+// mode (rows_in / nrows_in: slot s of the list plays the role of row s).
+// In MODE 1 rows the screen cannot evaluate (non-finite values, fp16
+// overflow, cmax beyond the fp16 range) are undecided too: the MODE 0 pass
+// routes them.  cnf is |c'|^2 (cnf2 of the prep) in MODE 1.
+template <int NCT, int KS, int MODE>
 __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const float* __restrict__ P, i64 ldp,
                                                                     const __bf16* __restrict__ CBh,
                                                                     const __bf16* __restrict__ CBl,
@@ -1623,22 +1660,38 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
                                                                     const double* cmax_p, i64* __restrict__ labels,
                                                                     unsigned int* __restrict__ counters,
                                                                     i64* __restrict__ full_list,
-                                                                    i64* __restrict__ und_list) {
+                                                                    unsigned long long* __restrict__ und_mask,
+                                                                    const i64* __restrict__ rows_in,
+                                                                    const unsigned int* __restrict__ nrows_in,
+                                                                    const float* __restrict__ muf) {
   extern __shared__ __attribute__((aligned(16))) unsigned char kb_lds[];
-  constexpr int NC = 32 * NCT, D = 16 * KS, RB = ks_row_bytes(D);
+  constexpr int NC = 32 * NCT, D = 16 * KS, RB = ks_row_bytes(D, MODE);
+  constexpr int CCOFF = MODE == 0 ? 4 * D : 2 * D;  // byte offset of the -cc/2 pieces in a row
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, h = lane >> 5;
   {
     // centre rows in the permuted k order of k_kmeans_filter_b3 (dim quads
     // 1 and 2 of every 16-dim step swapped: an A lane's two 16-byte loads
     // are adjacent in its row)
     typedef unsigned int kb_u2 __attribute__((ext_vector_type(2)));
+    typedef __bf16 kb_b4 __attribute__((ext_vector_type(4)));
+    typedef _Float16 kh_f4 __attribute__((ext_vector_type(4)));
     constexpr int D4 = D / 4;
     for (int i = t; i < NC * D4; i += KS_WAVES * 64) {
       const int c = i / D4, q = i % D4, qi = q & 3;
       const int pq = (q & ~3) | (qi == 1 ? 2 : qi == 2 ? 1 : qi);
       unsigned char* row = kb_lds + c * RB;
-      *(kb_u2*)(row + 8 * pq) = *(const kb_u2*)&CBh[(i64)c * D + 4 * q];
-      *(kb_u2*)(row + 2 * D + 8 * pq) = *(const kb_u2*)&CBl[(i64)c * D + 4 * q];
+      if constexpr (MODE == 0) {
+        *(kb_u2*)(row + 8 * pq) = *(const kb_u2*)&CBh[(i64)c * D + 4 * q];
+        *(kb_u2*)(row + 2 * D + 8 * pq) = *(const kb_u2*)&CBl[(i64)c * D + 4 * q];
+      } else {
+        // fp16(hi + lo): hi + lo is c' to 2^-16 (priced in the bound)
+        const kb_b4 bh = *(const kb_b4*)&CBh[(i64)c * D + 4 * q];
+        const kb_b4 bl = *(const kb_b4*)&CBl[(i64)c * D + 4 * q];
+        kh_f4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (_Float16)((float)bh[j] + (float)bl[j]);
+        *(kh_f4*)(row + 8 * pq) = v;
+      }
     }
     // -cc/2 split exactly into three bf16 (8 + 8 + 8 significant bits of
     // the fp32 value), for the k-step that adds it on the MFMA (lanes of the
@@ -1651,8 +1704,12 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
       const __bf16 b3 = (__bf16)(v1 - (float)b2);
       const __bf16 z = (__bf16)0.f;
       unsigned char* row = kb_lds + i * RB;
-      *(kb_bf8*)(row + 4 * D) = (kb_bf8){b1, b2, b3, z, z, z, z, z};
-      *(kb_bf8*)(row + 4 * D + 16) = (kb_bf8){z, z, z, z, z, z, z, z};
+      *(kb_bf8*)(row + CCOFF) = (kb_bf8){b1, b2, b3, z, z, z, z, z};
+      *(kb_bf8*)(row + CCOFF + 16) = (kb_bf8){z, z, z, z, z, z, z, z};
+    }
+    if constexpr (MODE == 1) {
+      float* mul = (float*)(kb_lds + NC * RB);
+      for (int i = t; i < D; i += KS_WAVES * 64) mul[i] = muf[i];
     }
   }
   __syncthreads();
@@ -1662,26 +1719,47 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
   // round to one value; the margin is folded into e (gap > 2e + margin)
   const double mcoef = cmax_p[1], mun = cmax_p[2];
   const double u32 = 5.9604644775390625e-08;
-  // one accumulator chain: 48 products per k-step over KS k-steps
-  const double chain = 48.0 * (double)KS;
-  const double eS = (u32 + 3.1 * 3.814697265625e-06 + 2.0 * (chain + 3.0) * u32) * 1.01 * cmax;
+  // one accumulator chain: 48 (bf16x3) or 16 (fp16) products per k-step
+  // over KS k-steps
+  const double chain = (MODE == 0 ? 48.0 : 16.0) * (double)KS;
+  // error of x.c' per |x|: bf16x3 (u + 3.1 * 2^-18 + chain) cmax.  fp16
+  // screen, per |x'|: u cmax (x' = fl(x - mu)) + 2^-11 cmax (x' to fp16) +
+  // 1.001 dcmax (c' to fp16, measured) + the chain over |xh| |ch| <=
+  // 1.001 |x'| (cmax + dcmax)
+  const double dcmax = MODE == 1 ? cmax_p[3] : 0.0;
+  const double eS = MODE == 0 ? (u32 + 3.1 * 3.814697265625e-06 + 2.0 * (chain + 3.0) * u32) * 1.01 * cmax
+                              : (u32 * cmax + 4.8828125e-04 * cmax + 1.001 * dcmax +
+                                 2.0 * (chain + 3.0) * u32 * 1.001 * (cmax + dcmax)) * 1.01;
   float kq[3];
   // the chain ends with one MFMA that adds -cc/2 (three nonzero products):
   // its roundings, at most 16 of <= 2u |S - cc/2 + ...| each, priced in a'
   // units as 64u |p| cmax + 32u (cmax^2 + 2|mu| cmax); the fma a' = cc - 2S
   // is gone, and the tile tag on the accumulator (7 ulp of |S - cc/2|, i.e.
-  // 14 eps (|p| cmax + cm2 / 2) in a' units) stays inside kc_coef's 8 eps amax
-  kc_coef(eS, cmax, mun, mcoef, D, kq, 64.0 * u32 * cmax, 32.0 * u32 * (cmax * cmax + 2.0 * mun * cmax));
-  // no overflow in S or a' (every a' finite): |p| cmax, cmax^2, |mu| cmax < 1e36
-  const bool cok = cmax * cmax < 1e36 && mun * cmax < 1e36;
+  // 14 eps (|p| cmax + cm2 / 2) in a' units) stays inside kc_coef's 8 eps amax.
+  // fp16 underflow of x' (MODE 1): each rounded component is off by at most
+  // 2^-25 absolute besides the relative 2^-11, i.e. 2^-25 sqrt(D) (cmax +
+  // dcmax) + D 2^-50 on S (dcmax already holds the centres' underflow),
+  // doubled in a'' units with slack.  The a'' form (|c'|^2 instead of cc)
+  // and |x - c| <= |x'| + cmax keep every other term of kc_coef an upper
+  // bound with |p| = |x'|.
+  double xk1 = 64.0 * u32 * cmax, xk0 = 32.0 * u32 * (cmax * cmax + 2.0 * mun * cmax);
+  if constexpr (MODE == 1)
+    xk0 += sqrt((double)D) * 1.1920928955078125e-07 * (cmax + dcmax) + (double)D * 3.552713678800501e-15;
+  kc_coef(eS, cmax, mun, mcoef, D, kq, xk1, xk0);
+  // no overflow in S or a' (every a' finite): |p| cmax, cmax^2, |mu| cmax < 1e36;
+  // MODE 1: every fp16 centre component finite (|c'_d| <= cmax < 3e4)
+  const bool cok = cmax * cmax < 1e36 && mun * cmax < 1e36 && (MODE == 0 || (cmax < 3.0e4 && dcmax == dcmax));
   const float pn_lim = (float)(cmax > 0.0 ? 1e36 / cmax : 1e36);
-  const i64 ntiles = (N + 31) / 32;
+  // list mode: slot s < nrows stands for row rows_in[s]
+  const i64 nlim = rows_in ? (i64)*nrows_in : N;
+  const i64 ntiles = (nlim + 31) / 32;
   const i64 stride = (i64)gridDim.x * KS_WAVES;
   i64 tile = (i64)blockIdx.x * KS_WAVES + w;
   kb_f4 ra[KS][2];
   auto load = [&](i64 tl) {
     i64 row = tl * 32 + r;
-    row = row < N ? row : N - 1;
+    row = row < nlim ? row : nlim - 1;
+    if (rows_in) row = rows_in[row];
 #ifdef KS_DEV_NOGLOBAL  // timing split only (tools/km_modes.py dev builds); never set in the product build
     row = r;
 #endif
@@ -1699,18 +1777,32 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
 #if !KS_PREFETCH
     load(tile);  // the partner wave's sweep covers the latency
 #endif
-    kb_bf8 ah[KS], al[KS];
+    using AT = std::conditional_t<MODE == 0, kb_bf8, kh_f8>;
+    AT ah[KS];
+    kb_bf8 al[MODE == 0 ? KS : 1];
     // |p|^2 only feeds the bound (x 1.001 slack): four independent partial
     // chains instead of one 64-deep dependent fma chain
     float p2q[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (MODE == 1) {  // x' = x - mu, mu read from LDS in the lane's dim order
+      const float* mul = (const float*)(kb_lds + NC * RB) + 4 * h;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        ra[ks][0] -= *(const kb_f4*)(mul + ks * 16);
+        ra[ks][1] -= *(const kb_f4*)(mul + ks * 16 + 8);
+      }
+    }
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float x = j < 4 ? ra[ks][0][j] : ra[ks][1][j - 4];
         p2q[j & 3] = __builtin_fmaf(x, x, p2q[j & 3]);
-        ah[ks][j] = (__bf16)x;
-        al[ks][j] = (__bf16)(x - (float)ah[ks][j]);
+        if constexpr (MODE == 0) {
+          ah[ks][j] = (__bf16)x;
+          al[ks][j] = (__bf16)(x - (float)ah[ks][j]);
+        } else {
+          ah[ks][j] = (_Float16)x;
+        }
       }
     }
     float p2 = (p2q[0] + p2q[1]) + (p2q[2] + p2q[3]);
@@ -1741,24 +1833,27 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
     const kb_bf8 a_one = (kb_bf8){one, one, one, one, one, one, one, one};
     // one centre tile: 3 KS MFMAs of x.c' in one chain, then the -cc/2 step
     // LAST (so only its own roundings see |cc|: the bound in kc_coef)
+    // k-step ks of x.c' for the centre tile at rp: three bf16 MFMAs (MODE 0)
+    // or one fp16 MFMA (MODE 1)
+    auto kstep = [&](int ks, const unsigned char* rp, kb_acc& c0) {
+      if constexpr (MODE == 0) {
+        const kb_bf8 bh = *(const kb_bf8*)(rp + 32 * ks);
+        const kb_bf8 bl = *(const kb_bf8*)(rp + 2 * D + 32 * ks);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bh, c0, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bl, c0, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ks], bh, c0, 0, 0, 0);
+      } else {
+        const kh_f8 bh = *(const kh_f8*)(rp + 32 * ks);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bh, c0, 0, 0, 0);
+      }
+    };
     auto chain = [&](int ct, kb_acc& c0) {
       c0 = (kb_acc){};
       const unsigned char* rp = rowp + ct * 32 * RB;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-#ifdef KS_DEV_NOLDS  // timing split only; never set in the product build
-        kb_bf8 bh = ah[(ks + ct) % KS], bl = al[(ks + 3 * ct) % KS];
-        bh[0] = (__bf16)(float)ct;
-#else
-        const kb_bf8 bh = *(const kb_bf8*)(rp + 32 * ks);
-        const kb_bf8 bl = *(const kb_bf8*)(rp + 2 * D + 32 * ks);
-#endif
-        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bh, c0, 0, 0, 0);
-        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bl, c0, 0, 0, 0);
-        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ks], bh, c0, 0, 0, 0);
-      }
+      for (int ks = 0; ks < KS; ++ks) kstep(ks, rp, c0);
 #ifndef KS_DEV_CCVALU
-      c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, *(const kb_bf8*)(rp + 4 * D), c0, 0, 0, 0);
+      c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, *(const kb_bf8*)(rp + CCOFF), c0, 0, 0, 0);
 #endif
     };
     // fold tile ct's acc, tagged with ct, into the running top-2 (3 VALU per
@@ -1786,16 +1881,12 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
       const unsigned char* rp = rowp + ct * 32 * RB;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        const kb_bf8 bh = *(const kb_bf8*)(rp + 32 * ks);
-        const kb_bf8 bl = *(const kb_bf8*)(rp + 2 * D + 32 * ks);
-        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bh, c0, 0, 0, 0);
-        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ks], bl, c0, 0, 0, 0);
-        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ks], bh, c0, 0, 0, 0);
+        kstep(ks, rp, c0);
 #pragma unroll
         for (int qq = 0; qq < 16 / KS; ++qq) fold1(ks * (16 / KS) + qq, pct, p0[ks * (16 / KS) + qq]);
       }
 #ifndef KS_DEV_CCVALU
-      c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, *(const kb_bf8*)(rp + 4 * D), c0, 0, 0, 0);
+      c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, *(const kb_bf8*)(rp + CCOFF), c0, 0, 0, 0);
 #endif
     };
     {
@@ -1854,7 +1945,9 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
     // one decision per row, by the even lane of its pair (as in k_kmeans_filter_b3)
     const int q = r >> 1;
     const int rt = (q & 3) + 8 * (q >> 2) + 4 * h;
-    const i64 grow = tile * 32 + rt;
+    const i64 slot = tile * 32 + rt;
+    const bool live = slot < nlim && (r & 1) == 0;
+    const i64 grow = rows_in ? (live ? rows_in[slot] : 0) : slot;
     const float b1 = lo[0], b2 = sec[0];
     const int i1 = 32 * (int)(__builtin_bit_cast(unsigned int, b1) & 7u) + rmin;
     const float p2f = __shfl(p2, rt, 64);
@@ -1865,44 +1958,99 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
     // argument is >= 1e-37, a normal number)
     const float pn = __builtin_amdgcn_sqrtf(__builtin_fmaf(p2f, 1.001f, 1e-37f)) * 1.0001f;
     const float e = __builtin_fmaf(__builtin_fmaf(kq[2], pn, kq[1]), pn, kq[0]) * 1.0001f;
-    const bool live = grow < N && (r & 1) == 0;
     const bool fin = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim && isfinite(b1) && isfinite(b2);
     // acc = -a'/2: a' gap > 2e  <=>  acc gap b1 - b2 > e
     const bool dec = fin && b1 - b2 > 1.0001f * e;
     if (live && dec) labels[grow] = i1;
-    if (live && !fin) full_list[atomicAdd(&counters[0], 1u)] = grow;
-    const bool needc = live && fin && !dec;
+    if (MODE == 0 && live && !fin) full_list[atomicAdd(&counters[0], 1u)] = grow;
+    const bool needc = live && !dec && (MODE == 1 || fin);
+    // the tile's undecided rows as one lane mask, compacted into a row list
+    // by k_ks_compact (one global atomic per tile on a single counter
+    // serialised at its L2 channel: 31 ms for the screen's 3.1 M tiles)
     const unsigned long long und = __ballot(needc);
-    if (und) {  // wave-uniform: one slot range per wave
-      unsigned int base = 0;
-      if (lane == 0) base = atomicAdd(&counters[2], (unsigned int)__popcll(und));
-      base = __builtin_amdgcn_readfirstlane(base);
-      if (needc) und_list[base + (unsigned int)__popcll(und & ((1ull << lane) - 1ull))] = grow;
-    }
+    if (lane == 0) und_mask[tile] = und;
   }
 }
 
-template <int NCT, int KS>
+// Row list of the undecided rows from the per-tile lane masks of
+// k_kmeans_filter_as (bit l: lane (h, r) = (l >> 5, l & 31) decided row rt(r >> 1, h)
+// of the tile); rows_in: the tile slots stand for rows_in[slot].  One thread
+// per tile, one atomic per block for the block's range.
+__global__ __launch_bounds__(256) void k_ks_compact(i64 N, const unsigned long long* __restrict__ mask,
+                                                    const i64* __restrict__ rows_in,
+                                                    const unsigned int* __restrict__ nrows_in, i64* __restrict__ out,
+                                                    unsigned int* __restrict__ cnt) {
+  __shared__ unsigned int wsum[4];
+  __shared__ unsigned int base;
+  const i64 nlim = rows_in ? (i64)*nrows_in : N;
+  const i64 ntiles = (nlim + 31) / 32;
+  const i64 tl = (i64)blockIdx.x * 256 + threadIdx.x;
+  if ((i64)blockIdx.x * 256 >= ntiles) return;  // block-uniform
+  const unsigned long long m = tl < ntiles ? mask[tl] : 0ull;
+  const unsigned int n = (unsigned int)__popcll(m);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned int inc = n;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned int v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) base = atomicAdd(cnt, wsum[0] + wsum[1] + wsum[2] + wsum[3]);
+  __syncthreads();
+  unsigned int pos = base + inc - n;
+  for (int k = 0; k < w; ++k) pos += wsum[k];
+  unsigned long long mm = m;
+  while (mm) {
+    const int l = __builtin_ctzll(mm);
+    mm &= mm - 1;
+    const int q = (l & 31) >> 1, h = l >> 5;
+    const i64 slot = tl * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+    out[pos++] = rows_in ? rows_in[slot] : slot;
+  }
+}
+
+template <int NCT, int KS, int MODE>
 static void ks_launch(hipStream_t s, i64 N, const float* P, i64 ldp, const __bf16* CBh, const __bf16* CBl,
                       const float* cnf, const double* cmax, i64* labels, unsigned int* counters, i64* full_list,
-                      i64* und_list, int grid) {
-  const size_t lds = ks_lds_bytes(16 * KS, NCT);
+                      unsigned long long* und_mask, const i64* rows_in, const unsigned int* nrows_in,
+                      const float* muf, int grid) {
+  const size_t lds = ks_lds_bytes(16 * KS, NCT, MODE);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_kmeans_filter_as<NCT, KS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)ks_lds_bytes(KB_DMAX, 8));
+    (void)hipFuncSetAttribute((const void*)k_kmeans_filter_as<NCT, KS, MODE>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)ks_lds_bytes(KB_DMAX, 8));
     attr = true;
   }
-  k_kmeans_filter_as<NCT, KS><<<grid, KS_WAVES * 64, lds, s>>>(N, P, ldp, CBh, CBl, cnf, cmax, labels, counters,
-                                                               full_list, und_list);
+  k_kmeans_filter_as<NCT, KS, MODE><<<grid, KS_WAVES * 64, lds, s>>>(N, P, ldp, CBh, CBl, cnf, cmax, labels, counters,
+                                                                     full_list, und_mask, rows_in, nrows_in, muf);
 }
 
-template <int NCT>
+template <int NCT, int MODE>
 static void ks_launch_d(hipStream_t s, i64 N, i64 D, const float* P, i64 ldp, const __bf16* CBh, const __bf16* CBl,
                         const float* cnf, const double* cmax, i64* labels, unsigned int* counters, i64* full_list,
-                        i64* und_list, int grid) {
-  if (D == 64) ks_launch<NCT, 4>(s, N, P, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_list, grid);
-  else ks_launch<NCT, 8>(s, N, P, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_list, grid);
+                        unsigned long long* und_mask, const i64* rows_in, const unsigned int* nrows_in,
+                        const float* muf, int grid) {
+  if (D == 64)
+    ks_launch<NCT, 4, MODE>(s, N, P, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_mask, rows_in,
+                            nrows_in, muf, grid);
+  else
+    ks_launch<NCT, 8, MODE>(s, N, P, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_mask, rows_in,
+                            nrows_in, muf, grid);
+}
+
+template <int MODE>
+static void ks_launch_n(int nct, hipStream_t s, i64 N, i64 D, const float* P, i64 ldp, const __bf16* CBh,
+                        const __bf16* CBl, const float* cnf, const double* cmax, i64* labels, unsigned int* counters,
+                        i64* full_list, unsigned long long* und_mask, const i64* rows_in,
+                        const unsigned int* nrows_in, const float* muf, int grid) {
+  switch (nct) {
+    case 1: ks_launch_d<1, MODE>(s, N, D, P, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_mask, rows_in, nrows_in, muf, grid); break;
+    case 2: ks_launch_d<2, MODE>(s, N, D, P, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_mask, rows_in, nrows_in, muf, grid); break;
+    case 4: ks_launch_d<4, MODE>(s, N, D, P, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_mask, rows_in, nrows_in, muf, grid); break;
+    default: ks_launch_d<8, MODE>(s, N, D, P, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_mask, rows_in, nrows_in, muf, grid); break;
+  }
 }
 
 // Exact-order labels of the undecided points from their candidate masks
@@ -2250,12 +2398,17 @@ static void ka_grid(int dtype, i64 N, i64 D, i64 K, i64* G, i64* ndb, i64* ncb) 
 
 static i64 kf_kp(i64 K) { return (K + KF_BN - 1) / KF_BN * KF_BN; }
 
-// SPX_KMEANS_FILTER=b3 selects the single all-accumulator filter pass (A/B
-// timing and the bit-exactness cross-check in the GPU tests); default: the
-// A-stationary pass + list-mode candidates
+// SPX_KMEANS_FILTER selects the first passes (A/B timing and the
+// bit-exactness cross-checks in the GPU tests): "b3" the single
+// all-accumulator filter pass; "as" the A-stationary bf16x3 pass over every
+// row; default: the fp16 screen over every row, the A-stationary bf16x3 pass
+// over its undecided rows.  All of them end in the list-mode all-accumulator
+// pass (candidate masks), k_kmeans_cand and the exact kernel.
 static int kmeans_filter_mode() {
   const char* v = getenv("SPX_KMEANS_FILTER");
-  return (v && strcmp(v, "b3") == 0) ? 1 : 0;
+  if (v && strcmp(v, "b3") == 0) return 1;
+  if (v && strcmp(v, "as") == 0) return 2;
+  return 0;
 }
 
 static int kf_persistent_grid(i64 N) {
@@ -2267,9 +2420,10 @@ extern "C" int64_t spx_kmeans_assign_workspace(int dtype, int64_t N, int64_t D, 
   if ((dtype != SPX_F32 && dtype != SPX_F64) || N < 0 || D < 1 || K < 1) return -1;
   const i64 Kp = kf_kp(K);
   // CT (D x Kp f32) | cn (Kp f64) | cmax | counters | full list (N i64) | candidate list (N KfCand, K <= 256)
-  // | undecided-row list (N i64, K <= 256)
+  // | undecided-row list (N i64, K <= 256) | screen's undecided-row list (N i64, K <= 256)
+  // | per-tile undecided lane masks (ceil(N / 32) u64, K <= 256) | centre mean (D f32, K <= 256)
   return (D * Kp * 4 + 15) / 16 * 16 + Kp * 8 + 32 + 16 + N * 8 +
-         (Kp == KF_BN ? N * (i64)sizeof(KfCand) + N * 8 : 0);
+         (Kp == KF_BN ? N * (i64)sizeof(KfCand) + 2 * N * 8 + (N + 31) / 32 * 8 + D * 4 : 0);
 }
 
 extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
@@ -2312,7 +2466,11 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
   ws += N * 8;
   KfCand* cand_list = (KfCand*)ws;
   i64* und_list = (i64*)(ws + (Kp == KF_BN ? N * (i64)sizeof(KfCand) : 0));
-  // counters: [0] full-list rows, [1] candidate rows, [2] undecided rows
+  i64* scr_list = und_list + N;  // (K <= 256 only)
+  unsigned long long* und_mask = (unsigned long long*)(scr_list + N);
+  float* muf = (float*)(und_mask + (N + 31) / 32);
+  // counters: [0] full-list rows, [1] candidate rows, [2] undecided rows,
+  // [3] rows the fp16 screen left undecided
   HIP_TRY(hipMemsetAsync(counters, 0, 4 * sizeof(unsigned int), S(stream)));
   const int gp = kf_persistent_grid(N);
   if (dtype == SPX_F32 && Kp == KF_BN && D % 64 == 0 && D <= KB_DMAX && ldp % 4 == 0 &&
@@ -2322,7 +2480,8 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
     __bf16* CBh = (__bf16*)CT;
     __bf16* CBl = CBh + (i64)32 * nct * D;
     float* cnf = (float*)cn;
-    k_kmeans_prep_b3<<<1, 1024, 0, S(stream)>>>(D, K, 32 * nct, centers, CBh, CBl, cnf, cmax, mcoef);
+    float* cnf2 = cnf + KF_BN;  // |c'|^2 for the screen (the cn area holds 2 KF_BN floats)
+    k_kmeans_prep_b3<<<1, 1024, 0, S(stream)>>>(D, K, 32 * nct, centers, CBh, CBl, cnf, cmax, mcoef, cnf2, muf);
     LAUNCH_CHECK("spx_kmeans_assign(prep)");
     static int ncu = 0;
     if (!ncu) {
@@ -2332,18 +2491,32 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
     }
     const i64 ntiles = (N + 31) / 32;
     const float* Pf = (const float*)points;
-    if (kmeans_filter_mode() == 0) {
-      // A-stationary first pass over every point, then the all-accumulator
-      // filter in list mode over its undecided rows (candidate masks)
+    const int fmode = kmeans_filter_mode();
+    if (fmode != 1) {
+      // fp16 screen over every row, then the A-stationary bf16x3 pass over
+      // its undecided rows (mode "as": over every row), then the
+      // all-accumulator filter in list mode over what is still undecided
+      // (candidate masks)
       const i64 need_as = (ntiles + KS_WAVES - 1) / KS_WAVES;
       const int grid_as = (int)(need_as < ncu ? need_as : ncu);
-      switch (nct) {
-        case 1: ks_launch_d<1>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_list, grid_as); break;
-        case 2: ks_launch_d<2>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_list, grid_as); break;
-        case 4: ks_launch_d<4>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_list, grid_as); break;
-        default: ks_launch_d<8>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_list, grid_as); break;
+      const unsigned int cgrid = (unsigned int)((ntiles + 255) / 256);
+      if (fmode == 0) {
+        ks_launch_n<1>(nct, S(stream), N, D, Pf, ldp, CBh, CBl, cnf2, cmax, labels, counters, full_list, und_mask,
+                       nullptr, nullptr, muf, grid_as);
+        LAUNCH_CHECK("spx_kmeans_assign(fp16 screen)");
+        k_ks_compact<<<cgrid, 256, 0, S(stream)>>>(N, und_mask, nullptr, nullptr, scr_list, counters + 3);
+        LAUNCH_CHECK("spx_kmeans_assign(compact)");
+        ks_launch_n<0>(nct, S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_mask,
+                       scr_list, counters + 3, nullptr, grid_as);
+        LAUNCH_CHECK("spx_kmeans_assign(filter A-stationary)");
+        k_ks_compact<<<cgrid, 256, 0, S(stream)>>>(N, und_mask, scr_list, counters + 3, und_list, counters + 2);
+      } else {
+        ks_launch_n<0>(nct, S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_mask,
+                       nullptr, nullptr, nullptr, grid_as);
+        LAUNCH_CHECK("spx_kmeans_assign(filter A-stationary)");
+        k_ks_compact<<<cgrid, 256, 0, S(stream)>>>(N, und_mask, nullptr, nullptr, und_list, counters + 2);
       }
-      LAUNCH_CHECK("spx_kmeans_assign(filter A-stationary)");
+      LAUNCH_CHECK("spx_kmeans_assign(compact)");
       const i64* rin = und_list;
       const unsigned int* nin = counters + 2;
       switch (nct) {

@@ -744,18 +744,22 @@ def test_kmeans_assign_certified_bit_exact(ex, kind, dt, ddt):
     assert (want64 != cdist(pts.astype(np.float64), C).astype(np.float32).argmin(1)).any()
 
 
+@pytest.mark.parametrize('mode', ['scr', 'as', 'b3'])
 @pytest.mark.parametrize('D', [64, 128])
 @pytest.mark.parametrize('K', [1, 7, 32, 33, 100, 256])
-def test_kmeans_bf16x3_filter_bit_exact(ex, D, K):
-  """The bf16x3-MFMA certified filter (fp32 points, K <= 256, D % 64 == 0):
-  labels bit-identical to the all-exact fp64 kernel (scipy cdist order, ties
-  -> first index) on uniform data, exact duplicate centres, equidistant
-  points, a ragged last tile, and rows that must take the non-finite path
-  (NaN, 1e30)."""
+def test_kmeans_bf16x3_filter_bit_exact(ex, D, K, mode, monkeypatch):
+  """The certified filters (fp32 points, K <= 256, D % 64 == 0) in all three
+  first-pass modes (fp16 screen + A-stationary bf16x3 list pass, A-stationary
+  bf16x3 over every row, all-accumulator bf16x3): labels bit-identical to the
+  all-exact fp64 kernel (scipy cdist order, ties -> first index) on uniform
+  data, exact duplicate centres, equidistant points, a ragged last tile, rows
+  that must take the non-finite path (NaN, 1e30), a component past the fp16
+  range (7e4) and rows in the fp16 subnormal range."""
   import torch
   from oracle import workloads as OW
   from spartan_amd import backend
   be = backend.get()
+  monkeypatch.setenv('SPX_KMEANS_FILTER', mode)
   g = np.random.default_rng(D * 1000 + K)
   n = 20011
   pts = g.random((n, D)).astype(np.float32)
@@ -767,6 +771,9 @@ def test_kmeans_bf16x3_filter_bit_exact(ex, D, K):
   pts[7] = np.nan
   pts[8, 3] = 1e30
   pts[9] = -pts[10]
+  pts[11, 5] = 7e4                  # finite in fp32, inf in fp16
+  pts[12] *= np.float32(1e-6)       # fp16 subnormals
+  pts[13] = 0.0
   P = torch.as_tensor(pts).cuda()
   C = torch.as_tensor(centers).cuda()
   fast = torch.empty(n, dtype=torch.int64, device='cuda')
@@ -779,9 +786,9 @@ def test_kmeans_bf16x3_filter_bit_exact(ex, D, K):
   np.testing.assert_array_equal(f[ok][:3000], OW.kmeans_assign(pts[ok][:3000], centers))
 
 
-@pytest.mark.parametrize('mode', ['as', 'b3'])
+@pytest.mark.parametrize('mode', ['scr', 'as', 'b3'])
 @pytest.mark.parametrize('ddt', [np.float64, np.float32])
-@pytest.mark.parametrize('kind', ['offset128', 'means', 'clusters64', 'negative'])
+@pytest.mark.parametrize('kind', ['offset128', 'means', 'clusters64', 'negative', 'wide'])
 def test_kmeans_centred_filters_bit_exact(ex, kind, ddt, mode, monkeypatch):
   """Both bf16x3 filters rank centres by cc - 2 x.c' with c' = c - mean(c)
   (spx.hip k_kmeans_prep_b3): labels stay bit-identical to argmin(cdist) for
@@ -805,11 +812,14 @@ def test_kmeans_centred_filters_bit_exact(ex, kind, ddt, mode, monkeypatch):
     ctr = g.random((40, 64)) * 5
     pts = (ctr[g.integers(0, 40, 20000)] + 1e-2 * g.standard_normal((20000, 64))).astype(np.float32)
     C = ctr[g.integers(0, 40, 200)] + 1e-2 * g.standard_normal((200, 64))
+  elif kind == 'wide':  # centres beyond the fp16 range: the screen passes every row on
+    pts = (g.random((20000, 128)) * 1e5).astype(np.float32)
+    C = pts[g.choice(20000, 150, replace=False)].astype(np.float64)
   else:
     pts = (g.standard_normal((20000, 128)) * 3 - 7).astype(np.float32)
     C = pts[g.choice(20000, 97, replace=False)].astype(np.float64)
   want = cdist(pts.astype(np.float64), C).astype(ddt).argmin(1)
-  monkeypatch.setenv('SPX_KMEANS_FILTER', 'b3' if mode == 'b3' else '')
+  monkeypatch.setenv('SPX_KMEANS_FILTER', mode)
   P = torch.as_tensor(pts).cuda()
   Cd = torch.as_tensor(np.ascontiguousarray(C)).cuda()
   fast = torch.empty(len(pts), dtype=torch.int64, device='cuda')
