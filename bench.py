@@ -268,9 +268,9 @@ def bench_dot(S, ctx, be, expr, comm, sync, runs=10, warm=2):
 
 
 def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
-  """configs[2]: one k-means iteration (certified bf16x3 filter + exact-order
-  fp64 recompute = scipy-exact labels, fp64 centroid accumulation,
-  all-reduce) over npts x 128 fp32 points, k=256."""
+  """configs[2]: one k-means iteration (certified fp16-screen + bf16x3
+  filters + exact-order fp64 recompute = scipy-exact labels, fp64 centroid
+  accumulation, all-reduce) over npts x 128 fp32 points, k=256."""
   import torch
   from spartan_amd import workloads
   X = expr.rand(npts * ctx.world_size, D, dtype=np.float32, seed=21).force()
@@ -285,15 +285,16 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
   n = npts * ctx.world_size
   out = {'ms_per_iter': round(el * 1e3, 3), 'points_per_s': round(n / el, 1),
          'gemm_form_tflops': round(2.0 * n * K * D / el / 1e12, 2),
-         # the filter runs the distance GEMM as three bf16 MFMA products
-         # (bf16x3), so its matrix-core rate is 3x the GEMM-form rate against
-         # the dense bf16 peak; the iteration also streams X twice (assign +
-         # accumulate: 2 * 4 * N * D bytes)
-         'bf16x3_mfma_frac_per_gpu': round(3.0 * 2.0 * n * K * D / el / 1e12 / (2500.0 * ctx.world_size), 4),
+         # the first pass runs the distance GEMM once on fp16 MFMAs (the
+         # screen; the bf16x3 pass re-runs only its few % undecided rows), so
+         # the GEMM-form rate over the dense fp16/bf16 peak is its matrix-core
+         # share of the whole iteration; the iteration also streams X twice
+         # (assign + accumulate: 2 * 4 * N * D bytes)
+         'f16_mfma_frac_per_gpu': round(2.0 * n * K * D / el / 1e12 / (2500.0 * ctx.world_size), 4),
          'hbm_GBps_two_passes': round(2.0 * 4.0 * n * D / el / 1e9, 1),
          'config': 'cfg3: %d x %d fp32 points (U[0,1), seed 21) per GPU, k=%d, centres = first %d points; '
-                   'assign = bf16x3-MFMA certified filter + exact-order fp64 recompute of undecided points '
-                   '(bit-exact labels), fp64 centroid sums' % (npts, D, K, K)}
+                   'assign = certified fp16-MFMA screen, bf16x3-MFMA pass over its undecided rows, exact-order '
+                   'fp64 recompute of the rest (bit-exact labels), fp64 centroid sums' % (npts, D, K, K)}
   del X, labels
   torch.cuda.empty_cache()
   return out

@@ -155,10 +155,12 @@ int spx_argreduce_combine(int op, int dtype, const void* vals, const int64_t* id
  * differences, separately rounded, then sqrt) -> bit-exact labels.  points
  * F32/F64 (N, D) with row stride ldp; centers fp64 (K, D).
  * With a workspace (>= spx_kmeans_assign_workspace(dtype, N, D, K) bytes) and
- * mindist == NULL, an fp32 MFMA GEMM first certifies the points whose nearest
- * centre is separated from the runner-up by more than a rigorous error bound;
- * only the remaining points run the exact-order kernel.  The labels are the
- * same bits either way.  With mindist != NULL (receives the fp64 distance)
+ * mindist == NULL, MFMA passes first certify the points whose nearest centre
+ * is separated from the runner-up by more than a rigorous error bound (fp32
+ * points, K <= 256, D % 64 == 0: an fp16 screen over every point, then a
+ * bf16x3 pass over the points it leaves undecided; other shapes: one fp32
+ * MFMA pass); only the remaining points run the exact-order kernel.  The
+ * labels are the same bits either way.  With mindist != NULL (receives the fp64 distance)
  * or workspace == NULL every point takes the exact-order kernel.
  * dist_dtype SPX_F64: argmin of the fp64 distances; SPX_F32: argmin of the
  * distances rounded to fp32, first index on equal rounded values -- the

@@ -1541,8 +1541,18 @@ static void kb_launch(hipStream_t s, i64 N, i64 D, const float* P, i64 ldp, cons
 #define KS_WAVES_CFG 8  // waves per block (one block per CU): 8 = two per SIMD (<= 256 registers), 4 = one (<= 512)
 #endif
 constexpr int KS_WAVES = KS_WAVES_CFG;
+#ifndef KS_WAVES1_CFG
+#define KS_WAVES1_CFG 8  // the same for the fp16 screen (MODE 1): 12 = three per SIMD (<= 168 registers)
+#endif
+#ifndef KS_PIN1
+#define KS_PIN1 0  // 1: the screen's |x'|^2 fmas pinned right after the split (frees the raw tile's registers)
+#endif
+__host__ __device__ constexpr int ks_waves(int mode) { return mode == 1 ? KS_WAVES1_CFG : KS_WAVES; }
 #ifndef KS_PREFETCH
 #define KS_PREFETCH 0  // 1: next tile's loads in flight during the sweep (+64 registers: spills at 2 waves/SIMD)
+#endif
+#ifndef KS_PREFETCH1
+#define KS_PREFETCH1 0  // the same for the fp16 screen (MODE 1)
 #endif
 #ifndef KS_PIPE
 #define KS_PIPE 1  // 1: tile ct's top-2 fold interleaved with tile ct+1's MFMAs (two accumulator sets)
@@ -1653,7 +1663,7 @@ __device__ __forceinline__ void ks_unroll(F&& f, std::integer_sequence<int, Q...
 // overflow, cmax beyond the fp16 range) are undecided too: the MODE 0 pass
 // routes them.  cnf is |c'|^2 (cnf2 of the prep) in MODE 1.
 template <int NCT, int KS, int MODE>
-__global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const float* __restrict__ P, i64 ldp,
+__global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N, const float* __restrict__ P, i64 ldp,
                                                                     const __bf16* __restrict__ CBh,
                                                                     const __bf16* __restrict__ CBl,
                                                                     const float* __restrict__ cnf,
@@ -1676,7 +1686,7 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
     typedef __bf16 kb_b4 __attribute__((ext_vector_type(4)));
     typedef _Float16 kh_f4 __attribute__((ext_vector_type(4)));
     constexpr int D4 = D / 4;
-    for (int i = t; i < NC * D4; i += KS_WAVES * 64) {
+    for (int i = t; i < NC * D4; i += ks_waves(MODE) * 64) {
       const int c = i / D4, q = i % D4, qi = q & 3;
       const int pq = (q & ~3) | (qi == 1 ? 2 : qi == 2 ? 1 : qi);
       unsigned char* row = kb_lds + c * RB;
@@ -1696,7 +1706,7 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
     // -cc/2 split exactly into three bf16 (8 + 8 + 8 significant bits of
     // the fp32 value), for the k-step that adds it on the MFMA (lanes of the
     // upper half read the zeros next to it)
-    for (int i = t; i < NC; i += KS_WAVES * 64) {
+    for (int i = t; i < NC; i += ks_waves(MODE) * 64) {
       const float v = -0.5f * cnf[i];
       const __bf16 b1 = (__bf16)v;
       const float v1 = v - (float)b1;
@@ -1709,7 +1719,7 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
     }
     if constexpr (MODE == 1) {
       float* mul = (float*)(kb_lds + NC * RB);
-      for (int i = t; i < D; i += KS_WAVES * 64) mul[i] = muf[i];
+      for (int i = t; i < D; i += ks_waves(MODE) * 64) mul[i] = muf[i];
     }
   }
   __syncthreads();
@@ -1753,8 +1763,8 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
   // list mode: slot s < nrows stands for row rows_in[s]
   const i64 nlim = rows_in ? (i64)*nrows_in : N;
   const i64 ntiles = (nlim + 31) / 32;
-  const i64 stride = (i64)gridDim.x * KS_WAVES;
-  i64 tile = (i64)blockIdx.x * KS_WAVES + w;
+  const i64 stride = (i64)gridDim.x * ks_waves(MODE);
+  i64 tile = (i64)blockIdx.x * ks_waves(MODE) + w;
   kb_f4 ra[KS][2];
   auto load = [&](i64 tl) {
     i64 row = tl * 32 + r;
@@ -1770,13 +1780,11 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
       ra[ks][1] = *(const kb_f4*)(p + ks * 16 + 8);  // dims 8+4h..8+4h+3
     }
   };
-#if KS_PREFETCH
-  if (tile < ntiles) load(tile);
-#endif
+  constexpr bool PF = MODE == 1 ? KS_PREFETCH1 : KS_PREFETCH;
+  if constexpr (PF)
+    if (tile < ntiles) load(tile);
   for (; tile < ntiles; tile += stride) {
-#if !KS_PREFETCH
-    load(tile);  // the partner wave's sweep covers the latency
-#endif
+    if constexpr (!PF) load(tile);  // the partner wave's sweep covers the latency
     using AT = std::conditional_t<MODE == 0, kb_bf8, kh_f8>;
     AT ah[KS];
     kb_bf8 al[MODE == 0 ? KS : 1];
@@ -1806,17 +1814,18 @@ __global__ __launch_bounds__(KS_WAVES * 64) void k_kmeans_filter_as(i64 N, const
       }
     }
     float p2 = (p2q[0] + p2q[1]) + (p2q[2] + p2q[3]);
+    if constexpr (MODE == 1 && KS_PIN1) __builtin_amdgcn_sched_barrier(0);
     // (the compiler sinks the 64 |p|^2 fmas to the decision, keeping the raw
     // tile live through the sweep; pinning them here frees 47 registers but
     // measured 2 % slower, and the freed registers buy a next-tile prefetch
     // that only wins that back: 20.3 / 20.7 / 20.5 ms, gpurun_out ksv4)
-#if KS_PREFETCH
-    // the split above must finish reading ra before the next tile's loads
-    // land in it: without this fence the scheduler hoists the loads above
-    // the split (three tiles' worth of registers live at once -> spills)
-    __builtin_amdgcn_sched_barrier(0);
-    if (tile + stride < ntiles) load(tile + stride);  // lands during the sweep below
-#endif
+    if constexpr (PF) {
+      // the split above must finish reading ra before the next tile's loads
+      // land in it: without this fence the scheduler hoists the loads above
+      // the split (three tiles' worth of registers live at once -> spills)
+      __builtin_amdgcn_sched_barrier(0);
+      if (tile + stride < ntiles) load(tile + stride);  // lands during the sweep below
+    }
     // running top-2 of acc = S - cc/2 = -a'/2 (the best centre has the
     // LARGEST acc); lo / sec keep their names from the a' form
     float lo[16], sec[16];
@@ -2023,7 +2032,7 @@ static void ks_launch(hipStream_t s, i64 N, const float* P, i64 ldp, const __bf1
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)ks_lds_bytes(KB_DMAX, 8));
     attr = true;
   }
-  k_kmeans_filter_as<NCT, KS, MODE><<<grid, KS_WAVES * 64, lds, s>>>(N, P, ldp, CBh, CBl, cnf, cmax, labels, counters,
+  k_kmeans_filter_as<NCT, KS, MODE><<<grid, ks_waves(MODE) * 64, lds, s>>>(N, P, ldp, CBh, CBl, cnf, cmax, labels, counters,
                                                                      full_list, und_mask, rows_in, nrows_in, muf);
 }
 
@@ -2499,10 +2508,12 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
       // (candidate masks)
       const i64 need_as = (ntiles + KS_WAVES - 1) / KS_WAVES;
       const int grid_as = (int)(need_as < ncu ? need_as : ncu);
+      const i64 need_scr = (ntiles + ks_waves(1) - 1) / ks_waves(1);
+      const int grid_scr = (int)(need_scr < ncu ? need_scr : ncu);
       const unsigned int cgrid = (unsigned int)((ntiles + 255) / 256);
       if (fmode == 0) {
         ks_launch_n<1>(nct, S(stream), N, D, Pf, ldp, CBh, CBl, cnf2, cmax, labels, counters, full_list, und_mask,
-                       nullptr, nullptr, muf, grid_as);
+                       nullptr, nullptr, muf, grid_scr);
         LAUNCH_CHECK("spx_kmeans_assign(fp16 screen)");
         k_ks_compact<<<cgrid, 256, 0, S(stream)>>>(N, und_mask, nullptr, nullptr, scr_list, counters + 3);
         LAUNCH_CHECK("spx_kmeans_assign(compact)");
