@@ -1544,6 +1544,9 @@ constexpr int KS_WAVES = KS_WAVES_CFG;
 #ifndef KS_WAVES1_CFG
 #define KS_WAVES1_CFG 8  // the same for the fp16 screen (MODE 1): 12 = three per SIMD (<= 168 registers)
 #endif
+#ifndef KS_PAIRF1
+#define KS_PAIRF1 1  // 1: the screen folds two centre tiles at a time (max3 / med3 / max)
+#endif
 #ifndef KS_PIN1
 #define KS_PIN1 0  // 1: the screen's |x'|^2 fmas pinned right after the split (frees the raw tile's registers)
 #endif
@@ -1587,6 +1590,11 @@ __device__ __forceinline__ float ks_med3(float a, float b, float c) {
 __device__ __forceinline__ float ks_max(float a, float b) {
   float r;
   asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float ks_max3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
 // (bits(a) & ~7) | ct.  Plain C, not inline asm: its operand comes straight
@@ -1675,6 +1683,9 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
                                                                     const unsigned int* __restrict__ nrows_in,
                                                                     const float* __restrict__ muf) {
   extern __shared__ __attribute__((aligned(16))) unsigned char kb_lds[];
+  // the screen always runs over every row: no list lookups in its code (a
+  // run-time-null list still cost a guarded load and a vmcnt(0) per tile)
+  if constexpr (MODE == 1) rows_in = nullptr;
   constexpr int NC = 32 * NCT, D = 16 * KS, RB = ks_row_bytes(D, MODE);
   constexpr int CCOFF = MODE == 0 ? 4 * D : 2 * D;  // byte offset of the -cc/2 pieces in a row
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, h = lane >> 5;
@@ -1776,8 +1787,13 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
     const float* p = P + row * ldp + 4 * h;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
+#ifdef KS_NT  // dev A/B: non-temporal A loads
+      ra[ks][0] = __builtin_nontemporal_load((const kb_f4*)(p + ks * 16));
+      ra[ks][1] = __builtin_nontemporal_load((const kb_f4*)(p + ks * 16 + 8));
+#else
       ra[ks][0] = *(const kb_f4*)(p + ks * 16);      // dims 4h..4h+3 of the k-step
       ra[ks][1] = *(const kb_f4*)(p + ks * 16 + 8);  // dims 8+4h..8+4h+3
+#endif
     }
   };
   constexpr bool PF = MODE == 1 ? KS_PREFETCH1 : KS_PREFETCH;
@@ -1871,6 +1887,12 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
 #ifdef KS_DEV_CCVALU  // dev A/B only: -cc/2 added on the VALU instead of the MFMA step
       acc = acc + -0.5f * cnf[ct * 32 + r];
 #endif
+#ifdef KS_DEV_NOFOLD  // timing split only (wrong labels); never set in the product build
+      if (MODE == 1) {
+        lo[q] = ks_max(lo[q], acc);
+        return;
+      }
+#endif
       const float v = ks_tag(acc, (unsigned int)ct);
       sec[q] = ks_med3(v, lo[q], sec[q]);
       lo[q] = ks_max(lo[q], v);
@@ -1898,7 +1920,55 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
       c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, *(const kb_bf8*)(rp + CCOFF), c0, 0, 0, 0);
 #endif
     };
-    {
+    // pairwise fold (KS_PAIRF1, screen only): two tiles' values a, b of one
+    // row fold as sec = max(sec, med3(lo, a, b)), lo = max3(lo, a, b) -- the
+    // top two of {lo, sec, a, b} with lo >= sec -- 5 VALU per 2 values
+    // instead of 6; needs both tiles' accumulators live (a third and fourth
+    // set: the screen has the registers, MODE 0 does not)
+    constexpr bool PAIRF = MODE == 1 && KS_PAIRF1 && NCT >= 2;
+    auto fold2 = [&](int q, int ct, float a, float b) {
+      const float ta = ks_tag(a, (unsigned int)ct), tb = ks_tag(b, (unsigned int)(ct + 1));
+      sec[q] = ks_max(sec[q], ks_med3(lo[q], ta, tb));
+      lo[q] = ks_max3(lo[q], ta, tb);
+    };
+    // chains of tiles ct, ct + 1 into c0, c1, with the pair fold of tiles
+    // pct, pct + 1 (p0, p1) written into their k-loops (16 / KS / 2 rows per k-step)
+    auto chain2_fold = [&](int ct, kb_acc& c0, kb_acc& c1, int pct, const kb_acc& p0, const kb_acc& p1) {
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        kb_acc& c = half ? c1 : c0;
+        c = (kb_acc){};
+        const unsigned char* rp = rowp + (ct + half) * 32 * RB;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          kstep(ks, rp, c);
+#pragma unroll
+          for (int qq = 0; qq < 8 / KS + (KS > 8 ? 1 : 0); ++qq) {
+            const int q = half * 8 + ks * (8 / KS) + qq;
+            if (q < 16) fold2(q, pct, p0[q], p1[q]);
+          }
+        }
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, *(const kb_bf8*)(rp + CCOFF), c, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    if constexpr (PAIRF) {
+      kb_acc a0, a1, b0, b1;
+      chain(0, a0);
+      chain(1, a1);
+#pragma unroll 1
+      for (int cp = 2; cp < NCT; cp += 4) {
+        chain2_fold(cp, b0, b1, cp - 2, a0, a1);
+        if (cp + 2 < NCT) chain2_fold(cp + 2, a0, a1, cp, b0, b1);
+      }
+      if constexpr (((NCT - 2) / 2) & 1) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) fold2(q, NCT - 2, b0[q], b1[q]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) fold2(q, NCT - 2, a0[q], a1[q]);
+      }
+    } else {
       kb_acc a0, b0;
       chain(0, a0);
       if constexpr (NCT == 1) {
@@ -1949,6 +2019,9 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
       asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(r1), "n"(32 + 2 * q));
       rmin = v;
     };
+#ifdef KS_DEV_NODEC  // timing split only (wrong labels); never set in the product build
+    if (MODE == 0)
+#endif
     ks_unroll(rmin_q, std::make_integer_sequence<int, 16>{});
     p2 += __shfl_xor(p2, 32, 64);  // row r's |p|^2 in lanes r and r + 32
     // one decision per row, by the even lane of its pair (as in k_kmeans_filter_b3)
@@ -1983,8 +2056,12 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
 
 // Row list of the undecided rows from the per-tile lane masks of
 // k_kmeans_filter_as (bit l: lane (h, r) = (l >> 5, l & 31) decided row rt(r >> 1, h)
-// of the tile); rows_in: the tile slots stand for rows_in[slot].  One thread
-// per tile, one atomic per block for the block's range.
+// of the tile); rows_in: the tile slots stand for rows_in[slot].  A block
+// covers KC_TPB = 256 x KC_TPT tiles (coalesced mask loads, tile j * 256 + t of
+// the chunk to thread t) and takes its range with ONE atomic: one atomic per
+// 256 tiles serialised on the counter's L2 channel (147 us at cfg3's 3.1 M
+// tiles, 25 MB of masks).
+constexpr int KC_TPT = 16;
 __global__ __launch_bounds__(256) void k_ks_compact(i64 N, const unsigned long long* __restrict__ mask,
                                                     const i64* __restrict__ rows_in,
                                                     const unsigned int* __restrict__ nrows_in, i64* __restrict__ out,
@@ -1993,10 +2070,16 @@ __global__ __launch_bounds__(256) void k_ks_compact(i64 N, const unsigned long l
   __shared__ unsigned int base;
   const i64 nlim = rows_in ? (i64)*nrows_in : N;
   const i64 ntiles = (nlim + 31) / 32;
-  const i64 tl = (i64)blockIdx.x * 256 + threadIdx.x;
-  if ((i64)blockIdx.x * 256 >= ntiles) return;  // block-uniform
-  const unsigned long long m = tl < ntiles ? mask[tl] : 0ull;
-  const unsigned int n = (unsigned int)__popcll(m);
+  const i64 t0 = (i64)blockIdx.x * 256 * KC_TPT;
+  if (t0 >= ntiles) return;  // block-uniform
+  unsigned long long m[KC_TPT];
+  unsigned int n = 0;
+#pragma unroll
+  for (int j = 0; j < KC_TPT; ++j) {
+    const i64 tl = t0 + j * 256 + threadIdx.x;
+    m[j] = tl < ntiles ? mask[tl] : 0ull;
+    n += (unsigned int)__popcll(m[j]);
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   unsigned int inc = n;
 #pragma unroll
@@ -2010,13 +2093,17 @@ __global__ __launch_bounds__(256) void k_ks_compact(i64 N, const unsigned long l
   __syncthreads();
   unsigned int pos = base + inc - n;
   for (int k = 0; k < w; ++k) pos += wsum[k];
-  unsigned long long mm = m;
-  while (mm) {
-    const int l = __builtin_ctzll(mm);
-    mm &= mm - 1;
-    const int q = (l & 31) >> 1, h = l >> 5;
-    const i64 slot = tl * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-    out[pos++] = rows_in ? rows_in[slot] : slot;
+#pragma unroll
+  for (int j = 0; j < KC_TPT; ++j) {
+    const i64 tl = t0 + j * 256 + threadIdx.x;
+    unsigned long long mm = m[j];
+    while (mm) {
+      const int l = __builtin_ctzll(mm);
+      mm &= mm - 1;
+      const int q = (l & 31) >> 1, h = l >> 5;
+      const i64 slot = tl * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+      out[pos++] = rows_in ? rows_in[slot] : slot;
+    }
   }
 }
 
@@ -2510,7 +2597,7 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
       const int grid_as = (int)(need_as < ncu ? need_as : ncu);
       const i64 need_scr = (ntiles + ks_waves(1) - 1) / ks_waves(1);
       const int grid_scr = (int)(need_scr < ncu ? need_scr : ncu);
-      const unsigned int cgrid = (unsigned int)((ntiles + 255) / 256);
+      const unsigned int cgrid = (unsigned int)((ntiles + 256 * KC_TPT - 1) / (256 * KC_TPT));
       if (fmode == 0) {
         ks_launch_n<1>(nct, S(stream), N, D, Pf, ldp, CBh, CBl, cnf2, cmax, labels, counters, full_list, und_mask,
                        nullptr, nullptr, muf, grid_scr);
@@ -2553,6 +2640,13 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
     k_kmeans_assign<float><<<gp, 256, 0, S(stream)>>>(N, D, K, Pf, ldp, centers, labels, nullptr, full_list,
                                                        counters, r32);
     LAUNCH_CHECK("spx_kmeans_assign(exact)");
+    if (getenv("SPX_KMEANS_DEBUG")) {  // dev: row counts of each stage (synchronises the stream)
+      unsigned int hc[4];
+      HIP_TRY(hipMemcpyAsync(hc, counters, sizeof(hc), hipMemcpyDeviceToHost, S(stream)));
+      HIP_TRY(hipStreamSynchronize(S(stream)));
+      fprintf(stderr, "spx_kmeans_assign: N %lld screen-undecided %u bf16x3-undecided %u candidate rows %u full %u\n",
+              (long long)N, hc[3], hc[2], hc[1], hc[0]);
+    }
     return SPX_OK;
   }
   k_kmeans_prep<<<1, 256, 0, S(stream)>>>(D, K, Kp, centers, CT, cn, cmax, mcoef);
