@@ -2061,7 +2061,10 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
 // the chunk to thread t) and takes its range with ONE atomic: one atomic per
 // 256 tiles serialised on the counter's L2 channel (147 us at cfg3's 3.1 M
 // tiles, 25 MB of masks).
-constexpr int KC_TPT = 16;
+// KC_TPT tiles per thread: 16 for the sparse full-row pass (~5 % of rows at
+// cfg3), 1 for the dense list pass (~20 % of its slots): a thread's rows are
+// written one after another, so a dense mask wants few tiles per thread.
+template <int KC_TPT>
 __global__ __launch_bounds__(256) void k_ks_compact(i64 N, const unsigned long long* __restrict__ mask,
                                                     const i64* __restrict__ rows_in,
                                                     const unsigned int* __restrict__ nrows_in, i64* __restrict__ out,
@@ -2597,22 +2600,23 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
       const int grid_as = (int)(need_as < ncu ? need_as : ncu);
       const i64 need_scr = (ntiles + ks_waves(1) - 1) / ks_waves(1);
       const int grid_scr = (int)(need_scr < ncu ? need_scr : ncu);
-      const unsigned int cgrid = (unsigned int)((ntiles + 256 * KC_TPT - 1) / (256 * KC_TPT));
+      const unsigned int cgrid = (unsigned int)((ntiles + 256 * 16 - 1) / (256 * 16));
+      const unsigned int cgrid1 = (unsigned int)((ntiles + 255) / 256);
       if (fmode == 0) {
         ks_launch_n<1>(nct, S(stream), N, D, Pf, ldp, CBh, CBl, cnf2, cmax, labels, counters, full_list, und_mask,
                        nullptr, nullptr, muf, grid_scr);
         LAUNCH_CHECK("spx_kmeans_assign(fp16 screen)");
-        k_ks_compact<<<cgrid, 256, 0, S(stream)>>>(N, und_mask, nullptr, nullptr, scr_list, counters + 3);
+        k_ks_compact<16><<<cgrid, 256, 0, S(stream)>>>(N, und_mask, nullptr, nullptr, scr_list, counters + 3);
         LAUNCH_CHECK("spx_kmeans_assign(compact)");
         ks_launch_n<0>(nct, S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_mask,
                        scr_list, counters + 3, nullptr, grid_as);
         LAUNCH_CHECK("spx_kmeans_assign(filter A-stationary)");
-        k_ks_compact<<<cgrid, 256, 0, S(stream)>>>(N, und_mask, scr_list, counters + 3, und_list, counters + 2);
+        k_ks_compact<1><<<cgrid1, 256, 0, S(stream)>>>(N, und_mask, scr_list, counters + 3, und_list, counters + 2);
       } else {
         ks_launch_n<0>(nct, S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_mask,
                        nullptr, nullptr, nullptr, grid_as);
         LAUNCH_CHECK("spx_kmeans_assign(filter A-stationary)");
-        k_ks_compact<<<cgrid, 256, 0, S(stream)>>>(N, und_mask, nullptr, nullptr, und_list, counters + 2);
+        k_ks_compact<16><<<cgrid, 256, 0, S(stream)>>>(N, und_mask, nullptr, nullptr, und_list, counters + 2);
       }
       LAUNCH_CHECK("spx_kmeans_assign(compact)");
       const i64* rin = und_list;
