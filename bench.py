@@ -144,7 +144,7 @@ def main():
   achieved = bytes_launch / avg / 1e9 if red else None
 
   traffic = None
-  tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r02_pmc_traffic.json')
+  tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r02s2_pmc_traffic.json')
   if os.path.exists(tpath) and rows_local == 32768 and S == 32768:
     with open(tpath) as f:
       traffic = json.load(f)['hbm_bytes_per_launch']
@@ -170,7 +170,7 @@ def main():
                    'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                    'frac': round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                    'traffic': traffic,
-                   'traffic_source': 'profiles/r02_pmc_traffic.json (FETCH_SIZE/WRITE_SIZE passes)' if traffic
+                   'traffic_source': 'profiles/r02s2_pmc_traffic.json (FETCH_SIZE/WRITE_SIZE passes)' if traffic
                    else None,
                    'kernel': 'spx_reduce (generated fused map+reduce)',
                    'bytes_per_launch': bytes_launch,
