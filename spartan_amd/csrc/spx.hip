@@ -2275,6 +2275,72 @@ __global__ __launch_bounds__(256) void k_kmeans_cand(i64 D, const TP* __restrict
   }
 }
 
+// The same exact-order candidate distances with 16 lanes per point (fp32
+// points, D = 16 DPL, 16-byte aligned rows and centres -- the bf16x3 path's
+// shapes): lane s loads dims [s DPL, (s + 1) DPL) of the point once and of each
+// candidate centre in one go and squares its differences in parallel; the
+// sum keeps scipy's order ((0 + sq_0) + sq_1) + ... by passing the running
+// fp64 sum from lane to lane (16 shuffles per candidate).  The 4-lane kernel
+// above walked each 128-dim row through a 2-deep register ring: one memory
+// round trip per 32 dims per candidate (0.46 ms for cfg3's ~0.6 M rows).
+template <int DPL>
+__global__ __launch_bounds__(256) void k_kmeans_cand16(const float* __restrict__ P, i64 ldp,
+                                                       const double* __restrict__ C, i64* __restrict__ labels,
+                                                       const unsigned int* __restrict__ counters,
+                                                       const KfCand* __restrict__ cand_list, int r32) {
+  constexpr int D = 16 * DPL;
+  const i64 n = counters[1];
+  const int g = threadIdx.x >> 4, s = threadIdx.x & 15;
+  const i64 step = (i64)gridDim.x * 16;
+  for (i64 q = (i64)blockIdx.x * 16 + g; q < n; q += step) {  // uniform per 16-lane group
+    const i64 row = cand_list[q].row;
+    float xv[DPL];
+    {
+      const float* x = P + row * ldp + s * DPL;
+#pragma unroll
+      for (int j = 0; j < DPL; j += 4) {
+        const kb_f4 v = *(const kb_f4*)(x + j);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xv[j + e] = v[e];
+      }
+    }
+    double best = 0.0;
+    int bi = -1;
+#pragma unroll 1
+    for (int wd = 0; wd < 8; ++wd) {
+      unsigned int m = cand_list[q].mask[wd];
+      while (m) {  // uniform per group
+        const int c = 32 * wd + __builtin_ctz(m);
+        m &= m - 1;
+        const double* cc = C + (i64)c * D + s * DPL;
+        double sq[DPL];
+#pragma unroll
+        for (int j = 0; j < DPL; j += 2) {
+          const double2 v = *(const double2*)(cc + j);
+          const double d0 = (double)xv[j] - v.x, d1 = (double)xv[j + 1] - v.y;
+          sq[j] = d0 * d0;
+          sq[j + 1] = d1 * d1;
+        }
+        double acc = 0.0;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          double a = acc;
+#pragma unroll
+          for (int j = 0; j < DPL; ++j) a = a + sq[j];
+          acc = __shfl(a, t, 16);  // lane t's dims follow lane t - 1's
+        }
+        double dist = sqrt(acc);
+        if (r32) dist = (double)(float)dist;  // fp32-rounded distances: equal values tie, first index wins
+        if (bi < 0 || dist < best || (dist == best && c < bi)) {
+          best = dist;
+          bi = c;
+        }
+      }
+    }
+    if (s == 0) labels[row] = bi;
+  }
+}
+
 // CT[d][c] = (float)C[c][d] (zero-padded to Kp centres), cn[c] = |C[c]|^2 in
 // fp64 (+inf for padding), *cmax = max_c |C[c]| (one block).
 __global__ __launch_bounds__(256) void k_kmeans_prep(i64 D, i64 K, i64 Kp, const double* __restrict__ C,
@@ -2639,7 +2705,12 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
       }
       LAUNCH_CHECK("spx_kmeans_assign(filter bf16x3)");
     }
-    k_kmeans_cand<float, true><<<gp, 256, 0, S(stream)>>>(D, Pf, ldp, centers, labels, counters, cand_list, r32);
+    if ((D == 64 || D == 128) && ((uintptr_t)centers % 16) == 0 && getenv("SPX_KMEANS_CAND4") == nullptr) {
+      if (D == 64) k_kmeans_cand16<4><<<gp, 256, 0, S(stream)>>>(Pf, ldp, centers, labels, counters, cand_list, r32);
+      else k_kmeans_cand16<8><<<gp, 256, 0, S(stream)>>>(Pf, ldp, centers, labels, counters, cand_list, r32);
+    } else {
+      k_kmeans_cand<float, true><<<gp, 256, 0, S(stream)>>>(D, Pf, ldp, centers, labels, counters, cand_list, r32);
+    }
     LAUNCH_CHECK("spx_kmeans_assign(candidates)");
     k_kmeans_assign<float><<<gp, 256, 0, S(stream)>>>(N, D, K, Pf, ldp, centers, labels, nullptr, full_list,
                                                        counters, r32);
