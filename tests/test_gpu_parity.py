@@ -471,10 +471,12 @@ def test_lreg_cfg5_full_size(ex):
   np.testing.assert_allclose(np.asarray(got, np.float64), exact, rtol=1e-5, atol=1e-5 * np.abs(exact).max())
 
 
-def test_kmeans_cfg3_full_size(ex):
+def test_kmeans_cfg3_full_size(ex, monkeypatch):
   """cfg3 at its BASELINE size (1e8 x 128 fp32, k = 256, second-iteration
   centres): the certified assignment equals the all-exact kernel on a 2M-row
-  prefix and on 2M rows at the end; the fp64 centroid sums and counts equal a
+  prefix and on 2M rows at the end, and on ALL 1e8 rows the default path (fp16
+  screen + bf16x3 list pass) equals the bf16x3 pass over every row (two
+  independently certified filters); the fp64 centroid sums and counts equal a
   chunked torch index_add restatement (counts exact, sums within 1e-12)."""
   import torch
   from spartan_amd import backend
@@ -496,6 +498,12 @@ def test_kmeans_cfg3_full_size(ex):
     ref = torch.empty((b - a,), dtype=torch.int64, device=dev)
     be.kmeans_assign(pts[a:b], cen, ref, exact_only=True)
     assert torch.equal(lab[a:b], ref)
+  monkeypatch.setenv('SPX_KMEANS_FILTER', 'as')
+  lab_as = torch.empty_like(lab)
+  be.kmeans_assign(pts, cen, lab_as)
+  monkeypatch.delenv('SPX_KMEANS_FILTER')
+  assert torch.equal(lab_as, lab)
+  del lab_as
   be.kmeans_accumulate(pts, lab, sums, cnt)
   s2 = torch.zeros((K, D), dtype=torch.float64, device=dev)
   c2 = torch.zeros((K,), dtype=torch.int64, device=dev)
