@@ -2054,6 +2054,262 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
   }
 }
 
+// ---------------------------------------------------------------------------
+// The fp16 screen on the 16x16x32 MFMA shape (KS_S16): the same certified
+// a'' = |c'|^2 - 2 x'.c' ranking and bound as k_kmeans_filter_as<.., 1>, with
+// v_mfma_f32_16x16x32_f16 (MI355X_MICROARCH.md: the chip holds a higher clock
+// on this shape, and the screen is clock bound).  A wave's 32-point tile is
+// two 16-row blocks; each B fragment (16 centres x 32 dims, ds_read_b128) feeds
+// both.  Lane (c, g) = (l & 15, l >> 4) holds, per k-step ks, dims
+// 32 ks + 4 g + {0..3} and 32 ks + 16 + 4 g + {0..3} of rows 16 b + c (64-byte
+// row pieces per load instruction); the centre rows are stored with the same
+// permutation.  Output: lane (c, g) holds rows 16 b + 4 g + j of centre c, so a
+// row's top two are reduced over the 16 lanes of one DPP row (no ds_swizzle),
+// 8 (lo, sec) registers per lane; tiles are tagged in 4 low mantissa bits
+// (16 centre tiles: 15 ulp, priced below).
+constexpr int S16_RB = 288;  // row stride: 18 quads = 2 (mod 16) -> a ds_read_b128 lane group hits 16 distinct bank quads
+constexpr int S16_CC = 256;  // byte offset of the -cc/2 pieces in a row (D <= 128)
+static size_t s16_lds_bytes(i64 D, int nct16) { return (size_t)16 * nct16 * S16_RB + 16 + 4 * (size_t)D; }
+typedef float s16_acc __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float ks_tag4(float a, unsigned int ct) {
+  return __builtin_bit_cast(float, (__builtin_bit_cast(unsigned int, a) & ~15u) | (ct & 15u));
+}
+
+template <int NCT, int KS>
+__global__ __launch_bounds__(512) void k_kmeans_screen16(i64 N, const float* __restrict__ P, i64 ldp,
+                                                         const __bf16* __restrict__ CBh,
+                                                         const __bf16* __restrict__ CBl,
+                                                         const float* __restrict__ cnf2, const double* cmax_p,
+                                                         i64* __restrict__ labels,
+                                                         unsigned long long* __restrict__ und_mask,
+                                                         const float* __restrict__ muf) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char kb_lds[];
+  constexpr int NC = 16 * NCT, D = 32 * KS, W = 8;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, c = lane & 15, g = lane >> 4;
+  unsigned char* zq = kb_lds + NC * S16_RB;  // 16 zero bytes (the cc step's B for lane groups 1-3)
+  float* mul = (float*)(zq + 16);
+  {
+    typedef __bf16 kb_b4 __attribute__((ext_vector_type(4)));
+    typedef _Float16 kh_f4 __attribute__((ext_vector_type(4)));
+    constexpr int D4 = D / 4;
+    for (int i = t; i < NC * D4; i += W * 64) {
+      const int cen = i / D4, q = i % D4, ks = q >> 3, qq = q & 7;
+      const int pos = 32 * ks + (qq < 4 ? 8 * qq : 8 * (qq - 4) + 4);  // half index in the permuted row
+      const kb_b4 bh = *(const kb_b4*)&CBh[(i64)cen * D + 4 * q];
+      const kb_b4 bl = *(const kb_b4*)&CBl[(i64)cen * D + 4 * q];
+      kh_f4 v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (_Float16)((float)bh[j] + (float)bl[j]);
+      *(kh_f4*)(kb_lds + cen * S16_RB + 2 * pos) = v;
+    }
+    for (int i = t; i < NC; i += W * 64) {
+      const float v = -0.5f * cnf2[i];
+      const __bf16 b1 = (__bf16)v;
+      const float v1 = v - (float)b1;
+      const __bf16 b2 = (__bf16)v1;
+      const __bf16 b3 = (__bf16)(v1 - (float)b2);
+      const __bf16 z = (__bf16)0.f;
+      *(kb_bf8*)(kb_lds + i * S16_RB + S16_CC) = (kb_bf8){b1, b2, b3, z, z, z, z, z};
+    }
+    if (t < 4) ((float*)zq)[t] = 0.f;
+    for (int i = t; i < D; i += W * 64) mul[i] = muf[i];
+  }
+  __syncthreads();
+  const double cmax = cmax_p[0], mcoef = cmax_p[1], mun = cmax_p[2], dcmax = cmax_p[3];
+  const double u32 = 5.9604644775390625e-08, eps = 1.1920928955078125e-07;
+  const double chain = 32.0 * (double)KS;
+  const double eS = (u32 * cmax + 4.8828125e-04 * cmax + 1.001 * dcmax +
+                     2.0 * (chain + 3.0) * u32 * 1.001 * (cmax + dcmax)) * 1.01;
+  const double cm2 = cmax * cmax + 2.0 * mun * cmax;
+  // as the 32x32 screen, plus the 4-bit tag: 15 ulp of |acc| = 30 eps (|x'| cmax + cmax^2 / 2) in a'' units
+  const double xk1 = 64.0 * u32 * cmax + 16.0 * eps * cmax;
+  const double xk0 = 32.0 * u32 * cm2 + 8.0 * eps * cm2 + sqrt((double)D) * 1.1920928955078125e-07 * (cmax + dcmax) +
+                     (double)D * 3.552713678800501e-15;
+  float kq[3];
+  kc_coef(eS, cmax, mun, mcoef, D, kq, xk1, xk0);
+  const bool cok = cmax * cmax < 1e36 && mun * cmax < 1e36 && cmax < 3.0e4 && dcmax == dcmax;
+  const float pn_lim = (float)(cmax > 0.0 ? 1e36 / cmax : 1e36);
+  const i64 ntiles = (N + 31) / 32;
+  const i64 stride = (i64)gridDim.x * W;
+  const __bf16 one = (__bf16)1.f;
+  const kb_bf8 a_one = (kb_bf8){one, one, one, one, one, one, one, one};
+  for (i64 tile = (i64)blockIdx.x * W + w; tile < ntiles; tile += stride) {
+    kb_f4 ra[2][KS][2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      i64 row = tile * 32 + 16 * b + c;
+      row = row < N ? row : N - 1;
+      const float* p = P + row * ldp + 4 * g;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        ra[b][ks][0] = *(const kb_f4*)(p + 32 * ks);
+        ra[b][ks][1] = *(const kb_f4*)(p + 32 * ks + 16);
+      }
+    }
+    kh_f8 ah[2][KS];
+    float p2b[2] = {0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const kb_f4 m0 = *(const kb_f4*)(mul + 32 * ks + 4 * g);
+      const kb_f4 m1 = *(const kb_f4*)(mul + 32 * ks + 16 + 4 * g);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const kb_f4 x0 = ra[b][ks][0] - m0, x1 = ra[b][ks][1] - m1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          p2b[b] = __builtin_fmaf(x0[e], x0[e], p2b[b]);
+          p2b[b] = __builtin_fmaf(x1[e], x1[e], p2b[b]);
+          ah[b][ks][e] = (_Float16)x0[e];
+          ah[b][ks][4 + e] = (_Float16)x1[e];
+        }
+      }
+    }
+    float lo[8], sec[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      lo[k] = -INFINITY;
+      sec[k] = -INFINITY;
+    }
+    // tiles ct, ct + 1 -> acc[tile-in-pair][block]
+    auto chain2 = [&](int ct, s16_acc (&acc)[2][2]) {
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const unsigned char* rp = kb_lds + ((ct + h2) * 16 + c) * S16_RB + 16 * g;
+        acc[h2][0] = (s16_acc){};
+        acc[h2][1] = (s16_acc){};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const kh_f8 bh = *(const kh_f8*)(rp + 64 * ks);
+          acc[h2][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[0][ks], bh, acc[h2][0], 0, 0, 0);
+          acc[h2][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[1][ks], bh, acc[h2][1], 0, 0, 0);
+        }
+        const kb_bf8 bcc = *(const kb_bf8*)(g == 0 ? kb_lds + ((ct + h2) * 16 + c) * S16_RB + S16_CC : zq);
+        acc[h2][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_one, bcc, acc[h2][0], 0, 0, 0);
+        acc[h2][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_one, bcc, acc[h2][1], 0, 0, 0);
+      }
+    };
+    auto fold2 = [&](int ct, const s16_acc (&acc)[2][2]) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = 4 * b + j;
+          const float ta = ks_tag4(acc[0][b][j], (unsigned int)ct), tb = ks_tag4(acc[1][b][j], (unsigned int)(ct + 1));
+          sec[k] = ks_max(sec[k], ks_med3(lo[k], ta, tb));
+          lo[k] = ks_max3(lo[k], ta, tb);
+        }
+    };
+    {
+      s16_acc A[2][2], B[2][2];
+      chain2(0, A);
+#pragma unroll 1
+      for (int cp = 2; cp < NCT; cp += 4) {
+        chain2(cp, B);
+        fold2(cp - 2, A);
+        __builtin_amdgcn_sched_barrier(0);
+        if (cp + 2 < NCT) {
+          chain2(cp + 2, A);
+          fold2(cp, B);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if constexpr (((NCT - 2) / 2) & 1) fold2(NCT - 2, B);
+      else fold2(NCT - 2, A);
+    }
+    float lo0[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) lo0[k] = lo[k];
+    // top two per row over the 16 lanes of the row's DPP row (register halving
+    // on lane bits 3, 2, 1, then bit 0): lane c keeps register (c >> 1) & 7
+    {
+      auto comb = [](float a, float as, float b, float bs, float& l, float& s2) {
+        s2 = ks_med3(a, b, ks_max(as, bs));
+        l = ks_max(a, b);
+      };
+      auto dpp_step = [&](auto ctrl, int n, int o) {
+        constexpr int C = decltype(ctrl)::value;
+        const bool up = (lane & o) != 0;
+#pragma unroll
+        for (int k = 0; k < n; ++k) {
+          const float kl = up ? lo[k + n] : lo[k], ks2 = up ? sec[k + n] : sec[k];
+          const float sl = up ? lo[k] : lo[k + n], ss = up ? sec[k] : sec[k + n];
+          const float ol = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sl), C, 0xF, 0xF, false));
+          const float os = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, ss), C, 0xF, 0xF, false));
+          comb(kl, ks2, ol, os, lo[k], sec[k]);
+        }
+      };
+      dpp_step(std::integral_constant<int, 0x140>{}, 4, 8);  // row_mirror: lane ^ 15
+      dpp_step(std::integral_constant<int, 0x141>{}, 2, 4);  // row_half_mirror: lane ^ 7
+      dpp_step(std::integral_constant<int, 0x4E>{}, 1, 2);   // quad_perm [2,3,0,1]: lane ^ 2
+      const float ol = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, lo[0]), 0xB1, 0xF, 0xF, false));
+      const float os = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sec[0]), 0xB1, 0xF, 0xF, false));
+      comb(lo[0], sec[0], ol, os, lo[0], sec[0]);
+    }
+    // the centre of each row's best: the lowest lane c of the group whose own
+    // best for that row equals it (equal tagged values share the tile)
+    const int kme = (c >> 1) & 7;
+    int rmin = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float bk = __shfl(lo[0], (lane & 48) | (2 * k), 64);
+      const unsigned long long m = __ballot(lo0[k] == bk);
+      const unsigned int mg = (unsigned int)(m >> (16 * g)) & 0xFFFFu;
+      const int ck = __builtin_ctz(mg | 0x10000u);
+      rmin = kme == k ? ck : rmin;
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      p2b[b] += __shfl_xor(p2b[b], 16, 64);
+      p2b[b] += __shfl_xor(p2b[b], 32, 64);
+    }
+    const int bme = (c >> 3) & 1, jme = (c >> 1) & 3;
+    const int src = 4 * g + jme;  // a lane holding |x'|^2 of row 16 bme + 4 g + jme
+    const float s0 = __shfl(p2b[0], src, 64), s1 = __shfl(p2b[1], src, 64);
+    const float p2f = bme ? s1 : s0;
+    const i64 grow = tile * 32 + 16 * bme + 4 * g + jme;
+    const float b1 = lo[0], b2 = sec[0];
+    const int i1 = 16 * (int)(__builtin_bit_cast(unsigned int, b1) & 15u) + rmin;
+    const float pn = __builtin_amdgcn_sqrtf(__builtin_fmaf(p2f, 1.001f, 1e-37f)) * 1.0001f;
+    const float e = __builtin_fmaf(__builtin_fmaf(kq[2], pn, kq[1]), pn, kq[0]) * 1.0001f;
+    const bool live = grow < N && (c & 1) == 0;
+    const bool fin = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim && isfinite(b1) && isfinite(b2);
+    const bool dec = fin && b1 - b2 > 1.0001f * e;
+    if (live && dec) labels[grow] = i1;
+    const unsigned long long und = __ballot(live && !dec);
+    if (lane == 0) und_mask[tile] = und;
+  }
+}
+
+template <int NCT, int KS>
+static void s16_launch(hipStream_t s, i64 N, const float* P, i64 ldp, const __bf16* CBh, const __bf16* CBl,
+                       const float* cnf2, const double* cmax, i64* labels, unsigned long long* und_mask,
+                       const float* muf, int grid) {
+  const size_t lds = s16_lds_bytes(32 * KS, NCT);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_kmeans_screen16<NCT, KS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)s16_lds_bytes(KB_DMAX, 16));
+    attr = true;
+  }
+  k_kmeans_screen16<NCT, KS><<<grid, 512, lds, s>>>(N, P, ldp, CBh, CBl, cnf2, cmax, labels, und_mask, muf);
+}
+
+static void s16_launch_n(int nct32, hipStream_t s, i64 N, i64 D, const float* P, i64 ldp, const __bf16* CBh,
+                         const __bf16* CBl, const float* cnf2, const double* cmax, i64* labels,
+                         unsigned long long* und_mask, const float* muf, int grid) {
+#define S16_CASE(NC)                                                                                        \
+  if (D == 64) s16_launch<NC, 2>(s, N, P, ldp, CBh, CBl, cnf2, cmax, labels, und_mask, muf, grid);       \
+  else s16_launch<NC, 4>(s, N, P, ldp, CBh, CBl, cnf2, cmax, labels, und_mask, muf, grid);
+  switch (nct32) {
+    case 1: S16_CASE(2) break;
+    case 2: S16_CASE(4) break;
+    case 4: S16_CASE(8) break;
+    default: S16_CASE(16) break;
+  }
+#undef S16_CASE
+}
+
 // Row list of the undecided rows from the per-tile lane masks of
 // k_kmeans_filter_as (bit l: lane (h, r) = (l >> 5, l & 31) decided row rt(r >> 1, h)
 // of the tile); rows_in: the tile slots stand for rows_in[slot].  A block
@@ -2064,7 +2320,7 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
 // KC_TPT tiles per thread: 16 for the sparse full-row pass (~5 % of rows at
 // cfg3), 1 for the dense list pass (~20 % of its slots): a thread's rows are
 // written one after another, so a dense mask wants few tiles per thread.
-template <int KC_TPT>
+template <int KC_TPT, int LAYOUT = 0>
 __global__ __launch_bounds__(256) void k_ks_compact(i64 N, const unsigned long long* __restrict__ mask,
                                                     const i64* __restrict__ rows_in,
                                                     const unsigned int* __restrict__ nrows_in, i64* __restrict__ out,
@@ -2103,8 +2359,14 @@ __global__ __launch_bounds__(256) void k_ks_compact(i64 N, const unsigned long l
     while (mm) {
       const int l = __builtin_ctzll(mm);
       mm &= mm - 1;
-      const int q = (l & 31) >> 1, h = l >> 5;
-      const i64 slot = tl * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+      i64 slot;
+      if (LAYOUT == 0) {  // 32x32 output layout (k_kmeans_filter_as)
+        const int q = (l & 31) >> 1, h = l >> 5;
+        slot = tl * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+      } else {  // 16x16 output layout (k_kmeans_screen16): lane (c, g) decided row 16 (c >> 3 & 1) + 4 g + (c >> 1 & 3)
+        const int c = l & 15, g = l >> 4;
+        slot = tl * 32 + 16 * ((c >> 3) & 1) + 4 * g + ((c >> 1) & 3);
+      }
       out[pos++] = rows_in ? rows_in[slot] : slot;
     }
   }
@@ -2573,6 +2835,7 @@ static int kmeans_filter_mode() {
   const char* v = getenv("SPX_KMEANS_FILTER");
   if (v && strcmp(v, "b3") == 0) return 1;
   if (v && strcmp(v, "as") == 0) return 2;
+  if (v && strcmp(v, "s16") == 0) return 3;
   return 0;
 }
 
@@ -2668,11 +2931,17 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
       const int grid_scr = (int)(need_scr < ncu ? need_scr : ncu);
       const unsigned int cgrid = (unsigned int)((ntiles + 256 * 16 - 1) / (256 * 16));
       const unsigned int cgrid1 = (unsigned int)((ntiles + 255) / 256);
-      if (fmode == 0) {
-        ks_launch_n<1>(nct, S(stream), N, D, Pf, ldp, CBh, CBl, cnf2, cmax, labels, counters, full_list, und_mask,
-                       nullptr, nullptr, muf, grid_scr);
-        LAUNCH_CHECK("spx_kmeans_assign(fp16 screen)");
-        k_ks_compact<16><<<cgrid, 256, 0, S(stream)>>>(N, und_mask, nullptr, nullptr, scr_list, counters + 3);
+      if (fmode == 0 || fmode == 3) {
+        if (fmode == 3) {
+          s16_launch_n(nct, S(stream), N, D, Pf, ldp, CBh, CBl, cnf2, cmax, labels, und_mask, muf, grid_scr);
+          LAUNCH_CHECK("spx_kmeans_assign(fp16 screen, 16x16x32)");
+          k_ks_compact<16, 1><<<cgrid, 256, 0, S(stream)>>>(N, und_mask, nullptr, nullptr, scr_list, counters + 3);
+        } else {
+          ks_launch_n<1>(nct, S(stream), N, D, Pf, ldp, CBh, CBl, cnf2, cmax, labels, counters, full_list, und_mask,
+                         nullptr, nullptr, muf, grid_scr);
+          LAUNCH_CHECK("spx_kmeans_assign(fp16 screen)");
+          k_ks_compact<16><<<cgrid, 256, 0, S(stream)>>>(N, und_mask, nullptr, nullptr, scr_list, counters + 3);
+        }
         LAUNCH_CHECK("spx_kmeans_assign(compact)");
         ks_launch_n<0>(nct, S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_mask,
                        scr_list, counters + 3, nullptr, grid_as);

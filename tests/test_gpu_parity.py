@@ -752,7 +752,7 @@ def test_kmeans_assign_certified_bit_exact(ex, kind, dt, ddt):
     assert (want64 != cdist(pts.astype(np.float64), C).astype(np.float32).argmin(1)).any()
 
 
-@pytest.mark.parametrize('mode', ['scr', 'as', 'b3'])
+@pytest.mark.parametrize('mode', ['scr', 's16', 'as', 'b3'])
 @pytest.mark.parametrize('D', [64, 128])
 @pytest.mark.parametrize('K', [1, 7, 32, 33, 100, 256])
 def test_kmeans_bf16x3_filter_bit_exact(ex, D, K, mode, monkeypatch):
@@ -794,7 +794,7 @@ def test_kmeans_bf16x3_filter_bit_exact(ex, D, K, mode, monkeypatch):
   np.testing.assert_array_equal(f[ok][:3000], OW.kmeans_assign(pts[ok][:3000], centers))
 
 
-@pytest.mark.parametrize('mode', ['scr', 'as', 'b3'])
+@pytest.mark.parametrize('mode', ['scr', 's16', 'as', 'b3'])
 @pytest.mark.parametrize('ddt', [np.float64, np.float32])
 @pytest.mark.parametrize('kind', ['offset128', 'means', 'clusters64', 'negative', 'wide'])
 def test_kmeans_centred_filters_bit_exact(ex, kind, ddt, mode, monkeypatch):
