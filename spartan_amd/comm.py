@@ -54,7 +54,7 @@ def _dt(t):
 
 def _stream():
   import torch
-  return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+  return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(torch.cuda.current_device()))
 
 
 def _p(t):
