@@ -24,10 +24,14 @@ __global__ __launch_bounds__(W * 64) void k_ld(i64 N, const float* __restrict__ 
         ra[2 * ks] = *(const f4*)(p + ks * 16);
         ra[2 * ks + 1] = *(const f4*)(p + ks * 16 + 8);
       }
-    } else {
+    } else if (MODE == 1) {
       const float* p = P + tile * 32 * 128 + 4 * lane;
 #pragma unroll
       for (int j = 0; j < 16; ++j) ra[j] = *(const f4*)(p + j * 256);
+    } else {  // MODE 2: coalesced, non-temporal
+      const float* p = P + tile * 32 * 128 + 4 * lane;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) ra[j] = __builtin_nontemporal_load((const f4*)(p + j * 256));
     }
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc += ra[j];
@@ -64,5 +68,9 @@ int main(int argc, char** argv) {
   t = run<0, 16>(N, P, out, 256); printf("screen pattern  16 waves/CU: %7.3f ms  %7.1f GB/s\n", t, gb / t * 1e3);
   t = run<1, 16>(N, P, out, 256); printf("coalesced       16 waves/CU: %7.3f ms  %7.1f GB/s\n", t, gb / t * 1e3);
   t = run<0, 8>(N, P, out, 512);  printf("screen pattern  2x8 waves/CU: %7.3f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+  t = run<2, 8>(N, P, out, 256);  printf("coalesced nt     8 waves/CU: %7.3f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+  t = run<2, 16>(N, P, out, 256); printf("coalesced nt    16 waves/CU: %7.3f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+  t = run<2, 16>(N, P, out, 512); printf("coalesced nt  2x16 waves/CU: %7.3f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+  t = run<1, 16>(N, P, out, 512); printf("coalesced     2x16 waves/CU: %7.3f ms  %7.1f GB/s\n", t, gb / t * 1e3);
   return 0;
 }
