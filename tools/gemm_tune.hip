@@ -99,14 +99,15 @@ int main(int argc, char** argv) {
     run<float>(S, rounds,
                {V(float, 128, 128, 16, 2, 2, 0), V(float, 128, 128, 16, 2, 2, 8), V(float, 128, 128, 32, 2, 2, 8),
                 V(float, 256, 128, 16, 4, 2, 8), V(float, 128, 256, 16, 2, 4, 8), V(float, 256, 256, 16, 4, 4, 8),
-                V(float, 128, 128, 32, 4, 4, 8), V(float, 256, 128, 32, 4, 2, 8)},
+                V(float, 128, 128, 32, 4, 4, 8), V(float, 256, 128, 32, 4, 2, 8), V(float, 256, 256, 32, 4, 4, 8),
+                V(float, 256, 256, 16, 2, 4, 8), V(float, 256, 256, 32, 2, 4, 8)},
                157.3);
   }
   if (which != "f32") {
     run<double>(S, rounds,
                 {V(double, 128, 128, 8, 2, 2, 0), V(double, 128, 128, 16, 4, 4, 8), V(double, 128, 128, 16, 4, 4, 0),
                  V(double, 128, 128, 16, 2, 2, 8), V(double, 256, 128, 16, 4, 4, 8), V(double, 128, 256, 16, 4, 4, 8),
-                 V(double, 256, 256, 16, 4, 4, 8)},
+                 V(double, 256, 256, 16, 4, 4, 8), V(double, 128, 128, 32, 4, 4, 8)},
                 78.6);
   }
   return 0;
