@@ -20,6 +20,10 @@
 
 #include <cstdint>
 
+#ifndef SPX_GEMM_AK
+#define SPX_GEMM_AK 1  // fp32: A k-contiguous in LDS, K split between lane halves (see gemm)
+#endif
+
 namespace spx_mfma {
 
 typedef int64_t i64;
@@ -91,7 +95,15 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
   constexpr int PADA = 16 / sizeof(T) / 2 > 0 ? 16 / sizeof(T) / 2 : 1;
   static_assert(LA >= 1 && LB >= 1 && LA * NT * VE == BM * BK && LB * NT * VE == BK * BN, "bad tiling");
   static_assert(TM >= 1 && TN >= 1 && BK % F::KS == 0, "bad wave tiling");
-  __shared__ T As[2][BK][BM + PADA];
+  // AK (fp32): A kept k-contiguous in LDS ([m][k], rows padded to BK + 4)
+  // and the tile's K split between the two lane halves: MFMA step kk takes
+  // k = kk from lanes 0-31 and k = BK/2 + kk from lanes 32-63 (B read the
+  // same way), so a lane's BK/2 A values are two ds_read_b128 per K-tile
+  // and the staging store is one ds_write_b128 -- instead of BK/2 ds_read_b32
+  // and a 4-way transposing scalar store.
+  constexpr bool AK = SPX_GEMM_AK && sizeof(T) == 4 && F::KS == 2 && BK % 8 == 0;
+  __shared__ __attribute__((aligned(16))) T As[AK ? 1 : 2][AK ? 1 : BK][AK ? 1 : BM + PADA];
+  __shared__ __attribute__((aligned(16))) T Ak[AK ? 2 : 1][AK ? BM : 1][AK ? BK + 4 : 1];
   __shared__ __attribute__((aligned(16))) T Bs[2][BK][BN];
   int tm, tn;
   tile_of(blockIdx.x, ntiles, tiles_n, GM, tm, tn);
@@ -135,8 +147,12 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
     for (int i = 0; i < LA; ++i) {
       const int idx = t + i * NT;
       const int r = idx / (BK / VE), kq = idx % (BK / VE);
+      if constexpr (AK) {
+        *(V*)(&Ak[buf][r][kq * VE]) = ra[i];
+      } else {
 #pragma unroll
-      for (int j = 0; j < VE; ++j) As[buf][kq * VE + j][r] = ra[i][j];
+        for (int j = 0; j < VE; ++j) As[buf][kq * VE + j][r] = ra[i][j];
+      }
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
@@ -152,18 +168,44 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) load((i64)(kt + 1) * BK);
+    if constexpr (AK) {
+      constexpr int KH = BK / 2;
+      const int kb = KH * F::opk(lane);
+      T av[TM][KH];
 #pragma unroll
-    for (int kk = 0; kk < BK / F::KS; ++kk) {
-      const int k = kk * F::KS + F::opk(lane);
-      T a[TM], b[TN];
+      for (int i = 0; i < TM; ++i) {
+        const T* ap = &Ak[cur][wm * WTM + i * F::TILE + F::opi(lane)][kb];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = As[cur][k][wm * WTM + i * F::TILE + F::opi(lane)];
+        for (int q = 0; q < KH; q += VE) {
+          const V v = *(const V*)(ap + q);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = Bs[cur][k][wn * WTN + j * F::TILE + F::opi(lane)];
+          for (int e = 0; e < VE; ++e) av[i][q + e] = v[e];
+        }
+      }
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int kk = 0; kk < KH; ++kk) {
+        T b[TN];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) b[j] = Bs[cur][kb + kk][wn * WTN + j * F::TILE + F::opi(lane)];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = F::mma(av[i][kk], b[j], acc[i][j]);
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < BK / F::KS; ++kk) {
+        const int k = kk * F::KS + F::opk(lane);
+        T a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = As[cur][k][wm * WTM + i * F::TILE + F::opi(lane)];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = Bs[cur][k][wn * WTN + j * F::TILE + F::opi(lane)];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
+      }
     }
     if (kt + 1 < nk) store(cur ^ 1);
     __syncthreads();
