@@ -102,7 +102,8 @@ int main(int argc, char** argv) {
                 V(float, 128, 128, 32, 4, 4, 8), V(float, 256, 128, 32, 4, 2, 8), V(float, 256, 256, 32, 4, 4, 8),
                 V(float, 256, 256, 16, 2, 4, 8), V(float, 256, 256, 32, 2, 4, 8), V(float, 256, 128, 16, 4, 2, 4),
                 V(float, 256, 128, 16, 4, 2, 16), V(float, 256, 128, 16, 2, 2, 8),
-                V(float, 256, 64, 16, 4, 1, 8)},
+                V(float, 256, 64, 16, 4, 1, 8), V(float, 256, 128, 16, 2, 4, 8), V(float, 256, 256, 16, 2, 8, 8),
+                V(float, 128, 128, 16, 1, 4, 8)},
                157.3);
   }
   if (which != "f32") {
