@@ -81,7 +81,8 @@ def main():
   ap.add_argument('--cpu-baseline', type=int, default=1)
   ap.add_argument('--cpu-rows', type=int, default=32768, help='rows of the CPU baseline sample (full cfg2 strip: ~10-20 s of CPU work)')
   ap.add_argument('--strong', action='store_true', help='fixed 2^30 global array (strong scaling)')
-  ap.add_argument('--workloads', type=int, default=1, help='also time k-means (cfg3) and lreg (cfg5)')
+  ap.add_argument('--workloads', default='1',
+                  help='also time k-means (cfg3) and lreg (cfg5): 1 / 0, or a comma list of lreg, kmeans, kmeans_api')
   ap.add_argument('--km-points', type=int, default=100000000)
   ap.add_argument('--lreg-points', type=int, default=100000000)
   args = ap.parse_args()
@@ -120,7 +121,7 @@ def main():
   be.kernel_events = []
   t0 = time.perf_counter()
   for _ in range(args.steps):
-    step()
+    last = step()
   sync()
   comm.barrier()
   sync()
@@ -135,7 +136,8 @@ def main():
   value = total_bytes / elapsed / 1e9
   # dominant kernel: the generated fused map+reduce kernel ('spx_reduce'),
   # timed with HIP events on the stream it is launched on
-  red = [(s.elapsed_time(e) * 1e-3) for (n, s, e) in events if n == 'spx_reduce']
+  red = [(s.elapsed_time(e) * 1e-3) for (n, s, e) in events if n.startswith('spx_reduce')]
+  knames = sorted({n for (n, s, e) in events if n.startswith('spx_reduce')})
   ax0 = red[0::2]
   ax1 = red[1::2]
   rows_local = sum(ex.shape[0] for ex in x.local) if hasattr(x, 'local') else S
@@ -155,6 +157,7 @@ def main():
       'n_gpus': N,
       'n_ranks_seen': _ranks_seen(),
       'dist_backend': ctx.dist_backend,
+      'dataplane_selftest': getattr(ctx, 'selftest', None),
       'steps': args.steps,
       'warmup': args.warmup,
       'ms_per_step': round(elapsed / args.steps * 1e3, 4),
@@ -172,13 +175,14 @@ def main():
                    'traffic': traffic,
                    'traffic_source': 'profiles/r02s2_pmc_traffic.json (FETCH_SIZE/WRITE_SIZE passes)' if traffic
                    else None,
-                   'kernel': 'spx_reduce (generated fused map+reduce)',
+                   'kernel': 'generated fused map+reduce: %s' % ' / '.join(knames),
                    'bytes_per_launch': bytes_launch,
                    'avg_launch_ms': round(avg * 1e3, 4) if red else None,
                    'axis0_ms': round(float(np.mean(ax0)) * 1e3, 4) if ax0 else None,
                    'axis1_ms': round(float(np.mean(ax1)) * 1e3, 4) if ax1 else None},
   }
-  del x, y, z, X, Y, Z
+  result['checked'] = check_cfg2(last, x, y, z, R, S)
+  del x, y, z, X, Y, Z, last
   torch.cuda.empty_cache()
 
   def leg(fn, *a):
@@ -197,9 +201,12 @@ def main():
   if args.dot:
     result['dot'] = leg(bench_dot, args.dot_size, ctx, be, expr, comm, sync)
 
-  if args.workloads:
+  wl = {'1': ('lreg', 'kmeans', 'kmeans_api'), '0': ()}.get(args.workloads, tuple(args.workloads.split(',')))
+  if 'lreg' in wl:
     result['lreg'] = leg(bench_lreg, args.lreg_points, ctx, expr, comm, sync)
+  if 'kmeans' in wl:
     result['kmeans'] = leg(bench_kmeans, args.km_points, ctx, expr, comm, sync)
+  if 'kmeans_api' in wl:
     result['kmeans_api'] = leg(bench_kmeans_api, args.km_points, ctx, expr, comm, sync)
 
   if args.cpu_baseline and N == 1 and ctx.rank == 0:
@@ -222,6 +229,44 @@ def main():
   if ctx.rank == 0:
     print(json.dumps(result), flush=True)
   spartan_amd.shutdown()
+  failed = [k for k, v in result.items() if k == 'checked' and v is not True] + [
+      k for k, v in result.items() if isinstance(v, dict) and v.get('checked') is False]
+  if failed:
+    sys.stderr.write('bench.py: post-timing validation FAILED for %s\n' % ', '.join(failed))
+    sys.exit(3)
+
+
+# ------------------------------------------------------------------ checks
+# Every leg validates the outputs it timed, after the timed region, against an
+# independent fp64 restatement on a sample (host NumPy on glom'd rows /
+# columns, or torch fp64 on the device tensors -- a checker, never the measured
+# path).  A failed check prints the line with "checked": false and exits 3.
+def _rel_ok(got, want, tol, scale=None):
+  got = np.asarray(got, dtype=np.float64)
+  want = np.asarray(want, dtype=np.float64)
+  sc = np.abs(want) if scale is None else np.asarray(scale, dtype=np.float64)
+  return bool(np.all(np.abs(got - want) <= tol * np.maximum(sc, 1e-300)))
+
+
+def check_cfg2(last, x, y, z, R, S):
+  """axis-1 results of three sampled rows and axis-0 results of three sampled
+  columns against fp64 sums of the same fp32 inputs; sum of the axis-0
+  result against the sum of the axis-1 result.  Tolerance 1e-5 relative
+  (the north star's fp32 bound)."""
+  from spartan_amd.array import distarray, extent as ext
+  a0, a1 = last
+  g0 = distarray.glom(a0).astype(np.float64)
+  g1 = distarray.glom(a1).astype(np.float64)
+  ok = _rel_ok(g0.sum(), g1.sum(), 1e-5)
+  for i in (0, R // 3, R - 1):
+    reg = ext.create((i, 0), (i + 1, S), (R, S))
+    xr, yr, zr = (distarray.glom_region(t, reg).astype(np.float64).ravel() for t in (x, y, z))
+    ok &= _rel_ok(g1[i], np.sum(xr * yr + np.exp(zr)), 1e-5)
+  for j in (0, S // 2 + 1, S - 1):
+    reg = ext.create((0, j), (R, j + 1), (R, S))
+    xc, yc, zc = (distarray.glom_region(t, reg).astype(np.float64).ravel() for t in (x, y, z))
+    ok &= _rel_ok(g0[j], np.sum(xc * yc + np.exp(zc)), 1e-5)
+  return bool(ok)
 
 
 def _ranks_seen():
@@ -253,18 +298,65 @@ def bench_dot(S, ctx, be, expr, comm, sync, runs=10, warm=2):
       comm.barrier()
       sync()
       times.append(comm.max_over_ranks(time.perf_counter() - t0))
-      del c
+      if len(times) < runs:
+        del c
+    checked = check_dot(c, A, B, S, dt, expr)
+    del c
     el = float(np.median(times))
     flops = 2.0 * S ** 3
     name = 'f32' if dt == np.float32 else 'f64'
     out[name] = {'gflops': round(flops / el / 1e9, 1), 'seconds': round(el, 4),
                  'seconds_min_max': [round(min(times), 4), round(max(times), 4)],
-                 'mfma_frac_per_gpu': round(flops / el / 1e12 / (peak * ctx.world_size), 4)}
+                 'mfma_frac_per_gpu': round(flops / el / 1e12 / (peak * ctx.world_size), 4),
+                 'checked': checked}
     del a, b, A, B
     torch.cuda.empty_cache()
   out['config'] = ('dot(A, B), A, B ~ U[0,1) (%d, %d), K-split over ranks; median of %d runs after %d warm-ups'
                    % (S, S, runs, warm))
   return out
+
+
+def check_dot(c, A, B, S, dt, expr):
+  """Row sums of two sampled rows of C = A B against A[i, :] . (B 1) and
+  column sums of two sampled columns against (1^T A) . B[:, j], the vectors
+  B 1 and 1^T A taken in fp64 by the reduction kernels (not the GEMM);
+  tolerance 1e-5 (fp32) / 1e-11 (fp64) relative to the fp64 sums of |terms|."""
+  from spartan_amd.array import distarray, extent as ext
+  tol = 1e-5 if dt == np.float32 else 1e-11
+  b1 = expr.sum(expr.astype(B, np.float64), axis=1).glom()
+  a1 = expr.sum(expr.astype(A, np.float64), axis=0).glom()
+  ok = True
+  for i in (1, S - 2):
+    ar = distarray.glom_region(A.force(), ext.create((i, 0), (i + 1, S), (S, S))).astype(np.float64).ravel()
+    cr = distarray.glom_region(c, ext.create((i, 0), (i + 1, S), (S, S))).astype(np.float64).ravel()
+    ok &= _rel_ok(cr.sum(), ar @ b1, tol, np.abs(ar) @ np.abs(b1))
+  for j in (2, S - 3):
+    bc = distarray.glom_region(B.force(), ext.create((0, j), (S, j + 1), (S, S))).astype(np.float64).ravel()
+    cc = distarray.glom_region(c, ext.create((0, j), (S, j + 1), (S, S))).astype(np.float64).ravel()
+    ok &= _rel_ok(cc.sum(), a1 @ bc, tol, np.abs(a1) @ np.abs(bc))
+  return bool(ok)
+
+
+KM_CENTERS = {}
+
+
+def check_kmeans(X, labels, centers, comm, n_check=1 << 20):
+  """The labels of the first n_check local rows against the all-exact
+  assignment kernel (scipy cdist order for every point and centre): bit
+  for bit."""
+  import torch
+  from spartan_amd import backend, runtime
+  be = backend.get()
+  ctx = runtime.get()
+  cdev = torch.as_tensor(np.ascontiguousarray(centers, dtype=np.float64)).to(ctx.device)
+  ok = True
+  for ex, tile in X.local.items():
+    n = min(n_check, ex.shape[0])
+    lab = labels.local[[e for e in labels.local if e.ul[0] == ex.ul[0]][0]].data[:n]
+    want = torch.empty((n,), dtype=torch.int64, device=ctx.device)
+    be.kmeans_assign(tile.data[:n], cdev, want, exact_only=True)
+    ok &= bool(torch.equal(lab, want))
+  return bool(comm.max_over_ranks(0.0 if ok else 1.0) == 0.0)
 
 
 def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
@@ -278,10 +370,13 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
   sync()
   comm.barrier()
   t0 = time.perf_counter()
-  c, labels = workloads.kmeans_fit(X, K, iters)
+  info = {}
+  c, labels = workloads.kmeans_fit(X, K, iters, info=info)
   sync()
   comm.barrier()
   el = comm.max_over_ranks(time.perf_counter() - t0) / iters
+  checked = check_kmeans(X, labels, info['assign_centers'], comm)
+  KM_CENTERS[npts] = c
   n = npts * ctx.world_size
   out = {'ms_per_iter': round(el * 1e3, 3), 'points_per_s': round(n / el, 1),
          'gemm_form_tflops': round(2.0 * n * K * D / el / 1e12, 2),
@@ -292,6 +387,7 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
          # (assign + accumulate: 2 * 4 * N * D bytes)
          'f16_mfma_frac_per_gpu': round(2.0 * n * K * D / el / 1e12 / (2500.0 * ctx.world_size), 4),
          'hbm_GBps_two_passes': round(2.0 * 4.0 * n * D / el / 1e9, 1),
+         'checked': checked,
          'config': 'cfg3: %d x %d fp32 points (U[0,1), seed 21) per GPU, k=%d, centres = first %d points; '
                    'assign = certified fp16-MFMA screen, bf16x3-MFMA pass over its undecided rows, exact-order '
                    'fp64 recompute of the rest (bit-exact labels), fp64 centroid sums' % (npts, D, K, K)}
@@ -314,17 +410,49 @@ def bench_kmeans_api(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
   sync()
   comm.barrier()
   t0 = time.perf_counter()
-  KMeans(K, iters).fit(X, c0)
+  c_api, _ = KMeans(K, iters).fit(X, c0)
   sync()
   comm.barrier()
   el = comm.max_over_ranks(time.perf_counter() - t0) / iters
   n = npts * ctx.world_size
-  out = {'ms_per_iter': round(el * 1e3, 3), 'points_per_s': round(n / el, 1),
+  # the same iterations as the direct leg (same points, same initial centres);
+  # the drop-in rounds the fp64 centre sums to the points' fp32 before the
+  # division, as the reference's map2 target does: 1e-5 relative
+  ref = KM_CENTERS.get(npts)
+  checked = None if ref is None else _rel_ok(c_api, ref, 1e-5, np.abs(ref) + 1e-3)
+  out = {'ms_per_iter': round(el * 1e3, 3), 'points_per_s': round(n / el, 1), 'checked': checked,
          'config': 'cfg3 via examples.kmeans.KMeans(%d, %d).fit(X, first %d points): outer + argmin '
                    '(OuterArgminFusion -> certified assignment), map2 bincount, map2 centre sums' % (K, iters, K)}
   del X
   torch.cuda.empty_cache()
   return out
+
+
+def check_lreg(Xe, Ye, w, expr, comm, chunk=1 << 23):
+  """The fused gradient sum(x * (dot(x, w) - y), axis=0) at the final w
+  against a chunked fp64 restatement over the local row strips (torch fp64
+  on the device, a checker only), all-reduced over ranks: per column within
+  1e-5 of sum_i |x_ij| |r_i| (the condition of the sum)."""
+  import torch
+  from spartan_amd import runtime
+  ctx = runtime.get()
+  g = expr.sum(Xe * (expr.dot(Xe, w) - Ye), axis=0).optimized().glom().astype(np.float64)
+  X, Y = Xe.force(), Ye.force()
+  D = X.shape[1]
+  wd = torch.as_tensor(np.asarray(w, dtype=np.float64).reshape(D)).to(ctx.device)
+  acc = torch.zeros((2, D), dtype=torch.float64, device=ctx.device)
+  ytiles = {ex.ul[0]: t for ex, t in Y.local.items()}
+  for ex, t in X.local.items():
+    yt = ytiles[ex.ul[0]].data.reshape(-1)
+    for r0 in range(0, ex.shape[0], chunk):
+      xc = t.data[r0:r0 + chunk].to(torch.float64)
+      res = xc @ wd - yt[r0:r0 + chunk].to(torch.float64)
+      acc[0] += res @ xc
+      acc[1] += res.abs() @ xc.abs()
+      del xc, res
+  comm.all_reduce(acc, 'sum')
+  ref = acc.cpu().numpy()
+  return _rel_ok(g, ref[0], 1e-5, ref[1])
 
 
 def bench_lreg(npts, ctx, expr, comm, sync, D=64, iters=30):
@@ -339,14 +467,16 @@ def bench_lreg(npts, ctx, expr, comm, sync, D=64, iters=30):
   sync()
   comm.barrier()
   t0 = time.perf_counter()
-  workloads.sgd_train(Xe, Ye, w, 1e-6, iters)
+  w_end = workloads.sgd_train(Xe, Ye, w, 1e-6, iters)
   sync()
   comm.barrier()
   el = comm.max_over_ranks(time.perf_counter() - t0) / iters
+  checked = check_lreg(Xe, Ye, w_end, expr, comm)
   n = npts * ctx.world_size
   nbytes = 4.0 * n * D + 4.0 * n   # one pass: X and y read once (DotReduceFusion)
   out = {'ms_per_iter': round(el * 1e3, 3), 'algorithmic_GBps': round(nbytes / el / 1e9, 1),
          'hbm_frac_per_gpu': round(nbytes / el / 1e9 / (HBM_PEAK_GBS * ctx.world_size), 4),
+         'checked': checked,
          'config': 'cfg5: X %d x %d fp32, y %d x 1, w 64 x 1 host; grad = sum(x * (dot(x, w) - y), axis=0): '
                    'dot folded into the fused axis-0 reduction (one pass over X) + all-reduce of 64 fp32'
                    % (n, D, n)}

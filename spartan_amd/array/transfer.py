@@ -91,12 +91,19 @@ def _blocks(shape, itemsize):
   return [(r, min(rows, r + per)) for r in range(0, rows, per)], row_bytes
 
 
+# dtypes the pinned ring uploads (native byte order, the backend's own
+# types); anything else (float16, int8, big-endian ...) takes the plain path
+_TINY_DTYPES = tuple(np.dtype(t) for t in (np.bool_, np.int32, np.int64, np.float32, np.float64))
+
+
 def upload(arr, device, dtype=None):
   """Device tensor holding ``arr`` (any strides, memmaps included)."""
   import torch
   from .. import backend
   arr = np.asarray(arr) if dtype is None else np.asarray(arr, dtype=dtype)
-  if device.type == 'cuda' and arr.nbytes <= TINY and arr.dtype.kind in 'biuf':
+  if not arr.dtype.isnative:  # torch takes native byte order only
+    arr = arr.astype(arr.dtype.newbyteorder('='))
+  if device.type == 'cuda' and arr.nbytes <= TINY and arr.dtype in _TINY_DTYPES:
     return _tiny_upload(arr, device)
   if device.type != 'cuda' or arr.ndim == 0 or arr.nbytes < SMALL or (
       arr.flags.c_contiguous and DIRECT_H2D):

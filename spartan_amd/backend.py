@@ -355,7 +355,9 @@ class HipBackend:
     sig = ('map', root.sig(), tuple(ins), tuple(classes), ndim, V, dense, nt)
     fn = self._sig_fns.get(sig)
     if fn is None:
-      fn = self._sig_fns[sig] = self.kernel(codegen.gen_map(root, ins, classes, ndim, V, dense, nt), 'spx_map')
+      src, kname = codegen.named(codegen.gen_map(root, ins, classes, ndim, V, dense, nt), 'spx_map',
+                                 'dense' if dense else 'nd')
+      fn = self._sig_fns[sig] = self.kernel(src, kname)
     per = V if args.flags & 1 else 1
     # one vector per lane and no grid-stride loop: x + 1 / x * y at 2^30 fp32
     # 1.75 / 2.58 ms with a 4096-block grid-stride loop, 1.34 / 2.01 ms with
@@ -372,8 +374,11 @@ class HipBackend:
     # launch plan of an identical call (same IR signature, operand layouts and
     # shapes: an iterative driver's replayed DAG): everything below up to the
     # kernel arguments is a function of this key
+    # (the pointer's residue mod 16, not just 16-byte alignment: the vector
+    # width of narrow types needs only 8 or 4 bytes, so two pointers with the
+    # same 16-alignment verdict can still differ in what V they allow)
     pkey = (root.sig(), op, tuple((s, inputs[s].dtype, tuple(inputs[s].shape), inputs[s].stride(),
-                                   inputs[s].data_ptr() % 16 == 0) for s in slots),
+                                   inputs[s].data_ptr() % 16) for s in slots),
             tuple(in_shape), axis, tuple(out_shape), np.dtype(out_dtype).str,
             None if idx_geom is None else repr(sorted(idx_geom.items())))
     plan = self._reduce_plans.get(pkey) if _REPLAY_PLANS else None
@@ -526,8 +531,9 @@ class HipBackend:
     sig = ('reduce', root.sig(), tuple(ins), tuple(classes), kind, op, V, U, rowinv)
     fn = self._sig_fns.get(sig)
     if fn is None:
-      fn = self._sig_fns[sig] = self.kernel(codegen.gen_reduce(root, ins, classes, kind, op, V, U, rowinv),
-                                            'spx_reduce')
+      src, kname = codegen.named(codegen.gen_reduce(root, ins, classes, kind, op, V, U, rowinv), 'spx_reduce',
+                                 kind)
+      fn = self._sig_fns[sig] = self.kernel(src, kname)
     self.launch(fn, nblk, args)
     if not direct:
       _check(self.lib.spx_reduce_finalize(

@@ -479,6 +479,19 @@ def cols_unroll(inputs, classes, vec, row_strides=None):
   return 4
 
 
+def named(src, base, kind):
+  """Give a generated kernel a distinct entry name: ``<base>_<kind>_<h>``,
+  h = 8 hex digits of the source's SHA-1 (e.g. spx_reduce_cols_1a2b3c4d), so
+  rocprofv3 reports every generated kernel on its own row instead of folding
+  all of them into one 'spx_reduce' line.  Returns (source, name)."""
+  import hashlib
+  h = hashlib.sha1(src.encode()).hexdigest()[:8]
+  name = '%s_%s_%s' % (base, kind, h)
+  old = 'KERN void %s(' % base
+  assert src.count(old) == 1, 'generated source has no single %s entry' % base
+  return src.replace(old, 'KERN void %s(' % name), name
+
+
 # ---------------------------------------------------------------- map
 def gen_map(root, inputs, classes, ndim, vec, dense, nt_store=False):
   """Elementwise kernel.  inputs: [(slot, dtype)], classes: per-input 'c'/'b'/'g'.

@@ -12,7 +12,8 @@ Data plane, by ``ctx.dist_backend``:
   (``SPARTAN_DIST_BACKEND=gloo``), where device tensors are staged through
   host memory.
 * ``'nccl'``: torch.distributed's own RCCL process group
-  (``SPARTAN_COMM=torch``, a debugging switch).
+  (``SPARTAN_COMM=torch``; also the fallback when the libspx communicator
+  fails its start-up self-test, ``selftest``).
 
 Replaces the reference's pickled ZeroMQ point-to-point messages
 (spartan/rpc/common.py:52-62, spartan/blob_ctx.py:127-179): every exchange
@@ -20,6 +21,8 @@ here is a collective that all ranks enter with identical arguments, because
 every rank computes the same tile plan (SPMD).
 """
 import ctypes
+import os
+import zlib
 
 from . import runtime
 
@@ -30,6 +33,12 @@ _SPX_OP = {'sum': 0, 'min': 1, 'max': 2}
 def _dist():
   import torch.distributed as dist
   return dist
+
+
+def _grp():
+  """The torch process group of the data plane: torch's own RCCL group when
+  the runtime fell back to it, else the default group."""
+  return getattr(runtime.get(), 'pg', None)
 
 
 def _staged(ctx, t):
@@ -99,11 +108,72 @@ def _contig(t, what):
     raise ValueError('%s needs a contiguous tensor' % what)
 
 
+# ---------------------------------------------------------------- SPMD guard
+# Every rank must issue the same collectives in the same order (each rank
+# computes the same tile plan); a divergence would otherwise show up as a hang
+# inside RCCL / gloo.  Each collective (and each plan-cache decision) folds
+# its name and shapes into a running CRC; the ranks compare it on the control
+# plane -- before every collective with SPARTAN_SPMD_GUARD=strict (the tests),
+# every N-th collective and at every barrier with SPARTAN_SPMD_GUARD=N (the
+# default, 64), never with 0 -- and raise RuntimeError on a mismatch.
+_GUARD = {'h': 0, 'n': 0, 'last': ()}
+
+
+def _guard_every():
+  v = os.environ.get('SPARTAN_SPMD_GUARD', '64').strip().lower()
+  if v == 'strict':
+    return 1
+  try:
+    return max(0, int(v))
+  except ValueError:
+    return 64
+
+
+def spmd_note(*desc):
+  """Fold ``desc`` (plain values) into this rank's running SPMD hash."""
+  ctx = runtime._ctx
+  if ctx is None or not ctx.distributed:
+    return
+  _GUARD['h'] = zlib.crc32(repr(desc).encode(), _GUARD['h'])
+  _GUARD['n'] += 1
+  _GUARD['last'] = desc
+
+
+def spmd_check(where='check'):
+  """Collective on the control plane: raise RuntimeError if the ranks'
+  running hashes differ."""
+  import torch
+  ctx = runtime.get()
+  if not ctx.distributed:
+    return
+  h = _GUARD['h']
+  dev = ctx.device if _dist().get_backend() == 'nccl' else torch.device('cpu')
+  t = torch.tensor([h, -h], dtype=torch.int64, device=dev)
+  _dist().all_reduce(t, op=_dist().ReduceOp.MAX)
+  hi, lo = int(t[0].item()), -int(t[1].item())
+  if hi != h or lo != h:
+    raise RuntimeError('SPMD divergence at %s: rank %d issued a different sequence of collectives than '
+                       'another rank (hash %08x, ranks span %08x..%08x after %d notes; last: %r)'
+                       % (where, ctx.rank, h, lo, hi, _GUARD['n'], _GUARD['last']))
+
+
+def _guard(*desc):
+  spmd_note(*desc)
+  every = _guard_every()
+  if every and _GUARD['n'] % every == 0:
+    spmd_check(desc[0])
+
+
+def _tdesc(t):
+  return (tuple(t.shape), str(t.dtype))
+
+
 # ------------------------------------------------------------- collectives
 def all_reduce(t, op):
   ctx = runtime.get()
   if not ctx.distributed:
     return t
+  _guard('all_reduce', op, _tdesc(t))
   if ctx.dist_backend == 'rccl':
     _contig(t, 'all_reduce')
     _check(_lib().spx_allreduce(ctx.rccl, _p(t), _p(t), t.numel(), _dt(t), _SPX_OP[op], _stream()),
@@ -115,13 +185,14 @@ def all_reduce(t, op):
     dist.all_reduce(h, op=getattr(dist.ReduceOp, _OPS[op]))
     t.copy_(h)
     return t
-  dist.all_reduce(t, op=getattr(dist.ReduceOp, _OPS[op]))
+  dist.all_reduce(t, op=getattr(dist.ReduceOp, _OPS[op]), group=_grp())
   return t
 
 
 def reduce_scatter_rows(out, full, op):
   """out = rank-th equal row slab of the element-wise reduction of ``full``."""
   ctx = runtime.get()
+  _guard('reduce_scatter', op, _tdesc(out), _tdesc(full))
   if ctx.dist_backend == 'rccl':
     _contig(out, 'reduce_scatter')
     _contig(full, 'reduce_scatter')
@@ -135,7 +206,7 @@ def reduce_scatter_rows(out, full, op):
     n = out.shape[0]
     out.copy_(full[ctx.rank * n:(ctx.rank + 1) * n])
     return out
-  dist.reduce_scatter_tensor(out, full, op=getattr(dist.ReduceOp, _OPS[op]))
+  dist.reduce_scatter_tensor(out, full, op=getattr(dist.ReduceOp, _OPS[op]), group=_grp())
   return out
 
 
@@ -145,6 +216,7 @@ def all_gather_stack(t):
   ctx = runtime.get()
   if not ctx.distributed:
     return t.unsqueeze(0)
+  _guard('all_gather', _tdesc(t))
   out = torch.empty((ctx.world_size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
   if ctx.dist_backend == 'rccl':
     t = t.contiguous()
@@ -158,7 +230,7 @@ def all_gather_stack(t):
   elif ctx.dist_backend == 'gloo':
     dist.all_gather(list(out.unbind(0)), t.contiguous())
   else:
-    dist.all_gather_into_tensor(out, t.contiguous())
+    dist.all_gather_into_tensor(out, t.contiguous(), group=_grp())
   return out
 
 
@@ -166,6 +238,7 @@ def broadcast(t, src_rank):
   ctx = runtime.get()
   if not ctx.distributed:
     return t
+  _guard('broadcast', int(src_rank), _tdesc(t))
   if ctx.dist_backend == 'rccl':
     _contig(t, 'broadcast')
     _check(_lib().spx_broadcast(ctx.rccl, _p(t), _p(t), t.numel(), _dt(t), int(src_rank), _stream()),
@@ -176,7 +249,7 @@ def broadcast(t, src_rank):
     _dist().broadcast(h, src=src_rank)
     t.copy_(h)
     return t
-  _dist().broadcast(t, src=src_rank)
+  _dist().broadcast(t, src=src_rank, group=_grp())
   return t
 
 
@@ -200,6 +273,7 @@ def reduce_async(t, dst_rank, op):
   runs on a side stream, after the work already queued on the current
   stream and concurrently with what follows it."""
   ctx = runtime.get()
+  _guard('reduce', int(dst_rank), op, _tdesc(t))
   if ctx.dist_backend == 'rccl':
     import torch
     _contig(t, 'reduce')
@@ -220,7 +294,7 @@ def reduce_async(t, dst_rank, op):
     if ctx.rank == dst_rank:
       t.copy_(h)
     return None
-  return dist.reduce(t, dst=dst_rank, op=getattr(dist.ReduceOp, _OPS[op]), async_op=True)
+  return dist.reduce(t, dst=dst_rank, op=getattr(dist.ReduceOp, _OPS[op]), group=_grp(), async_op=True)
 
 
 def wait_all(handles):
@@ -235,7 +309,12 @@ def exchange(sends, recvs):
   Every rank passes the pairs it takes part in; messages between the same pair
   of ranks are matched in list order."""
   ctx = runtime.get()
-  if not ctx.distributed or (not sends and not recvs):
+  if not ctx.distributed:
+    return
+  # every rank enters (the plans are identical); what each sends differs by
+  # rank, so only the call itself is folded into the SPMD hash
+  _guard('exchange')
+  if not sends and not recvs:
     return
   import torch
   if ctx.dist_backend == 'rccl':
@@ -265,12 +344,65 @@ def exchange(sends, recvs):
       else:
         staged.append((t, peer))
     recvs = staged
-  ops = [dist.P2POp(dist.isend, t.contiguous(), peer) for t, peer in sends]
-  ops += [dist.P2POp(dist.irecv, t, peer) for t, peer in recvs]
+  g = _grp()
+  ops = [dist.P2POp(dist.isend, t.contiguous(), peer, group=g) for t, peer in sends]
+  ops += [dist.P2POp(dist.irecv, t, peer, group=g) for t, peer in recvs]
   for req in dist.batch_isend_irecv(ops):
     req.wait()
   for t, h in post:
     t.copy_(h)
+
+
+def selftest():
+  """Exercise every collective of the data plane once on small tensors and
+  check the results on the host; returns None, or a description of the first
+  wrong result / error.  All ranks call it (collective) and all get the same
+  verdict (a max over ranks on the control plane).  runtime.initialize runs
+  it on the libspx RCCL communicator before any tile data moves, and falls
+  back to torch.distributed's own RCCL group if it fails."""
+  import torch
+  ctx = runtime.get()
+  if not ctx.distributed:
+    return None
+  W, r = ctx.world_size, ctx.rank
+  dev = ctx.device
+  err = None
+  try:
+    base = torch.arange(4 * W, dtype=torch.float32, device=dev)
+    t = base + float(r)
+    all_reduce(t, 'sum')
+    want = (W * torch.arange(4 * W, dtype=torch.float64) + W * (W - 1) / 2.0)
+    if not torch.equal(t.double().cpu(), want):
+      err = 'all_reduce(sum) wrong'
+    full = base.double() * (r + 1)
+    out = torch.empty((4,), dtype=torch.float64, device=dev)
+    reduce_scatter_rows(out, full, 'sum')
+    want = torch.arange(4 * W, dtype=torch.float64)[4 * r:4 * r + 4] * (W * (W + 1) / 2.0)
+    if err is None and not torch.equal(out.cpu(), want):
+      err = 'reduce_scatter(sum) wrong'
+    mx = torch.full((3,), float(r), dtype=torch.float64, device=dev)
+    all_reduce(mx, 'max')
+    if err is None and not bool((mx.cpu() == W - 1).all()):
+      err = 'all_reduce(max) wrong'
+    g = all_gather_stack(torch.full((3,), r, dtype=torch.int64, device=dev))
+    if err is None and not torch.equal(g.cpu(), torch.arange(W, dtype=torch.int64).repeat_interleave(3).view(W, 3)):
+      err = 'all_gather wrong'
+    b = torch.full((5,), 7 * r + 1, dtype=torch.int64, device=dev)
+    broadcast(b, W - 1)
+    if err is None and not bool((b.cpu() == 7 * (W - 1) + 1).all()):
+      err = 'broadcast wrong'
+    src = torch.full((6,), 10 * r + 3, dtype=torch.int32, device=dev)
+    dst = torch.empty((6,), dtype=torch.int32, device=dev)
+    exchange([(src, (r + 1) % W)], [(dst, (r - 1) % W)])
+    if err is None and not bool((dst.cpu() == 10 * ((r - 1) % W) + 3).all()):
+      err = 'send/recv wrong'
+    torch.cuda.synchronize(dev) if dev.type == 'cuda' else None
+  except Exception as e:  # noqa: BLE001  (reported to the caller, which decides)
+    err = '%s: %s' % (type(e).__name__, e)
+  bad = max_over_ranks(1.0 if err else 0.0)
+  if bad and err is None:
+    err = 'another rank failed'
+  return err
 
 
 def barrier():
@@ -278,6 +410,8 @@ def barrier():
   streams around it)."""
   ctx = runtime.get()
   if ctx.distributed:
+    if _guard_every():
+      spmd_check('barrier')
     _dist().barrier()
 
 
@@ -287,7 +421,9 @@ def max_over_ranks(x):
   ctx = runtime.get()
   if not ctx.distributed:
     return x
-  dev = ctx.device if ctx.dist_backend == 'nccl' else torch.device('cpu')
+  # the default (control-plane) group: gloo -> a host tensor; nccl only when
+  # the whole job runs on torch's RCCL group (SPARTAN_COMM=torch)
+  dev = ctx.device if _dist().get_backend() == 'nccl' else torch.device('cpu')
   t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
   _dist().all_reduce(t, op=_dist().ReduceOp.MAX)
   return float(t.item())

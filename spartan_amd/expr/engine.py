@@ -24,7 +24,7 @@ from ..array import distarray, extent as ext
 from ..array.distarray import DistArrayImpl, LocalWrapper, ReplicatedArray
 from ..util import prod
 from .broadcast import Broadcast
-from .local import CodegenError, LowerEnv, Pre, has_location, lower
+from .local import CodegenError, LowerEnv, Pre, UntraceableMapper, has_location, host_evaluate, lower
 
 
 # --------------------------------------------------------------- binding
@@ -55,7 +55,9 @@ def bind(children, child_to_var, op, extent=None):
     desc = []
     for child in children:
       sv = _scalar_value(child)
-      desc.append(('a', child.dtype.str) if sv is None else (type(sv), sv))
+      # floats by their repr: 0.0 and -0.0 (and nan) must not share a lowering
+      desc.append(('a', child.dtype.str) if sv is None else
+                  (type(sv), repr(sv) if isinstance(sv, (float, np.floating)) else sv))
     key = (id(op), tuple(child_to_var), tuple(desc))
     hit = _BIND_MEMO.get(key)
     if hit is not None:
@@ -202,12 +204,79 @@ def run_location_map(children, child_to_var, op):
   return distarray.from_tiles(largest.shape, dtype, tiles, out_local)
 
 
+# ------------------------------------------------ untraceable user mappers
+HOST_MAPPER_CALLS = [0]   # tiles evaluated on the host (tests assert on it)
+_HOST_WARNED = set()
+
+
+def _agree_dtype(dt):
+  """The result dtype every rank uses: ranks without a local tile learn it
+  from the others (control plane); ranks that disagree raise."""
+  codes = [np.dtype(t) for t in (np.bool_, np.int32, np.int64, np.float32, np.float64)]
+  if dt is not None and np.dtype(dt) not in codes:
+    raise TypeError('mapper result dtype %s is not supported by the MI355X backend' % dt)
+  mine = -1 if dt is None else codes.index(np.dtype(dt))
+  hi = int(comm.max_over_ranks(float(mine)))
+  lo = -int(comm.max_over_ranks(float(-mine if mine >= 0 else -99)))
+  if hi < 0:
+    raise ValueError('map over an array without tiles')
+  if mine >= 0 and (lo != hi or mine != hi):
+    raise CodegenError('mapper yields different dtypes on different ranks')
+  return codes[hi]
+
+
+def run_host_map(children, child_to_var, op, err):
+  """A map whose tree holds an untraceable USER mapper, evaluated like the
+  reference's tile_mapper (spartan/expr/map.py:48-88): per local tile, the
+  inputs come to the host (broadcast children as their base tiles, so NumPy
+  broadcasts inside the mapper, as fetch_base_tile does), the tree runs in
+  NumPy (local.host_evaluate), the result is checked against the tile shape
+  and uploaded.  Counted in HOST_MAPPER_CALLS; warns once per mapper."""
+  import warnings
+  from ..array import transfer
+  ctx = runtime.get()
+  key = getattr(err, 'fn', None)
+  if key not in _HOST_WARNED:
+    _HOST_WARNED.add(key)
+    warnings.warn('spartan_amd: %s -- evaluating it per tile on the host (NumPy), as the reference does' % err,
+                  RuntimeWarning, stacklevel=3)
+  largest = distarray.largest_value(children)
+  tiles = driving_tiles(largest)
+  arrays = {i: i for i, c in enumerate(children) if _scalar_value(c) is None}
+  per_ex = fetch_inputs(children, arrays, tiles)
+  out_local, dtype = {}, None
+  for ex, fetched in per_ex.items():
+    env = {'extent': ex}
+    for i, (c, var) in enumerate(zip(children, child_to_var)):
+      sv = _scalar_value(c)
+      env[var] = sv if sv is not None else transfer.download(fetched[i])
+    res = np.asarray(host_evaluate(op, env))
+    shape = ex.shape if ex.ndim else ()
+    if tuple(res.shape) != tuple(shape):  # tile_mapper's Assert.eq (map.py:80-82)
+      raise AssertionError('Bad shape -- tile %s, mapper result %s' % (shape, res.shape))
+    if dtype is not None and res.dtype != dtype:
+      raise CodegenError('mapper yields %s on one tile and %s on another' % (dtype, res.dtype))
+    dtype = res.dtype
+    out_local[ex] = res
+    HOST_MAPPER_CALLS[0] += 1
+  dtype = _agree_dtype(dtype)
+  out_local = {ex: transfer.upload(np.ascontiguousarray(res, dtype=dtype), ctx.device)
+               for ex, res in out_local.items()}
+  if all(w == -1 for w in tiles.values()):
+    (ex, out), = out_local.items()
+    return ReplicatedArray(out)
+  return distarray.from_tiles(largest.shape, dtype, tiles, out_local)
+
+
 def run_map(children, child_to_var, op):
   ctx = runtime.get()
-  if has_location(op):
-    return run_location_map(children, child_to_var, op)
-  largest = distarray.largest_value(children)
-  root, slots, pres = bind(children, child_to_var, op)
+  try:
+    if has_location(op):
+      return run_location_map(children, child_to_var, op)
+    largest = distarray.largest_value(children)
+    root, slots, pres = bind(children, child_to_var, op)
+  except UntraceableMapper as e:
+    return run_host_map(children, child_to_var, op, e)
   tiles = driving_tiles(largest)
   replicated = all(w == -1 for w in tiles.values())
   # identity map returns the driving input itself (map.py:76-77)
@@ -256,7 +325,15 @@ def run_reduce(children, child_to_var, local_op, axis, dtype, accumulate_fn, til
   opname, transform = REDUCE_FNS[fn]
   tree = local_op.deps[1]
   largest = distarray.largest_value(children)
-  root, slots, pres = bind(children, child_to_var, tree)
+  try:
+    root, slots, pres = bind(children, child_to_var, tree)
+  except UntraceableMapper as e:
+    # the mapped values on the host (reference semantics), then the same
+    # device reduction over the materialised tiles
+    from .local import LocalInput, LocalReduceExpr
+    m = run_host_map(children, child_to_var, tree, e)
+    return run_reduce([m], ['_host0'], LocalReduceExpr(fn=fn, deps=[LocalInput('extent'), LocalInput('_host0')]),
+                      axis, dtype, accumulate_fn, tile_hint)
   if transform is not None:
     root = transform(root)
   in_shape_full = largest.shape

@@ -13,10 +13,14 @@ Lowering rules (``lower``):
                                          generator leaves materialised by spx_fill);
   * any other Python callable         -> traced once with symbolic proxies
                                          (operators and ufuncs on the proxies
-                                         record IR); if tracing fails the map
-                                         cannot run on the GPU and
-                                         ``CodegenError`` is raised -- there is
-                                         no host fallback.
+                                         record IR); if tracing fails
+                                         (``UntraceableMapper``) the tree is
+                                         evaluated per tile on the host exactly
+                                         as the reference does
+                                         (``host_evaluate``; counted in
+                                         engine.HOST_MAPPER_CALLS, warned once).
+                                         Trees of ufuncs / builtins never take
+                                         that path.
 """
 import itertools
 
@@ -29,6 +33,17 @@ _var_ids = itertools.count()
 
 class CodegenError(NotImplementedError):
   pass
+
+
+class UntraceableMapper(CodegenError):
+  """A USER mapper whose body cannot be traced into a kernel (data-dependent
+  control flow, NumPy calls other than ufuncs on the tile, ...).  The engine
+  then evaluates the tree on the host exactly as the reference does
+  (engine.run_host_map); builtin ufunc trees never raise this."""
+
+  def __init__(self, msg, fn=None):
+    super().__init__(msg)
+    self.fn = fn
 
 
 def make_var():
@@ -274,16 +289,30 @@ def trace_callable(fn, args, kw, env, extra=()):
   syms = [Sym(a, env) for a in args]
   try:
     out = fn(*syms, *extra, **kw)
-  except CodegenError:
-    raise
   except Exception as e:
-    raise CodegenError('mapper %s cannot be lowered to a gfx950 kernel (%s: %s)'
-                       % (getattr(fn, '__name__', fn), type(e).__name__, e))
+    raise UntraceableMapper('mapper %s cannot be lowered to a gfx950 kernel (%s: %s)'
+                            % (getattr(fn, '__name__', fn), type(e).__name__, e), fn)
   if isinstance(out, Sym):
     return out.node
   if extra and args and isinstance(out, (bool, int, float, np.generic)) and np.ndim(out) == 0:
     # a location mapper returning a scalar for a whole tile (e.g. nbody.py:30-40
     # _set_diagonal_mapper): the tile is filled with it, in the input's dtype
     return codegen.Const(out.item() if isinstance(out, np.generic) else out, args[0].dtype)
-  raise CodegenError('mapper %s did not return a traced tile value'
-                     % getattr(fn, '__name__', fn))
+  raise UntraceableMapper('mapper %s did not return a traced tile value' % getattr(fn, '__name__', fn), fn)
+
+
+def host_evaluate(op, env):
+  """The reference's per-tile evaluation of a LocalExpr tree
+  (FnCallExpr.evaluate, spartan/expr/local.py:110-122, and
+  LocalMapLocationExpr.evaluate, :133-142): ``fn(*deps, **kw)`` on host NumPy
+  tiles, recursively.  ``env``: var name -> NumPy tile / scalar, 'extent' ->
+  the TileExtent.  Used only for trees holding an untraceable USER mapper."""
+  if isinstance(op, LocalInput):
+    return env[op.idx]
+  deps = []
+  for d in op.deps:
+    if isinstance(d, LocalInput) and d.idx == 'extent' and isinstance(op, LocalMapLocationExpr):
+      deps.append(env['extent'].to_tuple())
+    else:
+      deps.append(host_evaluate(d, env))
+  return op.fn(*deps, **op.kw)

@@ -35,7 +35,10 @@ The signature is the DAG's structure with leaves abstracted:
     plain scalars, strings, dtypes: value;
   * whether a node's value is already in the evaluation cache (the template
     then holds that value as a slot, as CollapsedCachedExpressions made it a
-    Val), and the optimisation flags / worker count the passes read.
+    Val), the tiling an earlier AutomaticTiling pinned on a node, and the
+    optimisation flags / worker count the passes read.
+Replay also repeats AutomaticTiling's side effect: each instantiated node
+gets the tiling the template's node was given (optimize._tiled_exprs).
 A structure whose optimised form holds a host array that is neither a leaf
 of the input nor a contiguous same-size view of one (a pass derived new
 values) is not cached: it is optimised every time, as before.
@@ -100,6 +103,8 @@ class _Sig:
     self.nodes = []       # input Expr nodes in memo order
     self.keep = []        # objects whose identity is part of the key
     self.Expr, self.LocalExpr, self.DistArray, self.cache = _classes()
+    from .optimize import _tiled_exprs
+    self.tiled = _tiled_exprs
 
   def slot(self, obj):
     k = id(obj)
@@ -134,8 +139,10 @@ class _Sig:
       if cached is not None:  # CollapsedCachedExpressions turns it into a Val of this value
         return ('cached', t, self.slot(cached) or self._obj_sig(cached))
       # attributes in insertion order: a node built another way only misses
-      # (the names are part of the key), never collides
-      return (t,) + tuple([(a, self.walk(b)) for a, b in v.__dict__.items() if a not in _SKIP])
+      # (the names are part of the key), never collides; plus the tiling an
+      # earlier optimisation pinned on this node (AutomaticTiling reads it)
+      return (t, self.tiled.get(v.expr_id)) + tuple(
+          [(a, self.walk(b)) for a, b in v.__dict__.items() if a not in _SKIP])
     if isinstance(v, self.LocalExpr):
       return (t,) + tuple([(a, self.walk(b)) for a, b in v.__dict__.items()])
     if t is np.ndarray:
@@ -238,6 +245,10 @@ def _template(v, slot_ids, slots, memo, id2pos=None):
       new.__dict__[a] = _template(b, slot_ids, slots, memo, id2pos)
     if isinstance(v, Expr):
       new.__dict__['_tpl_pos'] = id2pos.get(v.expr_id)
+      # the tiling AutomaticTiling chose for this node: replay pins it on the
+      # instance's node too, as a fresh optimisation would have
+      from .optimize import _tiled_exprs
+      new.__dict__['_tpl_tiling'] = _tiled_exprs.get(v.expr_id)
     elif _pure(new.__dict__):
       # no slot, view or expression inside: every instantiation shares this
       # tree object (engine.bind lowers it once per binding pattern)
@@ -274,6 +285,8 @@ class _Inst:
   def __init__(self, Expr, LocalExpr, cache, new_id, slots, nodes):
     self.Expr, self.LocalExpr, self.cache, self.new_id, self.slots = Expr, LocalExpr, cache, new_id, slots
     self.nodes = nodes
+    from .optimize import _tiled_exprs
+    self.tiled = _tiled_exprs
     self.memo = {}
 
   def run(self, v):
@@ -299,27 +312,34 @@ class _Inst:
       self.memo[k] = new
       nd = new.__dict__
       for a, b in v.__dict__.items():
-        if a != '_tpl_pos':
+        if a != '_tpl_pos' and a != '_tpl_tiling':
           nd[a] = self.run(b)
       if isinstance(v, self.Expr):
         pos = v.__dict__.get('_tpl_pos')
         new.expr_id = self.nodes[pos].expr_id if pos is not None else self.new_id()
         self.cache.register(new.expr_id)
+        tiling = v.__dict__.get('_tpl_tiling')
+        if tiling is not None:
+          self.tiled[new.expr_id] = tiling
       return new
     return v
 
 
 def optimize_cached(dag, run_passes):
   """``run_passes(dag)``, or the replay of an earlier identical structure."""
+  from .. import comm
   key, st = signature(dag)
   if key is None:
     STATS['uncacheable'] += 1
+    comm.spmd_note('plan', 'uncacheable')
     return run_passes(dag)
   entry = _PLANS.get(key)
   if entry is not None:
     STATS['hits'] += 1
+    comm.spmd_note('plan', 'hit')
     return _instantiate(entry[0], st.slots, st.nodes)
   STATS['misses'] += 1
+  comm.spmd_note('plan', 'miss')
   opt = run_passes(dag)
   try:
     tpl = _template(opt, {id(o): i for i, o in enumerate(st.slots)}, st.slots, {},

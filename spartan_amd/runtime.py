@@ -26,6 +26,8 @@ class Context:
     self.dist_backend = dist_backend   # data plane: 'rccl' (libspx), 'gloo' (tests / rehearsal), 'nccl' (torch)
     self.rccl = rccl                   # libspx RCCL communicator handle when dist_backend == 'rccl'
     self._comm_stream = None
+    self.pg = None          # torch process group of the data plane when dist_backend == 'nccl' (None: default)
+    self.selftest = None    # data-plane self-test verdict at start-up (multi-rank RCCL only)
     self.num_workers = int(FLAGS.num_workers or world_size)
     if self.num_workers < 1:
       raise ValueError('num_workers must be >= 1')
@@ -102,6 +104,24 @@ def initialize(argv=None, device=None):
       dist.broadcast_object_list(obj, src=0)
       rccl = comm.rccl_init(rank, world, obj[0])
   _ctx = Context(rank, world, local_rank, device, backend, rccl)
+  if backend == 'rccl' and os.environ.get('SPARTAN_RCCL_SELFTEST', '1') != '0':
+    # every collective of the libspx data plane, once, on small tensors,
+    # checked on the host before any tile moves; a wrong result or an error
+    # moves the data plane to torch.distributed's own RCCL group (loudly)
+    from . import comm
+    err = comm.selftest()
+    _ctx.selftest = err or 'ok'
+    if err:
+      import warnings
+      warnings.warn('spartan_amd: the libspx RCCL data plane failed its self-test (%s); '
+                    'using torch.distributed\'s RCCL process group instead' % err)
+      import torch.distributed as dist
+      _ctx.pg = dist.new_group(backend='nccl')
+      _ctx.dist_backend = 'nccl'
+      _ctx.rccl = None  # not destroyed: a communicator in an unknown state may block in ncclCommDestroy
+      bad = comm.selftest()
+      if bad:
+        raise RuntimeError('spartan_amd: no working GPU data plane (libspx RCCL: %s; torch RCCL: %s)' % (err, bad))
   return _ctx
 
 

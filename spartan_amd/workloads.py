@@ -35,7 +35,7 @@ def sgd_train(x, y, w, alpha, iterations):
   return w
 
 
-def kmeans_fit(X, n_clusters, n_iter, centers=None, seed=0):
+def kmeans_fit(X, n_clusters, n_iter, centers=None, seed=0, info=None):
   """KMeans.fit, 'outer' implementation (spartan/examples/sklearn/cluster/
   k_means_.py:108-152), one fused pass pair per iteration on every rank:
 
@@ -54,7 +54,9 @@ def kmeans_fit(X, n_clusters, n_iter, centers=None, seed=0):
 
   X: (N, D) expression or DistArray (row strips).  centers: (K, D) host array
   or None (first K rows of X).  Returns (centers (K, D) fp64 host array,
-  labels DistArray (N,) int64 tiled like X's rows)."""
+  labels DistArray (N,) int64 tiled like X's rows).  ``info`` (a dict, optional)
+  receives 'assign_centers': the (K, D) centres the returned labels were
+  assigned against (bench.py's post-timing check)."""
   import torch
   from . import backend, comm, runtime
   from .array import distarray, extent as ext
@@ -71,6 +73,8 @@ def kmeans_fit(X, n_clusters, n_iter, centers=None, seed=0):
     assert ex.ul[1] == 0 and ex.lr[1] == D, 'k-means needs row-strip tiles (k_means_.py:116)'
   label_tiles = {}
   for it in range(n_iter):
+    if info is not None:
+      info['assign_centers'] = centers
     cdev = torch.as_tensor(centers).to(ctx.device)
     # sums and counts share one buffer: one D2H per iteration
     buf = torch.empty((K * D + K,), dtype=torch.float64, device=ctx.device)

@@ -42,9 +42,9 @@ def _body(rank, world, port, W, q):
     sys.path.insert(0, os.path.dirname(HERE))
     sys.path.insert(0, HERE)
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), SPARTAN_SPMD_GUARD='strict')
     import torch
-    from spartan_amd import backend, runtime, expr
+    from spartan_amd import backend, runtime, expr, comm
     from spartan_amd.config import FLAGS
     from fake_backend import FakeBackend
     from oracle import rng
@@ -54,6 +54,8 @@ def _body(rank, world, port, W, q):
     runtime.initialize(device='cpu')
     ctx = runtime.get()
     assert ctx.world_size == world and ctx.dist_backend == 'gloo'
+    # the data-plane self-test the runtime runs on a multi-rank RCCL start
+    assert comm.selftest() is None
 
     # placement: only the local tiles hold data
     x = expr.arange((40, 30), dtype=np.int64).force()
@@ -176,6 +178,47 @@ def _body(rank, world, port, W, q):
       runtime.shutdown()
     except Exception:
       pass
+
+
+def _diverge_body(rank, world, port, q):
+  """Rank 1 issues a collective with another shape than rank 0's: the SPMD
+  guard must raise on both ranks instead of letting the collective hang."""
+  try:
+    sys.path.insert(0, os.path.dirname(HERE))
+    sys.path.insert(0, HERE)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), SPARTAN_SPMD_GUARD='strict')
+    import torch
+    from spartan_amd import backend, runtime, comm
+    from fake_backend import FakeBackend
+    backend.set_backend(FakeBackend())
+    runtime.initialize(device='cpu')
+    comm.all_reduce(torch.ones(4), 'sum')    # identical on both ranks: fine
+    comm.barrier()
+    try:
+      comm.all_reduce(torch.ones(4 + rank), 'sum')  # divergent
+      q.put((rank, 'no error'))
+    except RuntimeError as e:
+      q.put((rank, 'raised' if 'SPMD divergence' in str(e) else repr(e)))
+  except Exception:  # pragma: no cover
+    import traceback
+    q.put((rank, traceback.format_exc()))
+
+
+def test_spmd_guard_divergence_raises():
+  import multiprocessing as mp
+  ctx = mp.get_context('spawn')
+  q = ctx.Queue()
+  port = _free_port()
+  procs = [ctx.Process(target=_diverge_body, args=(r, 2, port, q)) for r in range(2)]
+  for p in procs:
+    p.start()
+  res = dict(q.get(timeout=120) for _ in procs)
+  for p in procs:
+    p.join(timeout=30)
+    if p.is_alive():
+      p.kill()
+  assert res == {0: 'raised', 1: 'raised'}, res
 
 
 @pytest.mark.parametrize('W', [2, 3, 4])

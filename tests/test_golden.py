@@ -129,6 +129,8 @@ def test_gpu_cfg2_golden(ex, tag, W):
     check_fp(got, g['sum_' + k], m.astype(np.float64).sum(ax), 1e-5)
     for red in ('min', 'max'):
       got = getattr(expr, red)(x * y + expr.exp(z), axis=ax).optimized().glom()
+      # selections: bit-exact on the GPU's own map values, 1e-6 of the frozen vector
+      np.testing.assert_array_equal(got, getattr(O, red + '_tiles')(m, ax, W))
       np.testing.assert_allclose(got, g['%s_%s' % (red, k)], rtol=1e-6)
     for kind in ('argmin', 'argmax'):
       got = getattr(expr, kind)(x * y + expr.exp(z), axis=ax).optimized().glom()

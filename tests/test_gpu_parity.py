@@ -251,6 +251,29 @@ def test_dot_cfg4_full_size(ex, dtype, rtol):
       cpu = np.dot(arow, bcol)
       exact = np.dot(arow.astype(f64), bcol.astype(f64))
       check_fp(np.array([crow[c]]), np.array([cpu]), np.array([exact]), rtol)
+  # one FULL row and one FULL column of C against host dots over the whole of
+  # B / A (the device values, bit-exact to the generator by
+  # test_rand_bit_exact), streamed in 4096-row blocks: the dtype's own dot
+  # (the CPU reference) and the fp64-exact one, same rule
+  r, c = 20000, 30001
+  crow = Ce[r:r + 1, :].glom().reshape(S)
+  ccol = Ce[:, c:c + 1].glom().reshape(S)
+  arow = Ae[r:r + 1, :].glom().reshape(S)
+  bcol = Be[:, c:c + 1].glom().reshape(S)
+  row_cpu = np.zeros(S, dtype)
+  row_ex = np.zeros(S, f64)
+  col_cpu = np.zeros(S, dtype)
+  col_ex = np.zeros(S, f64)
+  for k0 in range(0, S, 4096):
+    bblk = Be[k0:k0 + 4096, :].glom()
+    row_cpu += arow[k0:k0 + 4096] @ bblk
+    row_ex += arow[k0:k0 + 4096].astype(f64) @ bblk.astype(f64)
+    ablk = Ae[k0:k0 + 4096, :].glom()
+    col_cpu[k0:k0 + 4096] = ablk @ bcol
+    col_ex[k0:k0 + 4096] = ablk.astype(f64) @ bcol.astype(f64)
+    del bblk, ablk
+  check_fp(crow, row_cpu, row_ex, rtol)
+  check_fp(ccol, col_cpu, col_ex, rtol)
   del A, B, C, Ae, Be, Ce
 
 
@@ -304,6 +327,10 @@ def test_fused_map_reduce_cfg2(ex, shape, W):
     check_fp(got, cpu, exact_src.sum(axis), 1e-5)
     for red, oref in [(expr.min, O.min_tiles), (expr.max, O.max_tiles)]:
       got = red(x * y + expr.exp(z), axis=axis).optimized().glom()
+      # a min / max only selects an element: bit-exact against the reference's
+      # tile-wise reduction of the GPU's own materialised map (whatever ulps
+      # OCML's exp differs from NumPy's by), and within 1e-6 of the host map's
+      np.testing.assert_array_equal(got, oref(m, axis, W))
       np.testing.assert_allclose(got, oref(mapped, axis, W), rtol=1e-6)
     for kind in ['argmin', 'argmax']:
       got = getattr(expr, kind)(x * y + expr.exp(z), axis=axis).optimized().glom()
@@ -313,6 +340,33 @@ def test_fused_map_reduce_cfg2(ex, shape, W):
       np.testing.assert_array_equal(got, O.arg_tiles(m, axis, W, kind))
       if (m == mapped).all():
         np.testing.assert_array_equal(got, O.arg_tiles(mapped, axis, W, kind))
+
+
+def test_arg_axis_none_block_tiles(ex):
+  """The documented axis=None divergence: (2, 100)
+  at W = 3 is tiled in blocks of (1, 66) (good_tile_shape fills the last
+  axis first), so the reference's _arg_mapper ravels a tile's local index
+  with the TILE shape (builtins.py:618-624, restated by the oracle) and
+  returns a position that is not NumPy's flat index; this build returns
+  NumPy's.  Both answers are stated here."""
+  expr, setw = ex
+  setw(3)
+  a = np.full((2, 100), 5.0)
+  a[1, 70] = -3.0   # min in the (1, 66:100) block
+  a[0, 10] = 9.0    # max in the first block
+  from spartan_amd.array import distarray
+  tiles = sorted((ex_.ul, ex_.lr) for ex_ in distarray.from_numpy(a).tiles)
+  assert tiles[0] == ((0, 0), (1, 66)), tiles
+  x = expr.from_numpy(a)
+  got_min = int(expr.argmin(x).glom())
+  got_max = int(expr.argmax(x).glom())
+  assert got_min == int(np.argmin(a)) == 170
+  assert got_max == int(np.argmax(a)) == 10
+  # the reference's answer: ravelled_pos((1, 66) + (0, 4), tile shape (1, 34)) = 104
+  ref_min = int(O.arg_tiles(a, None, 3, 'argmin'))
+  ref_max = int(O.arg_tiles(a, None, 3, 'argmax'))
+  assert ref_min == 104 and ref_min != got_min
+  assert ref_max == 10 == got_max  # first block: ul = 0, both agree
 
 
 @pytest.mark.parametrize('W', [1, 3, 4])
@@ -960,6 +1014,35 @@ def test_multirank_rehearsal_gpu(tmp_path):
   assert r.stdout.count('rehearsal ok') == 2, r.stdout[-2000:]
 
 
+def test_bench_two_ranks_gpu():
+  """bench.py --gpus 2 exactly as the driver's scaling sweep starts it by
+  hand: no RANK in the environment, so bench.py launches its own two ranks
+  (launch_ranks -> torch.distributed.run) and relays rank 0's line.  Both
+  ranks share this box's one GPU, so the data plane is the gloo rehearsal
+  (SPARTAN_DIST_BACKEND=gloo; RCCL refuses two ranks on one device); every
+  leg runs at small sizes and validates its own outputs.  Reference harness:
+  tests/test_common.py:102-121 (worker-count sweep)."""
+  import json
+  import subprocess
+  env = {k: v for k, v in os.environ.items() if k not in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK')}
+  env.update(SPARTAN_DIST_BACKEND='gloo', SPARTAN_SPMD_GUARD='strict')
+  cmd = [sys.executable, os.path.join(os.path.dirname(HERE), 'bench.py'), '--gpus', '2', '--size', '4096',
+         '--steps', '2', '--warmup', '1', '--dot-size', '2048', '--km-points', '200000', '--lreg-points',
+         '200000', '--cpu-baseline', '0']
+  r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280)
+  assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+  lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+  assert len(lines) == 1, r.stdout[-3000:]
+  d = json.loads(lines[0])
+  assert d['n_gpus'] == 2 and d['n_ranks_seen'] == 2 and d['scaling'] == 'weak'
+  assert d['config']['shape'] == [8192, 4096]   # weak scaling: one 4096-row strip per rank
+  assert d['checked'] is True
+  for leg in ('lreg', 'kmeans', 'kmeans_api'):
+    assert d[leg].get('checked') is True, (leg, d[leg])
+  for dt in ('f32', 'f64'):
+    assert d['dot'][dt]['checked'] is True, d['dot']
+
+
 @pytest.mark.parametrize('W', [1, 3])
 def test_nonfinite_reductions(ex, W):
   """NaN / +-inf through sum / min / max / argmin / argmax, across tiles:
@@ -1100,3 +1183,38 @@ def test_rccl_single_rank_collectives(ex):
   finally:
     torch.cuda.synchronize()
     comm.rccl_destroy(c)
+
+
+@pytest.mark.parametrize('W', [1, 3])
+def test_untraceable_mappers_gpu(ex, W):
+  """User mappers that cannot become a kernel (np.sort on the tile, a Python
+  branch on the tile's values) run per tile on the host as the reference
+  runs every mapper (local.py:110-122); counted, and results equal NumPy's.
+  A reduction over such a mapper reduces the uploaded tiles on the GPU."""
+  import warnings
+  expr, setw = ex
+  setw(W)
+  from spartan_amd.expr import engine
+  from spartan_amd.array import distarray
+  a = (rng.rand((300, 50), 5, np.float64) * 10.0).round()
+  x = expr.from_numpy(a)
+  tiles = sorted(distarray.from_numpy(a).tiles, key=lambda e: e.ul)
+  strips = [a[e.ul[0]:e.lr[0]] for e in tiles]
+
+  def branchy(t):
+    if t.sum() > 100 * t.shape[0] * 5:
+      return t * 2.0
+    return t - 1.0
+
+  n0 = engine.HOST_MAPPER_CALLS[0]
+  with warnings.catch_warnings():
+    warnings.simplefilter('ignore', RuntimeWarning)
+    np.testing.assert_array_equal(expr.map(x, lambda t: np.sort(t, axis=1)).glom(), np.sort(a, axis=1))
+    want = np.concatenate([branchy(s) for s in strips])
+    np.testing.assert_array_equal(expr.map(x, branchy).glom(), want)
+    np.testing.assert_allclose(expr.sum(expr.map(x, branchy), axis=0).optimized().glom(), want.sum(0),
+                               rtol=1e-12)
+  assert engine.HOST_MAPPER_CALLS[0] - n0 == 3 * len(tiles)
+  n1 = engine.HOST_MAPPER_CALLS[0]
+  np.testing.assert_allclose(expr.map(x, lambda t: t * t + 1.0).glom(), a * a + 1.0, rtol=1e-15)
+  assert engine.HOST_MAPPER_CALLS[0] == n1   # traceable: a generated kernel

@@ -99,15 +99,19 @@ def test_rand_is_tiling_independent(host_ctx):
   np.testing.assert_array_equal(outs[0], rng.rand((13, 11), 5, np.float32))
 
 
-def test_unlowerable_mapper_raises(host_ctx):
+def test_unlowerable_mapper_runs_like_the_reference(host_ctx):
+  """A mapper the tracer cannot lower runs per tile in NumPy: np.sort works;
+  a Python branch on an array's truth value fails exactly as it would in the
+  reference's FnCallExpr.evaluate (NumPy's ValueError)."""
   host_ctx(1)
+  import warnings
   from spartan_amd import expr
-  from spartan_amd.expr.local import CodegenError
   x = expr.ones((4,))
-  with pytest.raises(CodegenError):
-    expr.map(x, lambda v: np.sort(v)).glom()
-  with pytest.raises(CodegenError):
-    expr.map(x, lambda v: v if v > 0 else -v).glom()
+  with warnings.catch_warnings():
+    warnings.simplefilter('ignore', RuntimeWarning)
+    np.testing.assert_array_equal(expr.map(x, lambda v: np.sort(v)).glom(), np.ones(4))
+    with pytest.raises(ValueError):
+      expr.map(x, lambda v: v if v > 0 else -v).glom()
 
 
 def test_dot_paths(host_ctx):
@@ -285,7 +289,10 @@ def test_plan_cache_replays_structures(host_ctx):
   plan_cache.clear()
   h0 = plan_cache.STATS['hits']
   w_cached = workloads.sgd_train(X, Y, w0, 1e-3, 6)
-  assert plan_cache.STATS['hits'] - h0 >= 5
+  # iteration 1 misses; iteration 2 misses too, because iteration 1's
+  # AutomaticTiling pinned a tiling on the X / Y nodes (part of the key, as a
+  # fresh optimisation would read it); iterations 3-6 replay
+  assert plan_cache.STATS['hits'] - h0 >= 4
   FLAGS.opt_plan_cache = False
   try:
     w_plain = workloads.sgd_train(X, Y, w0, 1e-3, 6)
@@ -336,3 +343,75 @@ def test_plan_cache_keeps_shared_node_ids(host_ctx):
     be.kmeans_assign = orig
   assert plan_cache.STATS['hits'] > h0
   assert calls == [np.float32] * 4
+
+
+def _host_mapper_cases(expr):
+  """(name, expression, NumPy result) for mappers that cannot be traced into
+  a kernel -- data-dependent control flow, non-ufunc NumPy calls on the tile
+  -- which the reference simply runs per tile (local.py:110-122)."""
+  a = np.arange(60.0).reshape(6, 10)[:, ::-1] % 7.0
+  x = expr.from_numpy(a)
+
+  def branchy(t):
+    if t.sum() > 100:       # a Python branch on the tile's data
+      return t * 2.0
+    return t - 1.0
+
+  def want_branchy(strips):
+    return np.concatenate([branchy(s) for s in strips])
+
+  return a, x, branchy, want_branchy
+
+
+@pytest.mark.parametrize('W', [1, 3])
+def test_untraceable_mapper_runs_on_host(host_ctx, W):
+  host_ctx(W)
+  from spartan_amd import expr
+  from spartan_amd.expr import engine
+  from spartan_amd.array import distarray
+  a, x, branchy, _ = _host_mapper_cases(expr)
+  n0 = engine.HOST_MAPPER_CALLS[0]
+  with pytest.warns(RuntimeWarning, match='host'):
+    got = expr.map(x, lambda t: np.sort(t, axis=1)).glom()
+  np.testing.assert_array_equal(got, np.sort(a, axis=1))
+  assert engine.HOST_MAPPER_CALLS[0] - n0 == len(distarray.from_numpy(a).tiles)
+  # a branch on the tile's values: per tile, as the reference evaluates it
+  strips = [a[ex.ul[0]:ex.lr[0]] for ex in sorted(distarray.from_numpy(a).tiles, key=lambda e: e.ul)]
+  got = expr.map(x, branchy).glom()
+  np.testing.assert_array_equal(got, np.concatenate([branchy(s) for s in strips]))
+  # the same mapper inside a reduction: host map, device reduction
+  np.testing.assert_array_equal(expr.sum(expr.map(x, branchy), axis=0).optimized().glom(),
+                                np.concatenate([branchy(s) for s in strips]).sum(0))
+  # ufunc trees never take the host path
+  n1 = engine.HOST_MAPPER_CALLS[0]
+  np.testing.assert_array_equal((x * 2.0 + 1.0).glom(), a * 2.0 + 1.0)
+  np.testing.assert_array_equal(expr.map(x, lambda t: t * t).glom(), a * a)
+  assert engine.HOST_MAPPER_CALLS[0] == n1
+  # the reference's shape assertion (map.py:80-82)
+  with pytest.raises(AssertionError):
+    expr.map(x, lambda t: np.sort(t, axis=None)[:3]).glom()
+
+
+def test_replayed_plans_keep_the_sign_of_zero(host_ctx):
+  """A 0-d host scalar is a plan-cache slot; the lowering memo of a replayed
+  tree must not hand -0.0 the lowering made for +0.0 (the sign survives a
+  division: +inf / -inf)."""
+  host_ctx(1)
+  from spartan_amd import expr
+  X = expr.lazify(expr.from_numpy(np.ones((4, 3))).force())
+  for _ in range(2):
+    for s, inf in ((np.array(0.0), np.inf), (np.array(-0.0), -np.inf)):
+      with np.errstate(divide='ignore'):
+        got = (1.0 / (X * s)).optimized().glom()
+      np.testing.assert_array_equal(got, np.full((4, 3), inf))
+
+
+def test_tiny_uploads_of_other_dtypes(host_ctx):
+  """Small host arrays of dtypes outside the backend's five (float16,
+  int8, big-endian) take the plain upload path instead of failing."""
+  host_ctx(1)
+  import torch
+  from spartan_amd.array import transfer
+  for a in (np.arange(6, dtype=np.float16), np.arange(6, dtype=np.int8), np.arange(6, dtype='>f8')):
+    t = transfer.upload(a, torch.device('cpu'))
+    np.testing.assert_array_equal(t.numpy().astype(np.float64), a.astype(np.float64))

@@ -25,7 +25,7 @@ for name, f, nin in (cases if os.environ.get("SC_REDUCE", "1") == "1" else []):
     for _ in range(10):
       expr.sum(f(), axis=ax).optimized().force()
     torch.cuda.synchronize()
-    t = [s.elapsed_time(e) for n, s, e in be.kernel_events if n == 'spx_reduce']
+    t = [s.elapsed_time(e) for n, s, e in be.kernel_events if n.startswith('spx_reduce')]
     be.kernel_events = None
     ms = float(np.median(t))
     print('%-12s axis %d  %.4f ms  %.1f GB/s' % (name, ax, ms, (nin * 4 * S * S + 4 * S) / ms / 1e6), flush=True)
@@ -40,7 +40,7 @@ for name, f, nin in [('x*y+exp(z)', lambda: X * Y + expr.exp(Z), 3), ('x+1', lam
   for _ in range(10):
     f().optimized().force()
   torch.cuda.synchronize()
-  t = [s.elapsed_time(e) for n, s, e in be.kernel_events if n == 'spx_map']
+  t = [s.elapsed_time(e) for n, s, e in be.kernel_events if n.startswith('spx_map')]
   be.kernel_events = None
   ms = float(np.median(t))
   print('map %-12s %.4f ms  %.1f GB/s (read+write)' % (name, ms, ((nin + 1) * 4 * S * S) / ms / 1e6), flush=True)
