@@ -337,13 +337,11 @@ def check_dot(c, A, B, S, dt, expr):
   return bool(ok)
 
 
-KM_CENTERS = {}
-
-
-def check_kmeans(X, labels, centers, comm, n_check=1 << 20):
+def check_kmeans(X, labels, centers, comm, n_check=1 << 20, dist_dtype=np.float64):
   """The labels of the first n_check local rows against the all-exact
-  assignment kernel (scipy cdist order for every point and centre): bit
-  for bit."""
+  assignment kernel (scipy cdist order for every point and centre; the
+  distances rounded to dist_dtype first, as the reference's outer target
+  does for the drop-in loop): bit for bit."""
   import torch
   from spartan_amd import backend, runtime
   be = backend.get()
@@ -354,7 +352,7 @@ def check_kmeans(X, labels, centers, comm, n_check=1 << 20):
     n = min(n_check, ex.shape[0])
     lab = labels.local[[e for e in labels.local if e.ul[0] == ex.ul[0]][0]].data[:n]
     want = torch.empty((n,), dtype=torch.int64, device=ctx.device)
-    be.kmeans_assign(tile.data[:n], cdev, want, exact_only=True)
+    be.kmeans_assign(tile.data[:n], cdev, want, exact_only=True, dist_dtype=dist_dtype)
     ok &= bool(torch.equal(lab, want))
   return bool(comm.max_over_ranks(0.0 if ok else 1.0) == 0.0)
 
@@ -376,7 +374,6 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
   comm.barrier()
   el = comm.max_over_ranks(time.perf_counter() - t0) / iters
   checked = check_kmeans(X, labels, info['assign_centers'], comm)
-  KM_CENTERS[npts] = c
   n = npts * ctx.world_size
   out = {'ms_per_iter': round(el * 1e3, 3), 'points_per_s': round(n / el, 1),
          'gemm_form_tflops': round(2.0 * n * K * D / el / 1e12, 2),
@@ -410,16 +407,18 @@ def bench_kmeans_api(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
   sync()
   comm.barrier()
   t0 = time.perf_counter()
-  c_api, _ = KMeans(K, iters).fit(X, c0)
+  km = KMeans(K, iters)
+  c_api, labels = km.fit(X, c0)
   sync()
   comm.barrier()
   el = comm.max_over_ranks(time.perf_counter() - t0) / iters
   n = npts * ctx.world_size
-  # the same iterations as the direct leg (same points, same initial centres);
-  # the drop-in rounds the fp64 centre sums to the points' fp32 before the
-  # division, as the reference's map2 target does: 1e-5 relative
-  ref = KM_CENTERS.get(npts)
-  checked = None if ref is None else _rel_ok(c_api, ref, 1e-5, np.abs(ref) + 1e-3)
+  # the last iteration's labels against the all-exact assignment kernel with
+  # the centres that iteration used (a prefix of each local row strip)
+  ac = km.assign_centers_
+  ac = ac.glom() if hasattr(ac, 'glom') else np.asarray(ac)
+  checked = check_kmeans(X, labels.force() if hasattr(labels, 'force') else labels, ac, comm,
+                         dist_dtype=X.dtype)  # kmeans_dist_mapper's target has the points' dtype
   out = {'ms_per_iter': round(el * 1e3, 3), 'points_per_s': round(n / el, 1), 'checked': checked,
          'config': 'cfg3 via examples.kmeans.KMeans(%d, %d).fit(X, first %d points): outer + argmin '
                    '(OuterArgminFusion -> certified assignment), map2 bincount, map2 centre sums' % (K, iters, K)}

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SPX_ABI_VERSION 2  /* 2: spx_kmeans_assign dist_dtype; collectives */
+#define SPX_ABI_VERSION 3  /* 2: spx_kmeans_assign dist_dtype; collectives; 3: spx_kmeans_step */
 
 /* error codes */
 #define SPX_OK 0
@@ -184,6 +184,21 @@ int64_t spx_kmeans_accumulate_workspace(int dtype, int64_t N, int64_t D, int64_t
 int spx_kmeans_accumulate(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
                           const int64_t* labels, double* sums, uint64_t* counts, int zero_first,
                           void* workspace, size_t workspace_bytes, void* stream);
+/* One k-means iteration's device work, fused: spx_kmeans_assign (labels, bit
+ * for bit the same) followed by spx_kmeans_accumulate (counts exact, sums
+ * deterministic) -- the argmin of outer((X, C), kmeans_dist_mapper) plus
+ * kmeans_count_mapper / kmeans_center_mapper of one KMeans.fit iteration
+ * (k_means_.py:126-136).  For fp32 points with K <= 256 and D in {64, 128}
+ * the decided rows are labelled AND accumulated in one pass over the points
+ * (k_kmeans_fscreen); their sums run in fp32 chains of at most 64 rows per
+ * centre, added into fp64 block partials (|error| <= 2^-18 sum |x| per
+ * element, far inside the fp32 rule; the reference sums in fp32).  Other
+ * shapes run the two calls.  workspace_bytes >=
+ * spx_kmeans_step_workspace(dtype, N, D, K). */
+int64_t spx_kmeans_step_workspace(int dtype, int64_t N, int64_t D, int64_t K);
+int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
+                    const double* centers, int64_t* labels, double* sums, uint64_t* counts, int zero_first,
+                    void* workspace, size_t workspace_bytes, int dist_dtype, void* stream);
 
 /* Full distance matrix out[p * ldo + c] = cdist(points, centers)[p, c] in
  * the exact order above, rounded once to out_dtype (F32/F64): the

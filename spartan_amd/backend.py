@@ -94,6 +94,10 @@ _SIGS = {
     'spx_kmeans_accumulate': ([ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                                ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p], ctypes.c_int),
+    'spx_kmeans_step_workspace': ([ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64], ctypes.c_int64),
+    'spx_kmeans_step': ([ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                         ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                         ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
     'spx_cdist': ([ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                    ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p], ctypes.c_int),
     'spx_bincount': ([ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int,
@@ -237,9 +241,8 @@ def compile_code_object(src):
   return img
 
 
-_REPLAY_PLANS = os.environ.get('SPX_REDUCE_PLANS', '1') != '0'  # dev A/B switch
 _NCU = []
-NT_STORE_BYTES = int(os.environ.get('SPX_NT_STORE_BYTES', 64 << 20))  # map outputs at least this large: non-temporal stores
+NT_STORE_BYTES = 64 << 20  # map outputs at least this large: non-temporal stores
 ROWS_GRID_PER_CU = 2  # rows reductions: 1.824 ms vs 1.836 uncapped at cfg2 axis 1 (profiles/r02_cfg2_grid.txt)
 
 
@@ -362,7 +365,7 @@ class HipBackend:
     # one vector per lane and no grid-stride loop: x + 1 / x * y at 2^30 fp32
     # 1.75 / 2.58 ms with a 4096-block grid-stride loop, 1.34 / 2.01 ms with
     # the full grid (6.4 TB/s read+write; profiles/r02_map_grid.txt)
-    grid = max(1, min(-(-n // (256 * per)), int(os.environ.get('SPX_MAP_GRID', 0x7fffffff))))  # env: dev knob
+    grid = max(1, -(-n // (256 * per)))
     self.launch(fn, grid, args)
 
   # --------------------------------------------------------------- reduce
@@ -381,7 +384,7 @@ class HipBackend:
                                    inputs[s].data_ptr() % 16) for s in slots),
             tuple(in_shape), axis, tuple(out_shape), np.dtype(out_dtype).str,
             None if idx_geom is None else repr(sorted(idx_geom.items())))
-    plan = self._reduce_plans.get(pkey) if _REPLAY_PLANS else None
+    plan = self._reduce_plans.get(pkey)
     if plan is not None:
       return self._replay_reduce(plan, root, inputs, slots, out_shape, out_dtype)
     ins = [(s, np_dtype(inputs[s].dtype)) for s in slots]
@@ -434,7 +437,7 @@ class HipBackend:
       for d in range(3):
         args.str[s][d] = vstr[k][d]
     args.dim[0], args.dim[1], args.dim[2] = O, R, I
-    target_blocks = int(os.environ.get('SPX_REDUCE_BLOCKS', '2048'))  # env: dev knob (experiments only)
+    target_blocks = 2048
     if I == 1 and R <= 64 * V * 16:
       # short segments: several per wave (LPR lanes each), grid-stride over O
       kind = 'rowsp'
@@ -466,11 +469,8 @@ class HipBackend:
       P = -(-R // chunk)
       nblk = O * P
       # grid-stride kernel: at most ROWS_GRID_PER_CU resident blocks per CU
-      # stream the segments (dev knob SPX_ROWS_GRID: blocks per CU, 0 = one
-      # block per segment)
-      gpc = int(os.environ.get('SPX_ROWS_GRID', ROWS_GRID_PER_CU))
-      if gpc > 0:
-        nblk = min(nblk, gpc * _num_cus())
+      # stream the segments
+      nblk = min(nblk, ROWS_GRID_PER_CU * _num_cus())
       args.aux[0], args.aux[1] = P, chunk
     else:
       kind = 'cols'
@@ -493,7 +493,7 @@ class HipBackend:
       # 1024 1.87, 2048 1.87, 4096 1.90); one narrow column tile (cfg5's 64
       # columns) with eight (2048: 4.06 ms per lreg iteration, 512: 4.15)
       # -- tools/cfg2_knobs.py, profiles/r02_cfg2_grid.txt
-      tb = int(os.environ.get('SPX_REDUCE_BLOCKS', 0)) or (2 if CT > 1 else 8) * _num_cus()
+      tb = (2 if CT > 1 else 8) * _num_cus()
       if base < tb:
         P = max(1, min(-(-tb // base), -(-R // (rows_per_step * 4))))
       chunk = -(-R // P)
@@ -712,6 +712,24 @@ class HipBackend:
                                           ctypes.c_void_p(counts.data_ptr()), 1 if zero_first else 0,
                                           ctypes.c_void_p(ws.data_ptr()), ws.numel(), self.stream()),
            'spx_kmeans_accumulate')
+
+  def kmeans_step(self, points, centers, labels, sums, counts, zero_first=True, dist_dtype=np.float64):
+    """kmeans_assign + kmeans_accumulate in one call (spx_kmeans_step): the
+    certified screen labels and accumulates the decided rows in one pass."""
+    N, D = points.shape
+    K = centers.shape[0]
+    assert centers.dtype == self._f64() and tuple(centers.shape) == (K, D) and labels.shape[0] == N
+    assert tuple(sums.shape) == (K, D) and counts.shape[0] == K and sums.is_contiguous() and counts.is_contiguous()
+    dt = spx_dtype(np_dtype(points.dtype))
+    need = self.lib.spx_kmeans_step_workspace(dt, N, D, K)
+    if need < 0:
+      raise RuntimeError('spx_kmeans_step_workspace: bad arguments')
+    ws = self._workspace(max(int(need), 8), points.device)
+    _check(self.lib.spx_kmeans_step(dt, N, D, K, ctypes.c_void_p(points.data_ptr()), points.stride(0),
+                                    ctypes.c_void_p(centers.data_ptr()), ctypes.c_void_p(labels.data_ptr()),
+                                    ctypes.c_void_p(sums.data_ptr()), ctypes.c_void_p(counts.data_ptr()),
+                                    1 if zero_first else 0, ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                                    spx_dtype(dist_dtype), self.stream()), 'spx_kmeans_step')
 
   def cdist(self, points, centers, out):
     """out (N, K) = exact-order cdist(points, centers), rounded to out's dtype."""

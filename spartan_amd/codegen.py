@@ -25,7 +25,6 @@ code object cached on disk by source hash) and launched through the C ABI
 (spx_launch).  Nothing here executes on the CPU.
 """
 import ctypes
-import os
 
 import numpy as np
 
@@ -33,7 +32,7 @@ MAX_IN = 16
 MAX_DIM = 8
 # streamed contiguous vector loads carry the non-temporal hint (global_load
 # ... nt): the inputs of a fused map / reduce are read exactly once
-NT_LOADS = os.environ.get('SPX_NT_LOADS', '1') != '0'
+NT_LOADS = True
 
 
 def _vstore(vtype, ptr_expr, val, nt):
@@ -453,8 +452,6 @@ def _suffix_names(line, sfx):
 def rows_unroll(inputs, classes):
   """Unrolled steps of the row-reduce loop: 4 for one streamed input, 2 for
   two, 1 from three on (cfg2's x*y+exp(z) already streams 3 KiB per wave)."""
-  if os.environ.get('SPX_ROWS_UNROLL'):  # dev knob (tools/, experiments only)
-    return int(os.environ['SPX_ROWS_UNROLL'])
   streamed = sum(1 for c in classes if c != 'b')
   return 4 if streamed <= 1 else 2 if streamed == 2 else 1
 
@@ -466,8 +463,6 @@ def cols_unroll(inputs, classes, vec, row_strides=None):
   columns ('b') or along the reduced rows (row stride 0, e.g. the (1, K) row
   vector of a fused row dot) cost no HBM stream; one row of 3 contiguous
   fp32x4 inputs is 3 KiB per wave."""
-  if os.environ.get('SPX_COLS_UNROLL'):  # dev knob (tools/, experiments only)
-    return int(os.environ['SPX_COLS_UNROLL'])
   streamed = 0
   for k, ((s, dt), cls) in enumerate(zip(inputs, classes)):
     if cls != 'b' and not (row_strides is not None and row_strides[k] == 0):

@@ -81,7 +81,14 @@ __device__ __forceinline__ void tile_of(int bid, int ntiles, int tiles_n, int GM
   }
 }
 
-template <typename T, int BM, int BN, int BK, int WM, int WN, int GM, bool ALIGNED>
+// SEG > 0: two-level accumulation -- the MFMA accumulators restart from zero
+// every SEG K-tiles and are added into running sums, so an fp32 element is a
+// chain of SEG * BK / 2 MFMA steps plus K / (SEG * BK) additions instead of
+// one chain of K / 2 steps (K = 32768: 128 + 128 roundings instead of 16384;
+// the relative error's spread drops from ~4e-6 to ~6e-7, well inside the fp32
+// tolerance of 1e-5 at every element, where one long chain exceeded it in a
+// few elements per row).
+template <typename T, int BM, int BN, int BK, int WM, int WN, int GM, bool ALIGNED, int SEG = 0>
 __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T* __restrict__ A, i64 lda,
                                                      const T* __restrict__ B, i64 ldb, T* __restrict__ C,
                                                      i64 ldc, T alpha, T beta, int tiles_n, int ntiles) {
@@ -110,11 +117,17 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
   const i64 row0 = (i64)tm * BM, col0 = (i64)tn * BN;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = w / WN, wn = w % WN;
-  typename F::acc_t acc[TM][TN];
+  typename F::acc_t acc[TM][TN], run[SEG > 0 ? TM : 1][SEG > 0 ? TN : 1];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = F::zero();
+  if constexpr (SEG > 0) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) run[i][j] = F::zero();
+  }
   V ra[LA], rb[LB];
   auto load = [&](i64 k0) {
 #pragma unroll
@@ -207,8 +220,25 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
           for (int j = 0; j < TN; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
       }
     }
+    if constexpr (SEG > 0) {
+      if ((kt + 1) % SEG == 0) {  // block-uniform
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            run[i][j] += acc[i][j];
+            acc[i][j] = F::zero();
+          }
+      }
+    }
     if (kt + 1 < nk) store(cur ^ 1);
     __syncthreads();
+  }
+  if constexpr (SEG > 0) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] += run[i][j];
   }
   const bool use_beta = beta != (T)0;
 #pragma unroll
@@ -227,7 +257,7 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
       }
 }
 
-template <typename T, int BM, int BN, int BK, int WM, int WN, int GM>
+template <typename T, int BM, int BN, int BK, int WM, int WN, int GM, int SEG = 0>
 struct Config {
   static constexpr int bm = BM, bn = BN, bk = BK, threads = 64 * WM * WN;
   static hipError_t launch(i64 M, i64 N, i64 K, const T* A, i64 lda, const T* B, i64 ldb, T* C, i64 ldc,
@@ -235,10 +265,10 @@ struct Config {
     i64 tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
     int nt = (int)(tm * tn);
     if (aligned)
-      gemm<T, BM, BN, BK, WM, WN, GM, true><<<nt, threads, 0, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta,
+      gemm<T, BM, BN, BK, WM, WN, GM, true, SEG><<<nt, threads, 0, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta,
                                                                    (int)tn, nt);
     else
-      gemm<T, BM, BN, BK, WM, WN, GM, false><<<nt, threads, 0, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha,
+      gemm<T, BM, BN, BK, WM, WN, GM, false, SEG><<<nt, threads, 0, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha,
                                                                     beta, (int)tn, nt);
     return hipGetLastError();
   }

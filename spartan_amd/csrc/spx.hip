@@ -120,15 +120,10 @@ static int grid_for(i64 n, int per_thread = 1) {
 }
 
 // Streamed once-read loads carry the non-temporal hint (global_load ... nt;
-// measured +5-9 % on the generated streaming kernels).  SPX_NO_NT builds a
-// variant without it for A/B timing (tools/km_split.py).
+// measured +5-9 % on the generated streaming kernels).
 template <typename T>
 __device__ __forceinline__ T ld_stream(const T* p) {
-#ifdef SPX_NO_NT
-  return *p;
-#else
   return __builtin_nontemporal_load(p);
-#endif
 }
 
 // =================================================================== fills
@@ -621,8 +616,8 @@ extern "C" int spx_argreduce_combine(int op, int dtype, const void* vals, const 
 // fp32: 256x128x16, 8 waves (with the k-contiguous A staging: 141.4 TF = 89.9 %
 // of 157.3 at 32768^3 against 135.6 TF for the 256x256x16 16-wave tile,
 // profiles/r02_gemm_tune_ak.txt)
-typedef spx_mfma::Config<float, 256, 128, 16, 4, 2, 8> GemmF32Big;
-typedef spx_mfma::Config<float, 128, 128, 16, 2, 2, 8> GemmF32Small;
+typedef spx_mfma::Config<float, 256, 128, 16, 4, 2, 8, 16> GemmF32Big;
+typedef spx_mfma::Config<float, 128, 128, 16, 2, 2, 8, 16> GemmF32Small;
 typedef spx_mfma::Config<double, 128, 128, 16, 4, 4, 0> GemmF64;
 
 // integer GEMM (exact, wrap-around like NumPy's int matmul): 16x16 output
@@ -1784,19 +1779,11 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
     i64 row = tl * 32 + r;
     row = row < nlim ? row : nlim - 1;
     if (rows_in) row = rows_in[row];
-#ifdef KS_DEV_NOGLOBAL  // timing split only (tools/km_modes.py dev builds); never set in the product build
-    row = r;
-#endif
     const float* p = P + row * ldp + 4 * h;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-#ifdef KS_NT  // dev A/B: non-temporal A loads
-      ra[ks][0] = __builtin_nontemporal_load((const kb_f4*)(p + ks * 16));
-      ra[ks][1] = __builtin_nontemporal_load((const kb_f4*)(p + ks * 16 + 8));
-#else
       ra[ks][0] = *(const kb_f4*)(p + ks * 16);      // dims 4h..4h+3 of the k-step
       ra[ks][1] = *(const kb_f4*)(p + ks * 16 + 8);  // dims 8+4h..8+4h+3
-#endif
     }
   };
   constexpr bool PF = MODE == 1 ? KS_PREFETCH1 : KS_PREFETCH;
@@ -1880,22 +1867,11 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
       const unsigned char* rp = rowp + ct * 32 * RB;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) kstep(ks, rp, c0);
-#ifndef KS_DEV_CCVALU
       c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, *(const kb_bf8*)(rp + CCOFF), c0, 0, 0, 0);
-#endif
     };
     // fold tile ct's acc, tagged with ct, into the running top-2 (3 VALU per
     // value: the a' = cc - 2S fma of the earlier form is the MFMA step above)
     auto fold1 = [&](int q, int ct, float acc) {
-#ifdef KS_DEV_CCVALU  // dev A/B only: -cc/2 added on the VALU instead of the MFMA step
-      acc = acc + -0.5f * cnf[ct * 32 + r];
-#endif
-#ifdef KS_DEV_NOFOLD  // timing split only (wrong labels); never set in the product build
-      if (MODE == 1) {
-        lo[q] = ks_max(lo[q], acc);
-        return;
-      }
-#endif
       const float v = ks_tag(acc, (unsigned int)ct);
       sec[q] = ks_med3(v, lo[q], sec[q]);
       lo[q] = ks_max(lo[q], v);
@@ -1919,9 +1895,7 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
 #pragma unroll
         for (int qq = 0; qq < 16 / KS; ++qq) fold1(ks * (16 / KS) + qq, pct, p0[ks * (16 / KS) + qq]);
       }
-#ifndef KS_DEV_CCVALU
       c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, *(const kb_bf8*)(rp + CCOFF), c0, 0, 0, 0);
-#endif
     };
     // pairwise fold (KS_PAIRF1, screen only): two tiles' values a, b of one
     // row fold as sec = max(sec, med3(lo, a, b)), lo = max3(lo, a, b) -- the
@@ -2022,9 +1996,6 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
       asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(r1), "n"(32 + 2 * q));
       rmin = v;
     };
-#ifdef KS_DEV_NODEC  // timing split only (wrong labels); never set in the product build
-    if (MODE == 0)
-#endif
     ks_unroll(rmin_q, std::make_integer_sequence<int, 16>{});
     p2 += __shfl_xor(p2, 32, 64);  // row r's |p|^2 in lanes r and r + 32
     // one decision per row, by the even lane of its pair (as in k_kmeans_filter_b3)
@@ -2057,262 +2028,6 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
   }
 }
 
-// ---------------------------------------------------------------------------
-// The fp16 screen on the 16x16x32 MFMA shape (KS_S16): the same certified
-// a'' = |c'|^2 - 2 x'.c' ranking and bound as k_kmeans_filter_as<.., 1>, with
-// v_mfma_f32_16x16x32_f16 (MI355X_MICROARCH.md: the chip holds a higher clock
-// on this shape, and the screen is clock bound).  A wave's 32-point tile is
-// two 16-row blocks; each B fragment (16 centres x 32 dims, ds_read_b128) feeds
-// both.  Lane (c, g) = (l & 15, l >> 4) holds, per k-step ks, dims
-// 32 ks + 4 g + {0..3} and 32 ks + 16 + 4 g + {0..3} of rows 16 b + c (64-byte
-// row pieces per load instruction); the centre rows are stored with the same
-// permutation.  Output: lane (c, g) holds rows 16 b + 4 g + j of centre c, so a
-// row's top two are reduced over the 16 lanes of one DPP row (no ds_swizzle),
-// 8 (lo, sec) registers per lane; tiles are tagged in 4 low mantissa bits
-// (16 centre tiles: 15 ulp, priced below).
-constexpr int S16_RB = 288;  // row stride: 18 quads = 2 (mod 16) -> a ds_read_b128 lane group hits 16 distinct bank quads
-constexpr int S16_CC = 256;  // byte offset of the -cc/2 pieces in a row (D <= 128)
-static size_t s16_lds_bytes(i64 D, int nct16) { return (size_t)16 * nct16 * S16_RB + 16 + 4 * (size_t)D; }
-typedef float s16_acc __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ float ks_tag4(float a, unsigned int ct) {
-  return __builtin_bit_cast(float, (__builtin_bit_cast(unsigned int, a) & ~15u) | (ct & 15u));
-}
-
-template <int NCT, int KS>
-__global__ __launch_bounds__(512) void k_kmeans_screen16(i64 N, const float* __restrict__ P, i64 ldp,
-                                                         const __bf16* __restrict__ CBh,
-                                                         const __bf16* __restrict__ CBl,
-                                                         const float* __restrict__ cnf2, const double* cmax_p,
-                                                         i64* __restrict__ labels,
-                                                         unsigned long long* __restrict__ und_mask,
-                                                         const float* __restrict__ muf) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char kb_lds[];
-  constexpr int NC = 16 * NCT, D = 32 * KS, W = 8;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, c = lane & 15, g = lane >> 4;
-  unsigned char* zq = kb_lds + NC * S16_RB;  // 16 zero bytes (the cc step's B for lane groups 1-3)
-  float* mul = (float*)(zq + 16);
-  {
-    typedef __bf16 kb_b4 __attribute__((ext_vector_type(4)));
-    typedef _Float16 kh_f4 __attribute__((ext_vector_type(4)));
-    constexpr int D4 = D / 4;
-    for (int i = t; i < NC * D4; i += W * 64) {
-      const int cen = i / D4, q = i % D4, ks = q >> 3, qq = q & 7;
-      const int pos = 32 * ks + (qq < 4 ? 8 * qq : 8 * (qq - 4) + 4);  // half index in the permuted row
-      const kb_b4 bh = *(const kb_b4*)&CBh[(i64)cen * D + 4 * q];
-      const kb_b4 bl = *(const kb_b4*)&CBl[(i64)cen * D + 4 * q];
-      kh_f4 v;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = (_Float16)((float)bh[j] + (float)bl[j]);
-      *(kh_f4*)(kb_lds + cen * S16_RB + 2 * pos) = v;
-    }
-    for (int i = t; i < NC; i += W * 64) {
-      const float v = -0.5f * cnf2[i];
-      const __bf16 b1 = (__bf16)v;
-      const float v1 = v - (float)b1;
-      const __bf16 b2 = (__bf16)v1;
-      const __bf16 b3 = (__bf16)(v1 - (float)b2);
-      const __bf16 z = (__bf16)0.f;
-      *(kb_bf8*)(kb_lds + i * S16_RB + S16_CC) = (kb_bf8){b1, b2, b3, z, z, z, z, z};
-    }
-    if (t < 4) ((float*)zq)[t] = 0.f;
-    for (int i = t; i < D; i += W * 64) mul[i] = muf[i];
-  }
-  __syncthreads();
-  const double cmax = cmax_p[0], mcoef = cmax_p[1], mun = cmax_p[2], dcmax = cmax_p[3];
-  const double u32 = 5.9604644775390625e-08, eps = 1.1920928955078125e-07;
-  const double chain = 32.0 * (double)KS;
-  const double eS = (u32 * cmax + 4.8828125e-04 * cmax + 1.001 * dcmax +
-                     2.0 * (chain + 3.0) * u32 * 1.001 * (cmax + dcmax)) * 1.01;
-  const double cm2 = cmax * cmax + 2.0 * mun * cmax;
-  // as the 32x32 screen, plus the 4-bit tag: 15 ulp of |acc| = 30 eps (|x'| cmax + cmax^2 / 2) in a'' units
-  const double xk1 = 64.0 * u32 * cmax + 16.0 * eps * cmax;
-  const double xk0 = 32.0 * u32 * cm2 + 8.0 * eps * cm2 + sqrt((double)D) * 1.1920928955078125e-07 * (cmax + dcmax) +
-                     (double)D * 3.552713678800501e-15;
-  float kq[3];
-  kc_coef(eS, cmax, mun, mcoef, D, kq, xk1, xk0);
-  const bool cok = cmax * cmax < 1e36 && mun * cmax < 1e36 && cmax < 3.0e4 && dcmax == dcmax;
-  const float pn_lim = (float)(cmax > 0.0 ? 1e36 / cmax : 1e36);
-  const i64 ntiles = (N + 31) / 32;
-  const i64 stride = (i64)gridDim.x * W;
-  const __bf16 one = (__bf16)1.f;
-  const kb_bf8 a_one = (kb_bf8){one, one, one, one, one, one, one, one};
-  for (i64 tile = (i64)blockIdx.x * W + w; tile < ntiles; tile += stride) {
-    kb_f4 ra[2][KS][2];
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      i64 row = tile * 32 + 16 * b + c;
-      row = row < N ? row : N - 1;
-      const float* p = P + row * ldp + 4 * g;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        ra[b][ks][0] = *(const kb_f4*)(p + 32 * ks);
-        ra[b][ks][1] = *(const kb_f4*)(p + 32 * ks + 16);
-      }
-    }
-    kh_f8 ah[2][KS];
-    float p2b[2] = {0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const kb_f4 m0 = *(const kb_f4*)(mul + 32 * ks + 4 * g);
-      const kb_f4 m1 = *(const kb_f4*)(mul + 32 * ks + 16 + 4 * g);
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const kb_f4 x0 = ra[b][ks][0] - m0, x1 = ra[b][ks][1] - m1;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          p2b[b] = __builtin_fmaf(x0[e], x0[e], p2b[b]);
-          p2b[b] = __builtin_fmaf(x1[e], x1[e], p2b[b]);
-          ah[b][ks][e] = (_Float16)x0[e];
-          ah[b][ks][4 + e] = (_Float16)x1[e];
-        }
-      }
-    }
-    float lo[8], sec[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      lo[k] = -INFINITY;
-      sec[k] = -INFINITY;
-    }
-    // tiles ct, ct + 1 -> acc[tile-in-pair][block]
-    auto chain2 = [&](int ct, s16_acc (&acc)[2][2]) {
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
-        const unsigned char* rp = kb_lds + ((ct + h2) * 16 + c) * S16_RB + 16 * g;
-        acc[h2][0] = (s16_acc){};
-        acc[h2][1] = (s16_acc){};
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          const kh_f8 bh = *(const kh_f8*)(rp + 64 * ks);
-          acc[h2][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[0][ks], bh, acc[h2][0], 0, 0, 0);
-          acc[h2][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[1][ks], bh, acc[h2][1], 0, 0, 0);
-        }
-        const kb_bf8 bcc = *(const kb_bf8*)(g == 0 ? kb_lds + ((ct + h2) * 16 + c) * S16_RB + S16_CC : zq);
-        acc[h2][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_one, bcc, acc[h2][0], 0, 0, 0);
-        acc[h2][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_one, bcc, acc[h2][1], 0, 0, 0);
-      }
-    };
-    auto fold2 = [&](int ct, const s16_acc (&acc)[2][2]) {
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int k = 4 * b + j;
-          const float ta = ks_tag4(acc[0][b][j], (unsigned int)ct), tb = ks_tag4(acc[1][b][j], (unsigned int)(ct + 1));
-          sec[k] = ks_max(sec[k], ks_med3(lo[k], ta, tb));
-          lo[k] = ks_max3(lo[k], ta, tb);
-        }
-    };
-    {
-      s16_acc A[2][2], B[2][2];
-      chain2(0, A);
-#pragma unroll 1
-      for (int cp = 2; cp < NCT; cp += 4) {
-        chain2(cp, B);
-        fold2(cp - 2, A);
-        __builtin_amdgcn_sched_barrier(0);
-        if (cp + 2 < NCT) {
-          chain2(cp + 2, A);
-          fold2(cp, B);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      if constexpr (((NCT - 2) / 2) & 1) fold2(NCT - 2, B);
-      else fold2(NCT - 2, A);
-    }
-    float lo0[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) lo0[k] = lo[k];
-    // top two per row over the 16 lanes of the row's DPP row (register halving
-    // on lane bits 3, 2, 1, then bit 0): lane c keeps register (c >> 1) & 7
-    {
-      auto comb = [](float a, float as, float b, float bs, float& l, float& s2) {
-        s2 = ks_med3(a, b, ks_max(as, bs));
-        l = ks_max(a, b);
-      };
-      auto dpp_step = [&](auto ctrl, int n, int o) {
-        constexpr int C = decltype(ctrl)::value;
-        const bool up = (lane & o) != 0;
-#pragma unroll
-        for (int k = 0; k < n; ++k) {
-          const float kl = up ? lo[k + n] : lo[k], ks2 = up ? sec[k + n] : sec[k];
-          const float sl = up ? lo[k] : lo[k + n], ss = up ? sec[k] : sec[k + n];
-          const float ol = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sl), C, 0xF, 0xF, false));
-          const float os = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, ss), C, 0xF, 0xF, false));
-          comb(kl, ks2, ol, os, lo[k], sec[k]);
-        }
-      };
-      dpp_step(std::integral_constant<int, 0x140>{}, 4, 8);  // row_mirror: lane ^ 15
-      dpp_step(std::integral_constant<int, 0x141>{}, 2, 4);  // row_half_mirror: lane ^ 7
-      dpp_step(std::integral_constant<int, 0x4E>{}, 1, 2);   // quad_perm [2,3,0,1]: lane ^ 2
-      const float ol = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, lo[0]), 0xB1, 0xF, 0xF, false));
-      const float os = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sec[0]), 0xB1, 0xF, 0xF, false));
-      comb(lo[0], sec[0], ol, os, lo[0], sec[0]);
-    }
-    // the centre of each row's best: the lowest lane c of the group whose own
-    // best for that row equals it (equal tagged values share the tile)
-    const int kme = (c >> 1) & 7;
-    int rmin = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float bk = __shfl(lo[0], (lane & 48) | (2 * k), 64);
-      const unsigned long long m = __ballot(lo0[k] == bk);
-      const unsigned int mg = (unsigned int)(m >> (16 * g)) & 0xFFFFu;
-      const int ck = __builtin_ctz(mg | 0x10000u);
-      rmin = kme == k ? ck : rmin;
-    }
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      p2b[b] += __shfl_xor(p2b[b], 16, 64);
-      p2b[b] += __shfl_xor(p2b[b], 32, 64);
-    }
-    const int bme = (c >> 3) & 1, jme = (c >> 1) & 3;
-    const int src = 4 * g + jme;  // a lane holding |x'|^2 of row 16 bme + 4 g + jme
-    const float s0 = __shfl(p2b[0], src, 64), s1 = __shfl(p2b[1], src, 64);
-    const float p2f = bme ? s1 : s0;
-    const i64 grow = tile * 32 + 16 * bme + 4 * g + jme;
-    const float b1 = lo[0], b2 = sec[0];
-    const int i1 = 16 * (int)(__builtin_bit_cast(unsigned int, b1) & 15u) + rmin;
-    const float pn = __builtin_amdgcn_sqrtf(__builtin_fmaf(p2f, 1.001f, 1e-37f)) * 1.0001f;
-    const float e = __builtin_fmaf(__builtin_fmaf(kq[2], pn, kq[1]), pn, kq[0]) * 1.0001f;
-    const bool live = grow < N && (c & 1) == 0;
-    const bool fin = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim && isfinite(b1) && isfinite(b2);
-    const bool dec = fin && b1 - b2 > 1.0001f * e;
-    if (live && dec) labels[grow] = i1;
-    const unsigned long long und = __ballot(live && !dec);
-    if (lane == 0) und_mask[tile] = und;
-  }
-}
-
-template <int NCT, int KS>
-static void s16_launch(hipStream_t s, i64 N, const float* P, i64 ldp, const __bf16* CBh, const __bf16* CBl,
-                       const float* cnf2, const double* cmax, i64* labels, unsigned long long* und_mask,
-                       const float* muf, int grid) {
-  const size_t lds = s16_lds_bytes(32 * KS, NCT);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_kmeans_screen16<NCT, KS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)s16_lds_bytes(KB_DMAX, 16));
-    attr = true;
-  }
-  k_kmeans_screen16<NCT, KS><<<grid, 512, lds, s>>>(N, P, ldp, CBh, CBl, cnf2, cmax, labels, und_mask, muf);
-}
-
-static void s16_launch_n(int nct32, hipStream_t s, i64 N, i64 D, const float* P, i64 ldp, const __bf16* CBh,
-                         const __bf16* CBl, const float* cnf2, const double* cmax, i64* labels,
-                         unsigned long long* und_mask, const float* muf, int grid) {
-#define S16_CASE(NC)                                                                                        \
-  if (D == 64) s16_launch<NC, 2>(s, N, P, ldp, CBh, CBl, cnf2, cmax, labels, und_mask, muf, grid);       \
-  else s16_launch<NC, 4>(s, N, P, ldp, CBh, CBl, cnf2, cmax, labels, und_mask, muf, grid);
-  switch (nct32) {
-    case 1: S16_CASE(2) break;
-    case 2: S16_CASE(4) break;
-    case 4: S16_CASE(8) break;
-    default: S16_CASE(16) break;
-  }
-#undef S16_CASE
-}
-
 // Row list of the undecided rows from the per-tile lane masks of
 // k_kmeans_filter_as (bit l: lane (h, r) = (l >> 5, l & 31) decided row rt(r >> 1, h)
 // of the tile); rows_in: the tile slots stand for rows_in[slot].  A block
@@ -2323,11 +2038,15 @@ static void s16_launch_n(int nct32, hipStream_t s, i64 N, i64 D, const float* P,
 // KC_TPT tiles per thread: 16 for the sparse full-row pass (~5 % of rows at
 // cfg3), 1 for the dense list pass (~20 % of its slots): a thread's rows are
 // written one after another, so a dense mask wants few tiles per thread.
+// LAYOUT 2 (k_kmeans_fscreen): bit l < 32 <-> row 32 tile + l.  base_in (the
+// deterministic form, k_ks_count + k_exscan_u32): the block's first list slot
+// instead of an atomic on cnt -- the list is then in row order.
 template <int KC_TPT, int LAYOUT = 0>
 __global__ __launch_bounds__(256) void k_ks_compact(i64 N, const unsigned long long* __restrict__ mask,
                                                     const i64* __restrict__ rows_in,
                                                     const unsigned int* __restrict__ nrows_in, i64* __restrict__ out,
-                                                    unsigned int* __restrict__ cnt) {
+                                                    unsigned int* __restrict__ cnt,
+                                                    const unsigned int* __restrict__ base_in = nullptr) {
   __shared__ unsigned int wsum[4];
   __shared__ unsigned int base;
   const i64 nlim = rows_in ? (i64)*nrows_in : N;
@@ -2351,7 +2070,7 @@ __global__ __launch_bounds__(256) void k_ks_compact(i64 N, const unsigned long l
   }
   if (lane == 63) wsum[w] = inc;
   __syncthreads();
-  if (threadIdx.x == 0) base = atomicAdd(cnt, wsum[0] + wsum[1] + wsum[2] + wsum[3]);
+  if (threadIdx.x == 0) base = base_in ? base_in[blockIdx.x] : atomicAdd(cnt, wsum[0] + wsum[1] + wsum[2] + wsum[3]);
   __syncthreads();
   unsigned int pos = base + inc - n;
   for (int k = 0; k < w; ++k) pos += wsum[k];
@@ -2366,9 +2085,8 @@ __global__ __launch_bounds__(256) void k_ks_compact(i64 N, const unsigned long l
       if (LAYOUT == 0) {  // 32x32 output layout (k_kmeans_filter_as)
         const int q = (l & 31) >> 1, h = l >> 5;
         slot = tl * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-      } else {  // 16x16 output layout (k_kmeans_screen16): lane (c, g) decided row 16 (c >> 3 & 1) + 4 g + (c >> 1 & 3)
-        const int c = l & 15, g = l >> 4;
-        slot = tl * 32 + 16 * ((c >> 3) & 1) + 4 * g + ((c >> 1) & 3);
+      } else {  // point order (k_kmeans_fscreen)
+        slot = tl * 32 + l;
       }
       out[pos++] = rows_in ? rows_in[slot] : slot;
     }
@@ -2414,6 +2132,432 @@ static void ks_launch_n(int nct, hipStream_t s, i64 N, i64 D, const float* P, i6
     case 2: ks_launch_d<2, MODE>(s, N, D, P, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_mask, rows_in, nrows_in, muf, grid); break;
     case 4: ks_launch_d<4, MODE>(s, N, D, P, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_mask, rows_in, nrows_in, muf, grid); break;
     default: ks_launch_d<8, MODE>(s, N, D, P, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_mask, rows_in, nrows_in, muf, grid); break;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused k-means step: the fp16 screen AND the centroid accumulation in ONE
+// pass over the points (spx_kmeans_step; kmeans_dist_mapper + argmin +
+// kmeans_count_mapper + kmeans_center_mapper, k_means_.py:52-89, 126-136).
+//
+// The A-stationary screen above holds a wave's 32-point tile in registers
+// and sweeps all 256 centres through it; its registers are full, so the
+// per-centre sums cannot live next to it and the accumulation had to read
+// the points a second time (51 GB at cfg3).  Here the roles are swapped
+// (B-stationary): wave w < NCT keeps ITS 32 centres in registers -- the MFMA A
+// operand, fp16(c') exactly as the screen stages them, plus the -cc/2 pieces
+// -- and every point tile passes through all of the block's waves from LDS.
+// Per 32-point tile:
+//   stage     512 threads convert the tile (16 KiB fp32, register prefetch
+//             ring KFS_R tiles deep) to x' = fl(x - mu) and fp16(x') in LDS,
+//             |x'|^2 per row, and keep the raw fp32 rows in LDS;
+//   screen    wave w: 8 fp16 MFMAs + 1 bf16 MFMA (-cc/2) give the 32 x 32
+//             block S - cc/2 = -a''/2 (rows = its centres, columns = the
+//             points), a per-lane top-2 over the lane's 16 centres, one
+//             half-swap, and (b1, b2, index) per point into LDS;
+//   decide    every wave reads the NCT candidates per point: the certified
+//             rule of the screen (b1 - b2 > e(|x'|), the same bound kq and
+//             the same finiteness checks as k_kmeans_filter_as MODE 1, whose
+//             arithmetic this is with A and B exchanged);
+//   accumulate wave w adds the decided rows whose centre it owns from the
+//             fp32 rows in LDS into fp32 register sums (32 centres x D / 64
+//             dims per lane) in point order.
+// Every KFS_FW tiles (a window) the labels / undecided bits buffered in LDS go
+// to global memory and every fp32 chain is added to the block's private fp64
+// partial (no-return fp64 atomics, one writer per address, so program order
+// fixes the result: deterministic); a chain therefore spans at most the rows
+// one block sees of one centre in one window (~32 at cfg3).  Keeping every
+// global store out of the tile loop lets the prefetch ring stay in flight
+// across the barriers (a pending store would make the compiler wait
+// vmcnt(0) at each staging).
+// One barrier per tile: tile t's decision / accumulation, tile t+1's screen
+// and tile t+2's staging share an iteration (fp32 rows triple-buffered, fp16
+// rows and the exchange double-buffered).  Undecided rows (near-ties,
+// non-finite or fp16-overflowing rows) are not added: they go through the
+// list passes of spx_kmeans_assign and a gathered accumulation afterwards.
+typedef _Float16 kfs_h4 __attribute__((ext_vector_type(4)));
+typedef float kfs_f2 __attribute__((ext_vector_type(2)));
+constexpr int KFS_WAVES = 8;
+#ifndef KFS_RING
+#define KFS_RING 6  // prefetch ring depth in tiles (registers, 8 per tile): the loads of tiles it+2 .. it+KFS_R+1 fly during iteration it
+#endif
+constexpr int KFS_R = KFS_RING;
+constexpr int KFS_NB = 3;      // fp32 row buffers in LDS (staged, waiting, being accumulated)
+constexpr int KFS_FW = 252;    // tiles per window (a multiple of KFS_R): labels / bits buffered in LDS, fp32 chains flushed per window
+static_assert(KFS_R % KFS_NB == 0 && KFS_FW % KFS_R == 0, "buffer / drain indices must be compile-time in the unrolled ring");
+__host__ __device__ constexpr int kfs_rs(int D) { return 2 * D + 16; }  // fp16 row stride: +16 B keeps ds_read_b128 conflict-free
+static size_t kfs_lds_bytes(int D) {
+  return (size_t)KFS_NB * 32 * D * 4 + (size_t)2 * 32 * kfs_rs(D) + KFS_NB * 32 * 4 + 2 * KFS_WAVES * 32 * 12 +
+         (size_t)D * 4 + 2 * KFS_FW * 4 + 2 * KFS_FW * 32;
+}
+
+template <int KS, int NCT, bool ACC>
+__global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fscreen(
+    i64 N, i64 K, const float* __restrict__ P, i64 ldp, const __bf16* __restrict__ CBh,
+    const __bf16* __restrict__ CBl, const float* __restrict__ cnf2, const double* cmax_p,
+    const float* __restrict__ muf, i64* __restrict__ labels, unsigned long long* __restrict__ und_mask,
+    double* __restrict__ psum, unsigned long long* __restrict__ pcnt) {
+  constexpr int D = 16 * KS, EPT = KS, DPL = D / 64, RS = kfs_rs(D), W = KFS_WAVES;
+  static_assert(EPT % 4 == 0 && (DPL == 1 || DPL == 2), "D = 64 or 128");
+  extern __shared__ __attribute__((aligned(16))) unsigned char kfs_lds[];
+  float* xs = (float*)kfs_lds;                                     // [KFS_NB][32][D] raw fp32 rows
+  unsigned char* xh = kfs_lds + (size_t)KFS_NB * 32 * D * 4;       // [2][32][RS] fp16 x'
+  float* p2s = (float*)(xh + 2 * 32 * RS);                         // [KFS_NB][32] |x'|^2
+  float* exv = p2s + KFS_NB * 32;                                  // [2][W][2][32] (b1, b2)
+  int* exi = (int*)(exv + 2 * W * 2 * 32);                         // [2][W][32] best centre
+  float* mus = (float*)(exi + 2 * W * 32);                         // [D] centre mean
+  unsigned int* und32 = (unsigned int*)(mus + D);                  // [2 KFS_FW] undecided bits per tile
+  unsigned char* lab8 = (unsigned char*)(und32 + 2 * KFS_FW);      // [2 KFS_FW][32] labels (K <= 256)
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, j = lane & 31, h = lane >> 5;
+  for (int i = t; i < D; i += W * 64) mus[i] = muf[i];
+
+  // this wave's centres (A operand): lane (j, h) = centre 32 w + j, dims
+  // 16 ks + 8 h .. + 7 of k-step ks; fp16(hi + lo) as the screen stages them
+  kh_f8 ca[KS];
+  kb_bf8 ccp;
+  {
+    const i64 c = 32 * (i64)(w < NCT ? w : 0) + j;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const i64 d = 16 * ks + 8 * h + e;
+        ca[ks][e] = (_Float16)((float)CBh[c * D + d] + (float)CBl[c * D + d]);
+      }
+    // -cc/2 as three bf16 pieces (8 + 8 + 8 significant bits, exact) in the
+    // h = 0 lanes, zeros in the h = 1 lanes: one bf16 MFMA against ones adds it
+    const float v = -0.5f * cnf2[c];
+    const __bf16 b1 = (__bf16)v;
+    const float v1 = v - (float)b1;
+    const __bf16 b2 = (__bf16)v1;
+    const __bf16 b3 = (__bf16)(v1 - (float)b2);
+    const __bf16 z = (__bf16)0.f;
+    ccp = h == 0 ? (kb_bf8){b1, b2, b3, z, z, z, z, z} : (kb_bf8){z, z, z, z, z, z, z, z};
+  }
+  const __bf16 one = (__bf16)1.f;
+  const kb_bf8 ones = (kb_bf8){one, one, one, one, one, one, one, one};
+
+  // the certified bound of k_kmeans_filter_as MODE 1 (same arithmetic)
+  const double cmax = cmax_p[0], mcoef = cmax_p[1], mun = cmax_p[2], dcmax = cmax_p[3];
+  const double u32 = 5.9604644775390625e-08;
+  const double chain = 16.0 * (double)KS;
+  const double eS = (u32 * cmax + 4.8828125e-04 * cmax + 1.001 * dcmax +
+                     2.0 * (chain + 3.0) * u32 * 1.001 * (cmax + dcmax)) * 1.01;
+  double xk1 = 64.0 * u32 * cmax, xk0 = 32.0 * u32 * (cmax * cmax + 2.0 * mun * cmax);
+  xk0 += sqrt((double)D) * 1.1920928955078125e-07 * (cmax + dcmax) + (double)D * 3.552713678800501e-15;
+  // the 4-bit tag (15 ulp of |S - cc/2| <= |p| cmax + cm2 / 2, i.e. 30 eps (|p|
+  // cmax + cm2 / 2) in a'' units) where kc_coef's 8 eps amax covers 16 eps (..)
+  xk1 += 14.0 * 1.1920928955078125e-07 * cmax;
+  xk0 += 7.0 * 1.1920928955078125e-07 * (cmax * cmax + 2.0 * mun * cmax);
+  float kq[3];
+  kc_coef(eS, cmax, mun, mcoef, D, kq, xk1, xk0);
+  const bool cok = cmax * cmax < 1e36 && mun * cmax < 1e36 && cmax < 3.0e4 && dcmax == dcmax;
+  const float pn_lim = (float)(cmax > 0.0 ? 1e36 / cmax : 1e36);
+
+  const i64 ntiles = (N + 31) / 32, G = gridDim.x, bk = blockIdx.x;
+  const i64 nit = bk < ntiles ? (ntiles - 1 - bk) / G + 1 : 0;
+  // this thread's slice of a tile: row t / 16, EPT columns from (t % 16) EPT
+  const int srow = t >> 4, scol = (t & 15) * EPT;
+  kb_f4 ring[KFS_R][EPT / 4];
+  auto load = [&](kb_f4 (&r)[EPT / 4], i64 it) __attribute__((always_inline)) {  // clamped: always a valid address
+    const i64 tl = bk + (it < nit ? it : nit - 1) * G;
+    i64 row = tl * 32 + srow;
+    row = row < N ? row : N - 1;
+    const float* p = P + row * ldp + scol;
+#pragma unroll
+    for (int q = 0; q < EPT / 4; ++q) r[q] = *(const kb_f4*)(p + 4 * q);
+  };
+  auto stage = [&](const kb_f4 (&r)[EPT / 4], i64 it, int b3) __attribute__((always_inline)) {  // ring slot -> LDS (buffers of iteration it)
+    float* xrow = xs + ((size_t)b3 * 32 + srow) * D + scol;
+    _Float16 hv[EPT];
+    float p2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < EPT / 4; ++q) {
+      *(kb_f4*)(xrow + 4 * q) = r[q];
+      const kb_f4 mu4 = *(const kb_f4*)(mus + scol + 4 * q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x = r[q][e] - mu4[e];  // x' = fl(x - mu), as the screen
+        p2 = __builtin_fmaf(x, x, p2);
+        hv[4 * q + e] = (_Float16)x;
+      }
+    }
+    unsigned char* hrow = xh + ((size_t)(it & 1) * 32 + srow) * RS + 2 * scol;
+    if constexpr (EPT == 8) {
+      *(kh_f8*)hrow = (kh_f8){hv[0], hv[1], hv[2], hv[3], hv[4], hv[5], hv[6], hv[7]};
+    } else {
+      *(kfs_h4*)hrow = (kfs_h4){hv[0], hv[1], hv[2], hv[3]};
+    }
+    // the row's |x'|^2 over its 16 threads (one DPP row): only the bound reads it (1.001 slack)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) p2 += __shfl_xor(p2, o, 64);
+    if ((t & 15) == 0) p2s[b3 * 32 + srow] = p2;
+  };
+
+  // fp32 sums of this wave's 32 centres: lane = DPL dims, register = centre
+  float s0[32], s1[32];
+#pragma unroll
+  for (int c = 0; c < 32; ++c) s0[c] = s1[c] = 0.f;
+  unsigned int cnt = 0u;  // lane c < 32: decided rows of centre 32 w + c in this block
+  double* pbase = psum + ((i64)bk * K + 32 * (i64)w) * D + DPL * lane;
+  auto flush = [&](int cl) __attribute__((always_inline)) {  // centre cl's fp32 chain into the block's fp64 partial
+    if (32 * w + cl < K) {
+      unsafeAtomicAdd(pbase + (i64)cl * D, (double)s0[cl]);
+      if constexpr (DPL == 2) unsafeAtomicAdd(pbase + (i64)cl * D + 1, (double)s1[cl]);
+    }
+    s0[cl] = 0.f;
+    s1[cl] = 0.f;
+  };
+
+  // screen of iteration it's tile (waves < NCT): top-2 + best centre per point into the exchange
+  auto screen = [&](i64 it) __attribute__((always_inline)) {
+    const unsigned char* bp = xh + ((size_t)(it & 1) * 32 + j) * RS + 16 * h;
+    kb_acc acc = (kb_acc){};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const kh_f8 bv = *(const kh_f8*)(bp + 32 * ks);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[ks], bv, acc, 0, 0, 0);
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ccp, ones, acc, 0, 0, 0);
+    // acc[q] = S - cc/2 = -a''/2 of point j and centre i(q) = (q & 3) + 8 (q >> 2) + 4 h,
+    // tagged with q in its 4 low mantissa bits (<= 15 ulp, priced in the
+    // bound: xk0 / xk1 above), so the top-2 fold carries its argument along
+    // (plain C on the fresh accumulators: MFMA -> VALU wait states; asm on the
+    // tagged values: no canonicalisation of bit-built operands)
+    float tv[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      tv[q] = __builtin_bit_cast(float, (__builtin_bit_cast(unsigned int, acc[q]) & ~15u) | (unsigned int)q);
+    float lo = ks_max(tv[0], tv[1]), sec = ks_med3(tv[0], tv[1], -INFINITY);
+#pragma unroll
+    for (int q = 2; q < 16; q += 2) {
+      sec = ks_max(sec, ks_med3(lo, tv[q], tv[q + 1]));
+      lo = ks_max3(lo, tv[q], tv[q + 1]);
+    }
+    const unsigned int qb = __builtin_bit_cast(unsigned int, lo) & 15u;
+    const int il = 32 * w + (int)((qb & 3) + 8 * (qb >> 2)) + 4 * h;
+    const float lo2 = __shfl_xor(lo, 32, 64), sec2 = __shfl_xor(sec, 32, 64);
+    const float b1 = ks_max(lo, lo2);
+    const float b2 = ks_med3(lo, lo2, ks_max(sec, sec2));
+    const int ib = lo >= lo2 ? il : __shfl_xor(il, 32, 64);  // equal tagged values: undecided anyway
+    if (h == 0) {
+      float* ev = exv + ((size_t)(it & 1) * W + w) * 64;
+      ev[j] = b1;
+      ev[32 + j] = b2;
+      exi[((size_t)(it & 1) * W + w) * 32 + j] = ib;
+    }
+  };
+
+  // decision + accumulation of iteration it's tile
+  auto decide = [&](i64 it, int b3) __attribute__((always_inline)) {
+    const i64 tl = bk + it * G;
+    float b1 = -INFINITY, b2 = -INFINITY;
+    int ib = 0;
+#pragma unroll
+    for (int v = 0; v < NCT; ++v) {
+      const float* ev = exv + ((size_t)(it & 1) * W + v) * 64;
+      const float a = ev[j], as = ev[32 + j];
+      const int ai = exi[((size_t)(it & 1) * W + v) * 32 + j];
+      b2 = __builtin_amdgcn_fmed3f(b1, a, fmaxf(b2, as));
+      ib = a > b1 ? ai : ib;  // strict: the lower centre index keeps a tie (undecided anyway)
+      b1 = fmaxf(b1, a);
+    }
+    const float p2f = p2s[b3 * 32 + j];
+    const float pn = __builtin_amdgcn_sqrtf(__builtin_fmaf(p2f, 1.001f, 1e-37f)) * 1.0001f;
+    const float e = __builtin_fmaf(__builtin_fmaf(kq[2], pn, kq[1]), pn, kq[0]) * 1.0001f;
+    const bool fin = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim && isfinite(b1) && isfinite(b2);
+    const i64 row = tl * 32 + j;
+    const bool live = it < nit && h == 0 && row < N;  // it >= nit: a ghost iteration
+    const bool dec = fin && b1 - b2 > 1.0001f * e;
+    // labels and the undecided bits go to the window buffers in LDS; no
+    // global store inside the tile loop (drain writes them)
+    if (w == 0 && it < nit) {
+      const int u = (int)(it % (2 * KFS_FW));
+      if (h == 0) lab8[u * 32 + j] = (unsigned char)ib;
+      const unsigned long long und = __ballot(live && !dec);
+      if (lane == 0) und32[u] = (unsigned int)und;  // bit j <-> row 32 tl + j
+    }
+    if constexpr (ACC) {
+      if (w < NCT) {
+        unsigned long long m = __ballot(live && dec && (ib >> 5) == w);
+        const float* xb = xs + (size_t)b3 * 32 * D + DPL * lane;
+        while (m) {  // wave-uniform, in point order; two rows per step (both reads in flight)
+          const int p = __builtin_ctzll(m);
+          m &= m - 1;
+          const bool two = m != 0;
+          const int p2 = two ? __builtin_ctzll(m) : p;
+          if (two) m &= m - 1;
+          const int cl = __builtin_amdgcn_readlane(ib, p) & 31;
+          const int cl2 = __builtin_amdgcn_readlane(ib, p2) & 31;
+          if constexpr (DPL == 2) {
+            const kfs_f2 x = *(const kfs_f2*)(xb + p * D);
+            const kfs_f2 x2 = *(const kfs_f2*)(xb + p2 * D);
+            s0[cl] += x[0];
+            s1[cl] += x[1];
+            if (two) {
+              s0[cl2] += x2[0];
+              s1[cl2] += x2[1];
+            }
+          } else {
+            const float x = xb[p * D], x2 = xb[p2 * D];
+            s0[cl] += x;
+            if (two) s0[cl2] += x2;
+          }
+          cnt += (lane == cl ? 1u : 0u) + (two && lane == cl2 ? 1u : 0u);
+        }
+      }
+    }
+  };
+  // window k (tiles k KFS_FW .. + KFS_FW) to global memory: labels of the
+  // decided rows, the undecided bits, and (ACC) every fp32 chain into the
+  // block's fp64 partial; then wait for the stores, so that no store is
+  // pending while the prefetch ring is in flight (a pending store makes the
+  // compiler drain the ring at every staging: vmcnt(0))
+  auto drain = [&](i64 k) __attribute__((always_inline)) {
+    const i64 i0 = k * KFS_FW, i1 = i0 + KFS_FW < nit ? i0 + KFS_FW : nit;
+    for (i64 ip = i0 + w; ip < i1; ip += W) {
+      const i64 tl = bk + ip * G;
+      const int u = (int)(ip % (2 * KFS_FW));
+      const unsigned int und = und32[u];
+      const i64 row = tl * 32 + j;
+      if (h == 0 && row < N && !((und >> j) & 1u)) labels[row] = lab8[u * 32 + j];
+      if (lane == 0) und_mask[tl] = und;
+    }
+    if constexpr (ACC) {
+      if (w < NCT) {
+#pragma unroll 1
+        for (int c = 0; c < 32; ++c) flush(c);  // rolled: the 64 converted sums are not all held at once
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  };
+
+  // iterations it = 0 .. nrun - 1 (tile it screened, tile it - 1 decided,
+  // tile it + 1 staged): every unrolled copy issues its loads unconditionally
+  // (clamped addresses; iterations >= nit are ghosts whose rows are never
+  // live) -- a skipped load on any path makes the compiler's count of the
+  // loads in flight unknown, and it then drains the ring (vmcnt(0))
+  const i64 nrun = nit > 0 ? (nit + KFS_R) / KFS_R * KFS_R : 0;
+  if (nit > 0) {
+    load(ring[0], 0);
+    stage(ring[0], 0, 0);
+#pragma unroll
+    for (int r = 1; r <= KFS_R; ++r) load(ring[r % KFS_R], r);
+  }
+  for (i64 it0 = 0; it0 < nrun; it0 += KFS_R) {
+    // KFS_R iterations with compile-time ring slots (tile T lives in slot T % KFS_R)
+    ks_unroll([&](auto sc) __attribute__((always_inline)) {
+      constexpr int s = decltype(sc)::value;
+      constexpr int sl = (s + 1) % KFS_R;   // ring slot of tile it + 1
+      constexpr int bn = (s + 1) % KFS_NB;  // fp32 buffer of tile it + 1
+      const i64 it = it0 + s;
+      __syncthreads();
+      // window k = (it - KFS_R) / KFS_FW - 1 is complete in LDS since this
+      // barrier (tiles <= it - 2 are decided); one drain site, s == 0 (KFS_FW
+      // is a multiple of KFS_R, so the drain points fall on it0)
+      if constexpr (s == 0)
+        if (it >= KFS_FW + KFS_R && (it - KFS_R) % KFS_FW == 0) drain((it - KFS_R) / KFS_FW - 1);
+      // waves w and w + 4 share a SIMD: they run the latency-bound decide /
+      // accumulate and the MFMA screen in opposite orders
+      if (w < 4) {
+        if (it >= 1) decide(it - 1, (s + KFS_NB - 1) % KFS_NB);
+        if (w < NCT) screen(it);
+      } else {
+        if (w < NCT) screen(it);
+        if (it >= 1) decide(it - 1, (s + KFS_NB - 1) % KFS_NB);
+      }
+      stage(ring[sl], it + 1, bn);
+      load(ring[sl], it + 1 + KFS_R);
+    }, std::make_integer_sequence<int, KFS_R>{});
+  }
+  // the windows not drained yet: the last one (its drain point lies past the
+  // loop), and the one before it when the loop ended before its drain point
+  __syncthreads();
+  if (nit > 0) {
+    const i64 last = (nit - 1) / KFS_FW;
+    if (last >= 1 && last * KFS_FW + KFS_R >= nrun) drain(last - 1);
+    drain(last);
+  }
+  if constexpr (ACC) {
+    if (w < NCT && lane < 32 && 32 * w + lane < K) pcnt[(i64)bk * K + 32 * w + lane] = cnt;
+  }
+}
+
+template <int KS, int NCT, bool ACC>
+static void kfs_launch(hipStream_t s, int grid, i64 N, i64 K, const float* P, i64 ldp, const __bf16* CBh,
+                       const __bf16* CBl, const float* cnf2, const double* cmax, const float* muf, i64* labels,
+                       unsigned long long* und_mask, double* psum, unsigned long long* pcnt) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_kmeans_fscreen<KS, NCT, ACC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kfs_lds_bytes(16 * KS));
+    attr = true;
+  }
+  k_kmeans_fscreen<KS, NCT, ACC><<<grid, KFS_WAVES * 64, kfs_lds_bytes(16 * KS), s>>>(
+      N, K, P, ldp, CBh, CBl, cnf2, cmax, muf, labels, und_mask, psum, pcnt);
+}
+
+template <bool ACC>
+static void kfs_launch_n(int nct, int KS, hipStream_t s, int grid, i64 N, i64 K, const float* P, i64 ldp,
+                         const __bf16* CBh, const __bf16* CBl, const float* cnf2, const double* cmax, const float* muf,
+                         i64* labels, unsigned long long* und_mask, double* psum, unsigned long long* pcnt) {
+#define KFS_CASE(KSV, NC)                                                                                        \
+  if (KS == KSV && nct == NC) {                                                                                  \
+    kfs_launch<KSV, NC, ACC>(s, grid, N, K, P, ldp, CBh, CBl, cnf2, cmax, muf, labels, und_mask, psum, pcnt); \
+    return;                                                                                                      \
+  }
+  KFS_CASE(8, 8) KFS_CASE(8, 4) KFS_CASE(8, 2) KFS_CASE(8, 1)
+  KFS_CASE(4, 8) KFS_CASE(4, 4) KFS_CASE(4, 2) KFS_CASE(4, 1)
+#undef KFS_CASE
+}
+
+// Deterministic compaction of lane masks (LAYOUT 2: bit j <-> row 32 tile + j)
+// into an index-ordered row list: per-block counts, one exclusive scan, then
+// k_ks_compact at the scanned bases (the summation order of the gathered
+// accumulation depends on the list order, so it must not follow atomics).
+template <int KC_TPT>
+__global__ __launch_bounds__(256) void k_ks_count(i64 N, const unsigned long long* __restrict__ mask,
+                                                  unsigned int* __restrict__ bcnt) {
+  __shared__ unsigned int ws[4];
+  const i64 ntiles = (N + 31) / 32;
+  const i64 t0 = (i64)blockIdx.x * 256 * KC_TPT;
+  unsigned int n = 0;
+#pragma unroll
+  for (int jj = 0; jj < KC_TPT; ++jj) {
+    const i64 tl = t0 + jj * 256 + threadIdx.x;
+    n += tl < ntiles ? (unsigned int)__popcll(mask[tl]) : 0u;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// exclusive scan of n block counts in place (one block), the total into *total
+__global__ __launch_bounds__(1024) void k_exscan_u32(unsigned int* __restrict__ v, i64 n, unsigned int* __restrict__ total) {
+  __shared__ unsigned int part[1024];
+  const i64 per = (n + 1023) / 1024;
+  const i64 a = threadIdx.x * per, b = a + per < n ? a + per : n;
+  unsigned int s = 0;
+  for (i64 i = a; i < b; ++i) s += v[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned int run = 0;
+    for (int i = 0; i < 1024; ++i) {
+      const unsigned int x = part[i];
+      part[i] = run;
+      run += x;
+    }
+    *total = run;
+  }
+  __syncthreads();
+  unsigned int run = part[threadIdx.x];
+  for (i64 i = a; i < b; ++i) {
+    const unsigned int x = v[i];
+    v[i] = run;
+    run += x;
   }
 }
 
@@ -2676,10 +2820,15 @@ constexpr int KA_CB = KA_WAVES * KA_CPW;   // centres per tile
 #define KA_BPC 1                          // resident blocks per CU (LDS: 2 KA_STAGES x 16 KiB per block)
 #endif
 
+// rows / nrows (optional): accumulate only the rows rows[0 .. *nrows) (a
+// row list in row order, gathered row by row; the count is read on the device).
 template <typename TP>
 __global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(4 * KA_BPC, 8))) void k_kmeans_accum(i64 N, i64 D, i64 K, const TP* __restrict__ P, i64 ldp,
                                                              const i64* __restrict__ labels, double* __restrict__ psum,
-                                                             unsigned long long* __restrict__ pcnt, int ndb) {
+                                                             unsigned long long* __restrict__ pcnt, int ndb,
+                                                             const i64* __restrict__ rows = nullptr,
+                                                             const unsigned int* __restrict__ nrows = nullptr) {
+  if (rows) N = (i64)*nrows;
   constexpr int VE = 16 / (int)sizeof(TP);                // elements per 16-byte load
   constexpr int CH = KA_THREADS * VE / KA_DB;             // points per chunk (64 f32 / 32 f64)
   constexpr int LPR = KA_DB / VE;                         // lanes per row slice
@@ -2712,8 +2861,10 @@ __global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(4 * 
   V pf[ST];
   i64 plab[ST];
   auto load = [&](int s, i64 ch) {
+    if (N == 0) return;  // an empty row list: nothing to load
     const i64 p0 = (ch < nch ? ch : nch - 1) * CH;
-    const i64 pr = p0 + lp < N ? p0 + lp : N - 1;
+    i64 pr = p0 + lp < N ? p0 + lp : N - 1;
+    if (rows) pr = rows[pr];
     if (vec) {
       pf[s] = ld_stream((const V*)(P + pr * ldp + d0 + lc));  // read once: nt
     } else {
@@ -2723,7 +2874,10 @@ __global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(4 * 
         pf[s][j] = P[pr * ldp + d];
       }
     }
-    if (t < CH) plab[s] = labels[p0 + t < N ? p0 + t : N - 1];
+    if (t < CH) {
+      const i64 pl = p0 + t < N ? p0 + t : N - 1;
+      plab[s] = labels[rows ? rows[pl] : pl];
+    }
   };
   const i64 G = gridDim.x;
 #pragma unroll
@@ -2828,20 +2982,6 @@ static void ka_grid(int dtype, i64 N, i64 D, i64 K, i64* G, i64* ndb, i64* ncb) 
 
 static i64 kf_kp(i64 K) { return (K + KF_BN - 1) / KF_BN * KF_BN; }
 
-// SPX_KMEANS_FILTER selects the first passes (A/B timing and the
-// bit-exactness cross-checks in the GPU tests): "b3" the single
-// all-accumulator filter pass; "as" the A-stationary bf16x3 pass over every
-// row; default: the fp16 screen over every row, the A-stationary bf16x3 pass
-// over its undecided rows.  All of them end in the list-mode all-accumulator
-// pass (candidate masks), k_kmeans_cand and the exact kernel.
-static int kmeans_filter_mode() {
-  const char* v = getenv("SPX_KMEANS_FILTER");
-  if (v && strcmp(v, "b3") == 0) return 1;
-  if (v && strcmp(v, "as") == 0) return 2;
-  if (v && strcmp(v, "s16") == 0) return 3;
-  return 0;
-}
-
 static int kf_persistent_grid(i64 N) {
   const i64 g = (N + 255) / 256;
   return (int)(g < 2048 ? (g < 1 ? 1 : g) : 2048);
@@ -2856,6 +2996,106 @@ extern "C" int64_t spx_kmeans_assign_workspace(int dtype, int64_t N, int64_t D, 
   return (D * Kp * 4 + 15) / 16 * 16 + Kp * 8 + 32 + 16 + N * 8 +
          (Kp == KF_BN ? N * (i64)sizeof(KfCand) + 2 * N * 8 + (N + 31) / 32 * 8 + D * 4 : 0);
 }
+
+// spx_kmeans_assign's workspace, carved: CT (D x Kp f32, reused for the
+// bf16 split of the centres) | cn (Kp f64; the cnf / cnf2 floats of the
+// centred filters) | cmax | counters | full list (N i64) | candidate list (N
+// KfCand) | undecided-row list (N i64) | screen's undecided-row list (N i64) |
+// per-tile undecided lane masks (ceil(N / 32) u64) | centre mean (D f32); the
+// last five only for K <= 256.
+struct KmWs {
+  float* CT;
+  double* cn;
+  double* cmax;  // [0] max |c'|, [1] fp32 tie margin coefficient, [2] |mu|, [3] max |c' - fp16(c')|
+  unsigned int* counters;  // [0] full-list rows, [1] candidate rows, [2] undecided rows, [3] screen-undecided rows
+  i64* full_list;
+  KfCand* cand_list;
+  i64* und_list;
+  i64* scr_list;
+  unsigned long long* und_mask;
+  float* muf;
+};
+
+static KmWs km_carve(void* workspace, i64 N, i64 D, i64 Kp) {
+  KmWs w;
+  unsigned char* ws = (unsigned char*)workspace;
+  w.CT = (float*)ws;
+  ws += (D * Kp * 4 + 15) / 16 * 16;
+  w.cn = (double*)ws;
+  ws += Kp * 8;
+  w.cmax = (double*)ws;
+  ws += 32;
+  w.counters = (unsigned int*)ws;
+  ws += 16;
+  w.full_list = (i64*)ws;
+  ws += N * 8;
+  w.cand_list = (KfCand*)ws;
+  w.und_list = (i64*)(ws + (Kp == KF_BN ? N * (i64)sizeof(KfCand) : 0));
+  w.scr_list = w.und_list + N;
+  w.und_mask = (unsigned long long*)(w.scr_list + N);
+  w.muf = (float*)(w.und_mask + (N + 31) / 32);
+  return w;
+}
+
+static int num_cus() {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
+      ncu = 256;
+  }
+  return ncu;
+}
+
+// The passes after a certified screen left its undecided rows in
+// w.scr_list (count in counters[3]): the A-stationary bf16x3 filter in list
+// mode over them, the all-accumulator filter in list mode over what is still
+// undecided (candidate masks), the exact recompute of the candidates in
+// scipy's order, and the all-centre exact kernel for the rows no filter could
+// evaluate (non-finite / overflowing).  Labels of every row are final after it.
+static int km_resolve(hipStream_t s, i64 N, i64 D, i64 K, const float* Pf, i64 ldp, const double* centers,
+                      i64* labels, const KmWs& w, int nct, int r32) {
+  const int ncu = num_cus();
+  const i64 ntiles = (N + 31) / 32;
+  __bf16* CBh = (__bf16*)w.CT;
+  __bf16* CBl = CBh + (i64)32 * nct * D;
+  const float* cnf = (const float*)w.cn;
+  const i64 need_as = (ntiles + KS_WAVES - 1) / KS_WAVES;
+  const int grid_as = (int)(need_as < ncu ? need_as : ncu);
+  const unsigned int cgrid1 = (unsigned int)((ntiles + 255) / 256);
+  ks_launch_n<0>(nct, s, N, D, Pf, ldp, CBh, CBl, cnf, w.cmax, labels, w.counters, w.full_list, w.und_mask,
+                 w.scr_list, w.counters + 3, nullptr, grid_as);
+  LAUNCH_CHECK("spx_kmeans_assign(filter A-stationary, list)");
+  k_ks_compact<1><<<cgrid1, 256, 0, s>>>(N, w.und_mask, w.scr_list, w.counters + 3, w.und_list, w.counters + 2);
+  LAUNCH_CHECK("spx_kmeans_assign(compact)");
+  switch (nct) {
+    case 1: kb_launch<1>(s, N, D, Pf, ldp, CBh, CBl, cnf, w.cmax, labels, w.counters, w.full_list, w.cand_list, ncu, w.und_list, w.counters + 2); break;
+    case 2: kb_launch<2>(s, N, D, Pf, ldp, CBh, CBl, cnf, w.cmax, labels, w.counters, w.full_list, w.cand_list, ncu, w.und_list, w.counters + 2); break;
+    case 4: kb_launch<4>(s, N, D, Pf, ldp, CBh, CBl, cnf, w.cmax, labels, w.counters, w.full_list, w.cand_list, ncu, w.und_list, w.counters + 2); break;
+    default: kb_launch<8>(s, N, D, Pf, ldp, CBh, CBl, cnf, w.cmax, labels, w.counters, w.full_list, w.cand_list, ncu, w.und_list, w.counters + 2); break;
+  }
+  LAUNCH_CHECK("spx_kmeans_assign(filter bf16x3, undecided rows)");
+  const int gp = kf_persistent_grid(N);
+  if ((D == 64 || D == 128) && ((uintptr_t)centers % 16) == 0) {
+    if (D == 64) k_kmeans_cand16<4><<<gp, 256, 0, s>>>(Pf, ldp, centers, labels, w.counters, w.cand_list, r32);
+    else k_kmeans_cand16<8><<<gp, 256, 0, s>>>(Pf, ldp, centers, labels, w.counters, w.cand_list, r32);
+  } else {
+    k_kmeans_cand<float, true><<<gp, 256, 0, s>>>(D, Pf, ldp, centers, labels, w.counters, w.cand_list, r32);
+  }
+  LAUNCH_CHECK("spx_kmeans_assign(candidates)");
+  k_kmeans_assign<float><<<gp, 256, 0, s>>>(N, D, K, Pf, ldp, centers, labels, nullptr, w.full_list, w.counters, r32);
+  LAUNCH_CHECK("spx_kmeans_assign(exact)");
+  return SPX_OK;
+}
+
+// the certified screens' domain: fp32 points, K <= 256, D in {64, 128}, 16-byte rows
+static bool km_screen_ok(int dtype, i64 K, i64 D, const void* points, i64 ldp) {
+  return dtype == SPX_F32 && kf_kp(K) == KF_BN && (D == 64 || D == 128) && ldp % 4 == 0 &&
+         ((uintptr_t)points % 16) == 0;
+}
+
+static int km_nct(i64 K) { return K <= 32 ? 1 : K <= 64 ? 2 : K <= 128 ? 4 : 8; }
 
 extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
                                  const double* centers, int64_t* labels, double* mindist, void* workspace,
@@ -2884,147 +3124,60 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
   if ((int64_t)workspace_bytes < need)
     return set_err(SPX_EINVAL, "spx_kmeans_assign: workspace %zu < %lld bytes", workspace_bytes, (long long)need);
   const i64 Kp = kf_kp(K);
-  unsigned char* ws = (unsigned char*)workspace;
-  float* CT = (float*)ws;
-  ws += (D * Kp * 4 + 15) / 16 * 16;
-  double* cn = (double*)ws;
-  ws += Kp * 8;
-  double* cmax = (double*)ws;  // [0] max |c'|, [1] fp32 tie margin coefficient, [2] |mu|
-  ws += 32;
-  unsigned int* counters = (unsigned int*)ws;
-  ws += 16;
-  i64* full_list = (i64*)ws;
-  ws += N * 8;
-  KfCand* cand_list = (KfCand*)ws;
-  i64* und_list = (i64*)(ws + (Kp == KF_BN ? N * (i64)sizeof(KfCand) : 0));
-  i64* scr_list = und_list + N;  // (K <= 256 only)
-  unsigned long long* und_mask = (unsigned long long*)(scr_list + N);
-  float* muf = (float*)(und_mask + (N + 31) / 32);
-  // counters: [0] full-list rows, [1] candidate rows, [2] undecided rows,
-  // [3] rows the fp16 screen left undecided
-  HIP_TRY(hipMemsetAsync(counters, 0, 4 * sizeof(unsigned int), S(stream)));
+  const KmWs w = km_carve(workspace, N, D, Kp);
+  HIP_TRY(hipMemsetAsync(w.counters, 0, 4 * sizeof(unsigned int), S(stream)));
   const int gp = kf_persistent_grid(N);
-  if (dtype == SPX_F32 && Kp == KF_BN && D % 64 == 0 && D <= KB_DMAX && ldp % 4 == 0 &&
-      ((uintptr_t)points % 16) == 0) {
-    // bf16x3 filter; the split centres reuse the CT area (2 x 2 B <= 4 B per element)
-    const int nct = K <= 32 ? 1 : K <= 64 ? 2 : K <= 128 ? 4 : 8;
-    __bf16* CBh = (__bf16*)CT;
+  if (km_screen_ok(dtype, K, D, points, ldp)) {
+    // fp16 screen (A-stationary, k_kmeans_filter_as MODE 1) over every row,
+    // then km_resolve over the rows it leaves undecided
+    const int nct = km_nct(K);
+    __bf16* CBh = (__bf16*)w.CT;
     __bf16* CBl = CBh + (i64)32 * nct * D;
-    float* cnf = (float*)cn;
+    float* cnf = (float*)w.cn;
     float* cnf2 = cnf + KF_BN;  // |c'|^2 for the screen (the cn area holds 2 KF_BN floats)
-    k_kmeans_prep_b3<<<1, 1024, 0, S(stream)>>>(D, K, 32 * nct, centers, CBh, CBl, cnf, cmax, mcoef, cnf2, muf);
+    k_kmeans_prep_b3<<<1, 1024, 0, S(stream)>>>(D, K, 32 * nct, centers, CBh, CBl, cnf, w.cmax, mcoef, cnf2, w.muf);
     LAUNCH_CHECK("spx_kmeans_assign(prep)");
-    static int ncu = 0;
-    if (!ncu) {
-      int dev = 0;
-      HIP_TRY(hipGetDevice(&dev));
-      HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    }
+    const int ncu = num_cus();
     const i64 ntiles = (N + 31) / 32;
-    const float* Pf = (const float*)points;
-    const int fmode = kmeans_filter_mode();
-    if (fmode != 1) {
-      // fp16 screen over every row, then the A-stationary bf16x3 pass over
-      // its undecided rows (mode "as": over every row), then the
-      // all-accumulator filter in list mode over what is still undecided
-      // (candidate masks)
-      const i64 need_as = (ntiles + KS_WAVES - 1) / KS_WAVES;
-      const int grid_as = (int)(need_as < ncu ? need_as : ncu);
-      const i64 need_scr = (ntiles + ks_waves(1) - 1) / ks_waves(1);
-      const int grid_scr = (int)(need_scr < ncu ? need_scr : ncu);
-      const unsigned int cgrid = (unsigned int)((ntiles + 256 * 16 - 1) / (256 * 16));
-      const unsigned int cgrid1 = (unsigned int)((ntiles + 255) / 256);
-      if (fmode == 0 || fmode == 3) {
-        if (fmode == 3) {
-          s16_launch_n(nct, S(stream), N, D, Pf, ldp, CBh, CBl, cnf2, cmax, labels, und_mask, muf, grid_scr);
-          LAUNCH_CHECK("spx_kmeans_assign(fp16 screen, 16x16x32)");
-          k_ks_compact<16, 1><<<cgrid, 256, 0, S(stream)>>>(N, und_mask, nullptr, nullptr, scr_list, counters + 3);
-        } else {
-          ks_launch_n<1>(nct, S(stream), N, D, Pf, ldp, CBh, CBl, cnf2, cmax, labels, counters, full_list, und_mask,
-                         nullptr, nullptr, muf, grid_scr);
-          LAUNCH_CHECK("spx_kmeans_assign(fp16 screen)");
-          k_ks_compact<16><<<cgrid, 256, 0, S(stream)>>>(N, und_mask, nullptr, nullptr, scr_list, counters + 3);
-        }
-        LAUNCH_CHECK("spx_kmeans_assign(compact)");
-        ks_launch_n<0>(nct, S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_mask,
-                       scr_list, counters + 3, nullptr, grid_as);
-        LAUNCH_CHECK("spx_kmeans_assign(filter A-stationary)");
-        k_ks_compact<1><<<cgrid1, 256, 0, S(stream)>>>(N, und_mask, scr_list, counters + 3, und_list, counters + 2);
-      } else {
-        ks_launch_n<0>(nct, S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, und_mask,
-                       nullptr, nullptr, nullptr, grid_as);
-        LAUNCH_CHECK("spx_kmeans_assign(filter A-stationary)");
-        k_ks_compact<16><<<cgrid, 256, 0, S(stream)>>>(N, und_mask, nullptr, nullptr, und_list, counters + 2);
-      }
-      LAUNCH_CHECK("spx_kmeans_assign(compact)");
-      const i64* rin = und_list;
-      const unsigned int* nin = counters + 2;
-      switch (nct) {
-        case 1: kb_launch<1>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, ncu, rin, nin); break;
-        case 2: kb_launch<2>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, ncu, rin, nin); break;
-        case 4: kb_launch<4>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, ncu, rin, nin); break;
-        default: kb_launch<8>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, ncu, rin, nin); break;
-      }
-      LAUNCH_CHECK("spx_kmeans_assign(filter bf16x3, undecided rows)");
-    } else {
-      const i64 need_blocks = (ntiles + KB_WAVES - 1) / KB_WAVES;
-      const int grid = (int)(need_blocks < ncu ? need_blocks : ncu);
-      switch (nct) {
-        case 1: kb_launch<1>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, grid); break;
-        case 2: kb_launch<2>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, grid); break;
-        case 4: kb_launch<4>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, grid); break;
-        default: kb_launch<8>(S(stream), N, D, Pf, ldp, CBh, CBl, cnf, cmax, labels, counters, full_list, cand_list, grid); break;
-      }
-      LAUNCH_CHECK("spx_kmeans_assign(filter bf16x3)");
-    }
-    if ((D == 64 || D == 128) && ((uintptr_t)centers % 16) == 0 && getenv("SPX_KMEANS_CAND4") == nullptr) {
-      if (D == 64) k_kmeans_cand16<4><<<gp, 256, 0, S(stream)>>>(Pf, ldp, centers, labels, counters, cand_list, r32);
-      else k_kmeans_cand16<8><<<gp, 256, 0, S(stream)>>>(Pf, ldp, centers, labels, counters, cand_list, r32);
-    } else {
-      k_kmeans_cand<float, true><<<gp, 256, 0, S(stream)>>>(D, Pf, ldp, centers, labels, counters, cand_list, r32);
-    }
-    LAUNCH_CHECK("spx_kmeans_assign(candidates)");
-    k_kmeans_assign<float><<<gp, 256, 0, S(stream)>>>(N, D, K, Pf, ldp, centers, labels, nullptr, full_list,
-                                                       counters, r32);
-    LAUNCH_CHECK("spx_kmeans_assign(exact)");
-    if (getenv("SPX_KMEANS_DEBUG")) {  // dev: row counts of each stage (synchronises the stream)
-      unsigned int hc[4];
-      HIP_TRY(hipMemcpyAsync(hc, counters, sizeof(hc), hipMemcpyDeviceToHost, S(stream)));
-      HIP_TRY(hipStreamSynchronize(S(stream)));
-      fprintf(stderr, "spx_kmeans_assign: N %lld screen-undecided %u bf16x3-undecided %u candidate rows %u full %u\n",
-              (long long)N, hc[3], hc[2], hc[1], hc[0]);
-    }
-    return SPX_OK;
+    const i64 need_scr = (ntiles + ks_waves(1) - 1) / ks_waves(1);
+    const int grid_scr = (int)(need_scr < ncu ? need_scr : ncu);
+    const unsigned int cgrid = (unsigned int)((ntiles + 256 * 16 - 1) / (256 * 16));
+    ks_launch_n<1>(nct, S(stream), N, D, (const float*)points, ldp, CBh, CBl, cnf2, w.cmax, labels, w.counters,
+                   w.full_list, w.und_mask, nullptr, nullptr, w.muf, grid_scr);
+    LAUNCH_CHECK("spx_kmeans_assign(fp16 screen)");
+    k_ks_compact<16><<<cgrid, 256, 0, S(stream)>>>(N, w.und_mask, nullptr, nullptr, w.scr_list, w.counters + 3);
+    LAUNCH_CHECK("spx_kmeans_assign(compact)");
+    return km_resolve(S(stream), N, D, K, (const float*)points, ldp, centers, labels, w, nct, r32);
   }
-  k_kmeans_prep<<<1, 256, 0, S(stream)>>>(D, K, Kp, centers, CT, cn, cmax, mcoef);
+  k_kmeans_prep<<<1, 256, 0, S(stream)>>>(D, K, Kp, centers, w.CT, w.cn, w.cmax, mcoef);
   LAUNCH_CHECK("spx_kmeans_assign(prep)");
   const i64 gf = (N + KfProd::BM - 1) / KfProd::BM;
   const bool al = D % KF_BK == 0 && ldp % 4 == 0 && ((uintptr_t)points % 16) == 0;
   if (dtype == SPX_F32) {
-    if (al) KfProd::launch<float, true>(gf, S(stream), N, D, K, Kp, points, ldp, CT, cn, cmax, labels, counters,
-                                        full_list, cand_list);
-    else KfProd::launch<float, false>(gf, S(stream), N, D, K, Kp, points, ldp, CT, cn, cmax, labels, counters,
-                                      full_list, cand_list);
+    if (al) KfProd::launch<float, true>(gf, S(stream), N, D, K, Kp, points, ldp, w.CT, w.cn, w.cmax, labels,
+                                        w.counters, w.full_list, w.cand_list);
+    else KfProd::launch<float, false>(gf, S(stream), N, D, K, Kp, points, ldp, w.CT, w.cn, w.cmax, labels, w.counters,
+                                      w.full_list, w.cand_list);
   } else {
-    KfProd::launch<double, false>(gf, S(stream), N, D, K, Kp, points, ldp, CT, cn, cmax, labels, counters, full_list,
-                                  cand_list);
+    KfProd::launch<double, false>(gf, S(stream), N, D, K, Kp, points, ldp, w.CT, w.cn, w.cmax, labels, w.counters,
+                                  w.full_list, w.cand_list);
   }
   LAUNCH_CHECK("spx_kmeans_assign(filter)");
   if (Kp == KF_BN) {
     if (dtype == SPX_F32)
-      k_kmeans_cand<float, false><<<gp, 256, 0, S(stream)>>>(D, (const float*)points, ldp, centers, labels, counters,
-                                                       cand_list, r32);
+      k_kmeans_cand<float, false><<<gp, 256, 0, S(stream)>>>(D, (const float*)points, ldp, centers, labels,
+                                                             w.counters, w.cand_list, r32);
     else
-      k_kmeans_cand<double, false><<<gp, 256, 0, S(stream)>>>(D, (const double*)points, ldp, centers, labels, counters,
-                                                        cand_list, r32);
+      k_kmeans_cand<double, false><<<gp, 256, 0, S(stream)>>>(D, (const double*)points, ldp, centers, labels,
+                                                              w.counters, w.cand_list, r32);
     LAUNCH_CHECK("spx_kmeans_assign(candidates)");
   }
   if (dtype == SPX_F32)
     k_kmeans_assign<float><<<gp, 256, 0, S(stream)>>>(N, D, K, (const float*)points, ldp, centers, labels, nullptr,
-                                                       full_list, counters, r32);
+                                                       w.full_list, w.counters, r32);
   else
     k_kmeans_assign<double><<<gp, 256, 0, S(stream)>>>(N, D, K, (const double*)points, ldp, centers, labels,
-                                                        nullptr, full_list, counters, r32);
+                                                        nullptr, w.full_list, w.counters, r32);
   LAUNCH_CHECK("spx_kmeans_assign(exact)");
   return SPX_OK;
 }
@@ -3074,6 +3227,102 @@ extern "C" int spx_kmeans_accumulate(int dtype, int64_t N, int64_t D, int64_t K,
   k_kmeans_reduce<unsigned long long><<<(unsigned)((K + 63) / 64), 256, 0, S(stream)>>>(
       K, G, pcnt, (unsigned long long*)counts, add);
   LAUNCH_CHECK("spx_kmeans_accumulate(reduce counts)");
+  return SPX_OK;
+}
+
+// ------------------------------------------------------- fused k-means step
+// spx_kmeans_step = spx_kmeans_assign + spx_kmeans_accumulate with the same
+// results (labels bit for bit; counts exact; sums deterministic, within the
+// fp32-chain bound below of the fp64 sums) and, in the certified screen's
+// domain, ONE pass over the points for the decided rows: k_kmeans_fscreen
+// labels and accumulates them; the rows it leaves undecided (a few %) are
+// listed in row order, resolved by km_resolve and accumulated by
+// k_kmeans_accum over that list.  Partials are combined in a fixed order.
+// Workspace: spx_kmeans_assign's | spx_kmeans_accumulate's | fused partial
+// sums (G x K x D f64) | fused partial counts (G x K u64) | compaction block
+// counts.
+static i64 kfs_grid(i64 N) {
+  const i64 ntiles = (N + 31) / 32, ncu = num_cus();
+  return ntiles < ncu ? (ntiles < 1 ? 1 : ntiles) : ncu;
+}
+
+static i64 kfs_nblk(i64 N) { return ((N + 31) / 32 + 256 * 16 - 1) / (256 * 16); }
+
+extern "C" int64_t spx_kmeans_step_workspace(int dtype, int64_t N, int64_t D, int64_t K) {
+  const int64_t a = spx_kmeans_assign_workspace(dtype, N, D, K);
+  const int64_t c = spx_kmeans_accumulate_workspace(dtype, N, D, K);
+  if (a < 0 || c < 0) return -1;
+  const i64 G = kfs_grid(N);
+  return (a + 255) / 256 * 256 + (c + 255) / 256 * 256 + G * K * D * 8 + G * K * 8 + (kfs_nblk(N) + 1) * 4 + 256;
+}
+
+extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
+                               const double* centers, int64_t* labels, double* sums, uint64_t* counts, int zero_first,
+                               void* workspace, size_t workspace_bytes, int dist_dtype, void* stream) {
+  if (dtype != SPX_F32 && dtype != SPX_F64) return set_err(SPX_ENOTSUP, "spx_kmeans_step: points must be F32/F64");
+  if (N < 0 || D < 1 || K < 1 || (N > 0 && ldp < D)) return set_err(SPX_EINVAL, "spx_kmeans_step: bad N/D/K/ldp");
+  if (dist_dtype != SPX_F64 && dist_dtype != SPX_F32)
+    return set_err(SPX_EINVAL, "spx_kmeans_step: dist_dtype must be F64 or F32");
+  if (!sums || !counts || !centers || (N > 0 && (!points || !labels)) || !workspace)
+    return set_err(SPX_EINVAL, "spx_kmeans_step: null pointer");
+  const int64_t need = spx_kmeans_step_workspace(dtype, N, D, K);
+  if (need < 0 || (int64_t)workspace_bytes < need)
+    return set_err(SPX_EINVAL, "spx_kmeans_step: workspace %zu < %lld bytes", workspace_bytes, (long long)need);
+  const int64_t na = spx_kmeans_assign_workspace(dtype, N, D, K);
+  const int64_t nc = spx_kmeans_accumulate_workspace(dtype, N, D, K);
+  unsigned char* wa = (unsigned char*)workspace;
+  unsigned char* wc = wa + (na + 255) / 256 * 256;
+  if (N == 0 || !km_screen_ok(dtype, K, D, points, ldp)) {  // two passes: assign, then accumulate
+    int rc = spx_kmeans_assign(dtype, N, D, K, points, ldp, centers, labels, nullptr, wa, (size_t)na, dist_dtype,
+                               stream);
+    if (rc) return rc;
+    return spx_kmeans_accumulate(dtype, N, D, K, points, ldp, labels, sums, counts, zero_first, wc, (size_t)nc, stream);
+  }
+  const i64 Kp = kf_kp(K), G = kfs_grid(N), nb = kfs_nblk(N), ntiles = (N + 31) / 32;
+  double* psumF = (double*)(wc + (nc + 255) / 256 * 256);
+  unsigned long long* pcntF = (unsigned long long*)(psumF + G * K * D);
+  unsigned int* bcnt = (unsigned int*)(pcntF + G * K);
+  const KmWs w = km_carve(wa, N, D, Kp);
+  const int r32 = dist_dtype == SPX_F32;
+  const double mcoef = r32 ? 4.76837158203125e-07 : 0.0;  // 2^-21
+  const int nct = km_nct(K);
+  const float* Pf = (const float*)points;
+  __bf16* CBh = (__bf16*)w.CT;
+  __bf16* CBl = CBh + (i64)32 * nct * D;
+  float* cnf = (float*)w.cn;
+  float* cnf2 = cnf + KF_BN;
+  HIP_TRY(hipMemsetAsync(w.counters, 0, 4 * sizeof(unsigned int), S(stream)));
+  HIP_TRY(hipMemsetAsync(psumF, 0, (size_t)G * K * D * sizeof(double), S(stream)));
+  k_kmeans_prep_b3<<<1, 1024, 0, S(stream)>>>(D, K, 32 * nct, centers, CBh, CBl, cnf, w.cmax, mcoef, cnf2, w.muf);
+  LAUNCH_CHECK("spx_kmeans_step(prep)");
+  kfs_launch_n<true>(nct, (int)(D / 16), S(stream), (int)G, N, K, Pf, ldp, CBh, CBl, cnf2, w.cmax, w.muf, labels,
+                     w.und_mask, psumF, pcntF);
+  LAUNCH_CHECK("spx_kmeans_step(fused screen + accumulate)");
+  // the screen's undecided rows, in row order (the gathered accumulation's order)
+  k_ks_count<16><<<(unsigned)nb, 256, 0, S(stream)>>>(N, w.und_mask, bcnt);
+  k_exscan_u32<<<1, 1024, 0, S(stream)>>>(bcnt, nb, w.counters + 3);
+  k_ks_compact<16, 2><<<(unsigned)nb, 256, 0, S(stream)>>>(N, w.und_mask, nullptr, nullptr, w.scr_list, nullptr, bcnt);
+  LAUNCH_CHECK("spx_kmeans_step(compact)");
+  (void)ntiles;
+  int rc = km_resolve(S(stream), N, D, K, Pf, ldp, centers, labels, w, nct, r32);
+  if (rc) return rc;
+  // the undecided rows' sums and counts, gathered through the row list
+  i64 G2, ndb, ncb;
+  ka_grid(dtype, N, D, K, &G2, &ndb, &ncb);
+  if (ndb * ncb > 65535) return set_err(SPX_ENOTSUP, "spx_kmeans_step: K*D too large");
+  double* psum2 = (double*)wc;
+  unsigned long long* pcnt2 = (unsigned long long*)(psum2 + G2 * K * D);
+  k_kmeans_accum<float><<<dim3((unsigned)G2, (unsigned)(ndb * ncb)), KA_THREADS, 0, S(stream)>>>(
+      N, D, K, Pf, ldp, labels, psum2, pcnt2, (int)ndb, w.scr_list, w.counters + 3);
+  LAUNCH_CHECK("spx_kmeans_step(accumulate undecided rows)");
+  const i64 n = K * D;
+  k_kmeans_reduce<double><<<(unsigned)((n + 63) / 64), 256, 0, S(stream)>>>(n, G, psumF, sums, zero_first ? 0 : 1);
+  k_kmeans_reduce<double><<<(unsigned)((n + 63) / 64), 256, 0, S(stream)>>>(n, G2, psum2, sums, 1);
+  k_kmeans_reduce<unsigned long long><<<(unsigned)((K + 63) / 64), 256, 0, S(stream)>>>(
+      K, G, pcntF, (unsigned long long*)counts, zero_first ? 0 : 1);
+  k_kmeans_reduce<unsigned long long><<<(unsigned)((K + 63) / 64), 256, 0, S(stream)>>>(
+      K, G2, pcnt2, (unsigned long long*)counts, 1);
+  LAUNCH_CHECK("spx_kmeans_step(reduce)");
   return SPX_OK;
 }
 

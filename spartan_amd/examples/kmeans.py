@@ -211,6 +211,7 @@ class KMeans(object):
     elif isinstance(centers, np.ndarray):
       centers = expr.from_numpy(centers)
     for i in range(self.n_iter):
+      self.assign_centers_ = centers  # the centres this iteration's labels are assigned against
       distances = expr.outer((X, centers), (0, 0), fn=kmeans_dist_mapper,
                              shape=(X.shape[0], centers.shape[0]))
       labels = expr.argmin(distances, axis=1)

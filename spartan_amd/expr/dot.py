@@ -168,14 +168,11 @@ def run_dot(a, b, tile_hint=None):
     return _combine_rows(partials, A, M, N, out_shape, dtype, tile_hint, k_split=any(
         ex.ul[1] != 0 or ex.lr[1] != K for ex in A.tiles2()))
   btiles = B.tiles2() if not b.replicated else {ext.from_shape((K, N)): -1}
-  # a lone rank whose B blocks tile every output column needs no zero fill:
-  # the first GEMM into each column block runs with beta = 0
+  # no zero fill of the (M, N) partial: the first GEMM into each column
+  # block runs with beta = 0, and only column blocks this rank computes
+  # nothing for are zeroed (a rank without local B blocks)
   col_blocks = sorted({(bex.ul[1], bex.lr[1]) for bex in btiles})
-  lone = not ctx.distributed
-  if lone:
-    C = torch.empty((M, N), dtype=backend.torch_dtype(dtype), device=ctx.device)
-  else:
-    C = torch.zeros((M, N), dtype=backend.torch_dtype(dtype), device=ctx.device)
+  C = torch.empty((M, N), dtype=backend.torch_dtype(dtype), device=ctx.device)
   started = set()
   requests, plan = [], []
   for bex, w in btiles.items():
@@ -188,7 +185,7 @@ def run_dot(a, b, tile_hint=None):
   got = distarray.gather_regions(a, requests)
   output = distarray.create(out_shape, dtype, reducer=np.add, tile_hint=tile_hint)
   if ctx.distributed and len(out_shape) == 2 and FLAGS.dot_overlap and _owner_slabs(output, ctx, M):
-    return _dot_overlapped(output, got, plan, b, B, K, M, N, dtype, C)
+    return _dot_overlapped(output, got, plan, b, B, K, M, N, dtype, C, col_blocks)
   for qi, (bex, dst) in enumerate(plan):
     if dst != ctx.rank:
       continue
@@ -200,9 +197,12 @@ def run_dot(a, b, tile_hint=None):
     bt = _as_dtype(bt, dtype)
     cview = C[:, bex.ul[1]:bex.lr[1]]
     key = (bex.ul[1], bex.lr[1])
-    beta = 0.0 if (lone and key not in started) else 1.0
+    beta = 0.0 if key not in started else 1.0
     started.add(key)
     be.gemm(at, bt, cview, 1.0, beta)
+  for c0, c1 in col_blocks:
+    if (c0, c1) not in started:
+      C[:, c0:c1].zero_()
   _scatter_full(output, C.reshape(out_shape), 'sum')
   return output
 
@@ -215,7 +215,7 @@ def _owner_slabs(output, ctx, M):
   return _rank_slabs(output, ctx) and M % ctx.world_size == 0
 
 
-def _dot_overlapped(output, got, plan, b, B, K, M, N, dtype, C):
+def _dot_overlapped(output, got, plan, b, B, K, M, N, dtype, C, col_blocks):
   """K-split partials reduced chunk by chunk while the next chunk computes.
 
   The output is one row slab per rank.  Every rank computes its partial of
@@ -242,8 +242,14 @@ def _dot_overlapped(output, got, plan, b, B, K, M, N, dtype, C):
   handles = []
   for j in range(ctx.world_size):
     r0, r1 = j * slab, (j + 1) * slab
+    started = set()
     for bex, at, bt in local:
-      be.gemm(at[r0:r1], bt, C[r0:r1, bex.ul[1]:bex.lr[1]], 1.0, 1.0)
+      key = (bex.ul[1], bex.lr[1])
+      be.gemm(at[r0:r1], bt, C[r0:r1, key[0]:key[1]], 1.0, 0.0 if key not in started else 1.0)
+      started.add(key)
+    for c0, c1 in col_blocks:
+      if (c0, c1) not in started:
+        C[r0:r1, c0:c1].zero_()
     handles.append(comm.reduce_async(C[r0:r1], j, 'sum'))
   comm.wait_all(handles)
   (d, t), = output.local.items()

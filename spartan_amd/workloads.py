@@ -39,12 +39,13 @@ def kmeans_fit(X, n_clusters, n_iter, centers=None, seed=0, info=None):
   """KMeans.fit, 'outer' implementation (spartan/examples/sklearn/cluster/
   k_means_.py:108-152), one fused pass pair per iteration on every rank:
 
-    assign      spx_kmeans_assign: cdist + argmin(axis=1) with scipy's exact
+    step        spx_kmeans_step: cdist + argmin(axis=1) with scipy's exact
                 fp64 operation order -> bit-exact int64 labels, no (N, k)
                 distance matrix is ever materialised (the reference's is
-                N x k fp64 = 204.8 GB at cfg3);
-    accumulate  spx_kmeans_accumulate: per-centre fp64 sums + counts of the
-                local row strips; one RCCL all-reduce of K*D + K values;
+                N x k fp64 = 204.8 GB at cfg3), and the per-centre sums +
+                counts of the local row strips -- one pass over the points
+                for the rows the certified screen decides; one RCCL
+                all-reduce of K*D + K values;
     host        empty-cluster reseed and centers = sums / counts (fp64).
 
   Divergences, documented in DESIGN.md: counts / centre sums are SUMMED over
@@ -83,8 +84,9 @@ def kmeans_fit(X, n_clusters, n_iter, centers=None, seed=0, info=None):
     first = True
     for ex, tile in Xa.local.items():
       lab = torch.empty((ex.shape[0],), dtype=torch.int64, device=ctx.device)
-      be.kmeans_assign(tile.data, cdev, lab)
-      be.kmeans_accumulate(tile.data, lab, sums, counts, zero_first=first)
+      # assignment + accumulation in one call: in the certified screen's
+      # domain one pass over the tile labels and accumulates the decided rows
+      be.kmeans_step(tile.data, cdev, lab, sums, counts, zero_first=first)
       first = False
       label_tiles[ex] = lab
     if first:  # no local tiles

@@ -213,3 +213,7 @@ class FakeBackend:
     np.add.at(c, lab, 1)
     sums.copy_(torch.as_tensor(s))
     counts.copy_(torch.as_tensor(c))
+
+  def kmeans_step(self, points, centers, labels, sums, counts, zero_first=True, dist_dtype=np.float64):
+    self.kmeans_assign(points, centers, labels, dist_dtype=dist_dtype)
+    self.kmeans_accumulate(points, labels, sums, counts, zero_first=zero_first)

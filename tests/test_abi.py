@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
   for n in declared():
     assert hasattr(lib, n), n
   lib.spx_abi_version.restype = ctypes.c_int
-  assert lib.spx_abi_version() == 2
+  assert lib.spx_abi_version() == 3
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason='libspx.so not built')

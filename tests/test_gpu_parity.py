@@ -525,7 +525,7 @@ def test_lreg_cfg5_full_size(ex):
   np.testing.assert_allclose(np.asarray(got, np.float64), exact, rtol=1e-5, atol=1e-5 * np.abs(exact).max())
 
 
-def test_kmeans_cfg3_full_size(ex, monkeypatch):
+def test_kmeans_cfg3_full_size(ex):
   """cfg3 at its BASELINE size (1e8 x 128 fp32, k = 256, second-iteration
   centres): the certified assignment equals the all-exact kernel on a 2M-row
   prefix and on 2M rows at the end, and on ALL 1e8 rows the default path (fp16
@@ -552,12 +552,14 @@ def test_kmeans_cfg3_full_size(ex, monkeypatch):
     ref = torch.empty((b - a,), dtype=torch.int64, device=dev)
     be.kmeans_assign(pts[a:b], cen, ref, exact_only=True)
     assert torch.equal(lab[a:b], ref)
-  monkeypatch.setenv('SPX_KMEANS_FILTER', 'as')
-  lab_as = torch.empty_like(lab)
-  be.kmeans_assign(pts, cen, lab_as)
-  monkeypatch.delenv('SPX_KMEANS_FILTER')
-  assert torch.equal(lab_as, lab)
-  del lab_as
+  # the fused step (B-stationary screen + accumulation, one pass) against
+  # the A-stationary screen's labels on every row: two certified screens
+  lab_st = torch.empty_like(lab)
+  s_st = torch.empty_like(sums)
+  c_st = torch.empty_like(cnt)
+  be.kmeans_step(pts, cen, lab_st, s_st, c_st)
+  assert torch.equal(lab_st, lab)
+  del lab_st
   be.kmeans_accumulate(pts, lab, sums, cnt)
   s2 = torch.zeros((K, D), dtype=torch.float64, device=dev)
   c2 = torch.zeros((K,), dtype=torch.int64, device=dev)
@@ -567,6 +569,8 @@ def test_kmeans_cfg3_full_size(ex, monkeypatch):
     c2 += torch.bincount(li, minlength=K)
   assert torch.equal(cnt, c2) and int(cnt.sum()) == N
   torch.testing.assert_close(sums, s2, rtol=1e-12, atol=1e-9)
+  assert torch.equal(c_st, c2)
+  torch.testing.assert_close(s_st, s2, rtol=1e-6, atol=0)   # fp32 chains of <= 255 tiles per block
 
 
 # ------------------------------------------------------ cfg5: lreg gradient
@@ -806,13 +810,28 @@ def test_kmeans_assign_certified_bit_exact(ex, kind, dt, ddt):
     assert (want64 != cdist(pts.astype(np.float64), C).astype(np.float32).argmin(1)).any()
 
 
-@pytest.mark.parametrize('mode', ['scr', 's16', 'as', 'b3'])
+def _first_pass(be, mode, P, C, out, ddt=np.float64):
+  """Labels through one of the two certified first passes: 'assign' -- the
+  A-stationary fp16 screen of spx_kmeans_assign; 'step' -- the B-stationary
+  fused screen + accumulation of spx_kmeans_step.  Both end in the same list
+  passes (bf16x3, candidate masks, exact recompute)."""
+  import torch
+  if mode == 'assign':
+    be.kmeans_assign(P, C, out, dist_dtype=ddt)
+  else:
+    K, D = C.shape
+    sums = torch.empty((K, D), dtype=torch.float64, device=P.device)
+    cnt = torch.empty((K,), dtype=torch.int64, device=P.device)
+    be.kmeans_step(P, C, out, sums, cnt, dist_dtype=ddt)
+
+
+@pytest.mark.parametrize('mode', ['assign', 'step'])
 @pytest.mark.parametrize('D', [64, 128])
 @pytest.mark.parametrize('K', [1, 7, 32, 33, 100, 256])
-def test_kmeans_bf16x3_filter_bit_exact(ex, D, K, mode, monkeypatch):
-  """The certified filters (fp32 points, K <= 256, D % 64 == 0) in all three
-  first-pass modes (fp16 screen + A-stationary bf16x3 list pass, A-stationary
-  bf16x3 over every row, all-accumulator bf16x3): labels bit-identical to the
+def test_kmeans_bf16x3_filter_bit_exact(ex, D, K, mode):
+  """The certified filters (fp32 points, K <= 256, D in {64, 128}) behind
+  both first passes (the A-stationary screen of spx_kmeans_assign and the
+  fused B-stationary screen of spx_kmeans_step): labels bit-identical to the
   all-exact fp64 kernel (scipy cdist order, ties -> first index) on uniform
   data, exact duplicate centres, equidistant points, a ragged last tile, rows
   that must take the non-finite path (NaN, 1e30), a component past the fp16
@@ -821,7 +840,6 @@ def test_kmeans_bf16x3_filter_bit_exact(ex, D, K, mode, monkeypatch):
   from oracle import workloads as OW
   from spartan_amd import backend
   be = backend.get()
-  monkeypatch.setenv('SPX_KMEANS_FILTER', mode)
   g = np.random.default_rng(D * 1000 + K)
   n = 20011
   pts = g.random((n, D)).astype(np.float32)
@@ -840,7 +858,7 @@ def test_kmeans_bf16x3_filter_bit_exact(ex, D, K, mode, monkeypatch):
   C = torch.as_tensor(centers).cuda()
   fast = torch.empty(n, dtype=torch.int64, device='cuda')
   exact = torch.empty(n, dtype=torch.int64, device='cuda')
-  be.kmeans_assign(P, C, fast)
+  _first_pass(be, mode, P, C, fast)
   be.kmeans_assign(P, C, exact, exact_only=True)
   f, e = fast.cpu().numpy(), exact.cpu().numpy()
   np.testing.assert_array_equal(f, e)
@@ -848,10 +866,10 @@ def test_kmeans_bf16x3_filter_bit_exact(ex, D, K, mode, monkeypatch):
   np.testing.assert_array_equal(f[ok][:3000], OW.kmeans_assign(pts[ok][:3000], centers))
 
 
-@pytest.mark.parametrize('mode', ['scr', 's16', 'as', 'b3'])
+@pytest.mark.parametrize('mode', ['assign', 'step'])
 @pytest.mark.parametrize('ddt', [np.float64, np.float32])
 @pytest.mark.parametrize('kind', ['offset128', 'means', 'clusters64', 'negative', 'wide'])
-def test_kmeans_centred_filters_bit_exact(ex, kind, ddt, mode, monkeypatch):
+def test_kmeans_centred_filters_bit_exact(ex, kind, ddt, mode):
   """Both bf16x3 filters rank centres by cc - 2 x.c' with c' = c - mean(c)
   (spx.hip k_kmeans_prep_b3): labels stay bit-identical to argmin(cdist) for
   data far from the origin (the case centring is for), second-iteration
@@ -881,11 +899,10 @@ def test_kmeans_centred_filters_bit_exact(ex, kind, ddt, mode, monkeypatch):
     pts = (g.standard_normal((20000, 128)) * 3 - 7).astype(np.float32)
     C = pts[g.choice(20000, 97, replace=False)].astype(np.float64)
   want = cdist(pts.astype(np.float64), C).astype(ddt).argmin(1)
-  monkeypatch.setenv('SPX_KMEANS_FILTER', mode)
   P = torch.as_tensor(pts).cuda()
   Cd = torch.as_tensor(np.ascontiguousarray(C)).cuda()
   fast = torch.empty(len(pts), dtype=torch.int64, device='cuda')
-  be.kmeans_assign(P, Cd, fast, dist_dtype=ddt)
+  _first_pass(be, mode, P, Cd, fast, ddt)
   np.testing.assert_array_equal(fast.cpu().numpy(), want)
 
 
@@ -1218,3 +1235,99 @@ def test_untraceable_mappers_gpu(ex, W):
   n1 = engine.HOST_MAPPER_CALLS[0]
   np.testing.assert_allclose(expr.map(x, lambda t: t * t + 1.0).glom(), a * a + 1.0, rtol=1e-15)
   assert engine.HOST_MAPPER_CALLS[0] == n1   # traceable: a generated kernel
+
+
+# ------------------------------------------ fused k-means step (one pass)
+def _step_case(kind):
+  g = np.random.default_rng(zlib.crc32(('step-' + kind).encode()))
+  if kind in ('uniform', 'ties32'):
+    return _assign_case(kind, np.float32)
+  if kind == 'd64':          # D = 64, K = 256, N not a multiple of 32
+    pts = g.random((50003, 64)).astype(np.float32); C = pts[:256].astype(np.float64)
+  elif kind == 'k20':        # one centre tile (NCT = 1), padding centres
+    pts = g.random((7001, 128)).astype(np.float32); C = g.random((20, 128))
+  elif kind == 'k50':        # NCT = 2
+    pts = g.random((9000, 64)).astype(np.float32); C = g.random((50, 64))
+  elif kind == 'k100':       # NCT = 4, tight clusters (many undecided rows)
+    ctr = g.random((100, 128)) * 2
+    pts = (ctr[g.integers(0, 100, 12000)] + 1e-3 * g.standard_normal((12000, 128))).astype(np.float32)
+    C = ctr + 1e-3 * g.standard_normal((100, 128))
+  elif kind == 'k1':
+    pts = g.random((3000, 64)).astype(np.float32); C = g.random((1, 64))
+  elif kind == 'nonfinite':
+    pts = g.random((8000, 128)).astype(np.float32); C = g.random((256, 128))
+    pts[5, 3] = np.nan; pts[9, 0] = np.inf; pts[4000, :] = -np.inf; pts[77, 1] = 7e4  # fp16 overflow
+  elif kind == 'tiny':       # fewer tiles than blocks
+    pts = g.random((45, 128)).astype(np.float32); C = pts[:7].astype(np.float64)
+  return np.ascontiguousarray(pts), np.ascontiguousarray(C)
+
+
+@pytest.mark.parametrize('ddt', [np.float64, np.float32])
+@pytest.mark.parametrize('kind', ['uniform', 'ties32', 'd64', 'k20', 'k50', 'k100', 'k1', 'nonfinite', 'tiny'])
+def test_kmeans_step_matches_two_passes(ex, kind, ddt):
+  """spx_kmeans_step (the fused screen + accumulation) against the two-pass
+  path: labels bit-identical to spx_kmeans_assign and to the all-exact kernel
+  (scipy cdist order, first index); counts exact; sums within the fp32 rule
+  of the fp64-exact sums (1e-5 of sum |x| per element: the rows the screen
+  decides are summed in fp32 chains flushed to fp64 every 255 tiles; the
+  reference sums in fp32, k_means_.py:67-89); repeated runs bit-identical;
+  zero_first=False adds."""
+  import torch
+  from spartan_amd import backend
+  be = backend.get()
+  pts, C = _step_case(kind)
+  N, D = pts.shape
+  K = C.shape[0]
+  P = torch.as_tensor(pts).cuda()
+  Cd = torch.as_tensor(C).cuda()
+  lab = torch.empty((N,), dtype=torch.int64, device='cuda')
+  sums = torch.full((K, D), 5.0, dtype=torch.float64, device='cuda')
+  cnt = torch.full((K,), 9, dtype=torch.int64, device='cuda')
+  be.kmeans_step(P, Cd, lab, sums, cnt, zero_first=True, dist_dtype=ddt)
+  want = torch.empty_like(lab)
+  be.kmeans_assign(P, Cd, want, dist_dtype=ddt)
+  exact = torch.empty_like(lab)
+  be.kmeans_assign(P, Cd, exact, exact_only=True, dist_dtype=ddt)
+  assert torch.equal(want, exact)
+  assert torch.equal(lab, exact)
+  L = lab.cpu().numpy()
+  ok = (L >= 0) & (L < K)
+  np.testing.assert_array_equal(cnt.cpu().numpy(), np.bincount(L[ok], minlength=K))
+  ws = np.zeros((K, D))
+  wa = np.zeros((K, D))
+  p64 = pts.astype(np.float64)
+  np.add.at(ws, L[ok], p64[ok])
+  np.add.at(wa, L[ok], np.abs(p64[ok]))
+  s1 = sums.cpu().numpy().copy()
+  fin = np.isfinite(ws)
+  assert np.all(np.abs(s1[fin] - ws[fin]) <= 1e-5 * wa[fin] + 1e-300)
+  assert np.array_equal(np.isnan(s1), np.isnan(ws))
+  be.kmeans_step(P, Cd, lab, sums, cnt, zero_first=True, dist_dtype=ddt)
+  np.testing.assert_array_equal(sums.cpu().numpy(), s1)   # deterministic
+  be.kmeans_step(P, Cd, lab, sums, cnt, zero_first=False, dist_dtype=ddt)
+  np.testing.assert_array_equal(cnt.cpu().numpy(), 2 * np.bincount(L[ok], minlength=K))
+  s2 = sums.cpu().numpy()
+  assert np.all(np.abs(s2[fin] - 2 * ws[fin]) <= 2e-5 * wa[fin] + 1e-300)
+
+
+def test_kmeans_step_windows(ex):
+  """Enough rows that every block passes several 255-tile windows (labels,
+  undecided bits and fp32 chains drained inside the tile loop): 3.2M x 64."""
+  import torch
+  from spartan_amd import backend
+  be = backend.get()
+  N, D, K = 3_200_000, 64, 256
+  P = torch.empty((N, D), dtype=torch.float32, device='cuda')
+  be.fill(P, backend.FILL_UNIFORM, 0.0, 1.0, 77, (0, 0), (N, D))
+  Cd = P[1000:1000 + K].to(torch.float64).contiguous()
+  lab = torch.empty((N,), dtype=torch.int64, device='cuda')
+  sums = torch.empty((K, D), dtype=torch.float64, device='cuda')
+  cnt = torch.empty((K,), dtype=torch.int64, device='cuda')
+  be.kmeans_step(P, Cd, lab, sums, cnt)
+  exact = torch.empty_like(lab)
+  be.kmeans_assign(P, Cd, exact, exact_only=True)
+  assert torch.equal(lab, exact)
+  ws = torch.zeros((K, D), dtype=torch.float64, device='cuda')
+  ws.index_add_(0, lab, P.to(torch.float64))
+  assert torch.equal(cnt, torch.bincount(lab, minlength=K))
+  torch.testing.assert_close(sums, ws, rtol=1e-6, atol=0)

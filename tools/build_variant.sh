@@ -1,6 +1,6 @@
 #!/bin/bash
 # Dev builds of libspx.so with extra -D flags into tools/bin/libspx_<name>.so
-# (timing splits / A-B variants for tools/km_modes.py); never the product build.
+# (timing splits / A-B variants for tools/km_step_once.py); never the product build.
 #   tools/build_variant.sh NAME [-DFLAG ...]
 set -e
 here=$(cd "$(dirname "$0")/.." && pwd)

@@ -34,6 +34,8 @@ struct Variant {
 
 #define V(T, BM, BN, BK, WM, WN, GM) \
   Variant<T>{#BM "x" #BN "x" #BK " w" #WM "x" #WN " g" #GM, Config<T, BM, BN, BK, WM, WN, GM>::launch}
+#define VS(T, BM, BN, BK, WM, WN, GM, SEG) \
+  Variant<T>{#BM "x" #BN "x" #BK " w" #WM "x" #WN " g" #GM " seg" #SEG, Config<T, BM, BN, BK, WM, WN, GM, SEG>::launch}
 
 template <typename T>
 __global__ void init(T* p, i64 n, unsigned seed) {
@@ -95,6 +97,14 @@ int main(int argc, char** argv) {
   i64 S = argc > 1 ? atoll(argv[1]) : 8192;
   int rounds = argc > 2 ? atoi(argv[2]) : 2;
   std::string which = argc > 3 ? argv[3] : "both";
+  if (which == "seg") {  // two-level accumulation (SEG K-tiles per fresh accumulator) against one chain
+    run<float>(S, rounds,
+               {V(float, 256, 128, 16, 4, 2, 8), VS(float, 256, 128, 16, 4, 2, 8, 16), VS(float, 256, 128, 16, 4, 2, 8, 32),
+                VS(float, 256, 128, 16, 4, 2, 8, 64), VS(float, 256, 128, 32, 4, 2, 8, 16), VS(float, 128, 128, 16, 2, 2, 8, 16),
+                VS(float, 256, 256, 16, 4, 4, 8, 16), VS(float, 128, 256, 16, 2, 4, 8, 16), VS(float, 256, 128, 16, 2, 4, 8, 16)},
+               157.3);
+    return 0;
+  }
   if (which != "f64") {
     run<float>(S, rounds,
                {V(float, 128, 128, 16, 2, 2, 0), V(float, 128, 128, 16, 2, 2, 8), V(float, 128, 128, 32, 2, 2, 8),

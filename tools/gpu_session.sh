@@ -16,12 +16,12 @@ export TMPDIR=/tmp
 step() {  # name, limit, command...
   local name=$1 lim=$2
   shift 2
-  echo "[$(date +%T)] $name" | tee -a $O/steps.log
+  echo "[$(date +%T)] $name" >> $O/steps.log
   timeout -k 10 $lim "$@"
   local rc=$?
-  echo "[$(date +%T)] $name rc=$rc" | tee -a $O/steps.log
+  echo "[$(date +%T)] $name rc=$rc" >> $O/steps.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
-    echo "stopping: $name ended with $rc" | tee -a $O/steps.log
+    echo "stopping: $name ended with $rc" >> $O/steps.log
     exit $rc
   fi
 }
@@ -30,6 +30,24 @@ for s in $STEPS; do
     tests)
       cd $R && step tests 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
         -p no:cacheprovider > $O/pytest.log 2>&1 ;;
+    kmtests)
+      cd $R && step kmtests 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+        -p no:cacheprovider -k "kmeans" > $O/kmtests.log 2>&1 ;;
+    kmbench)
+      cd $R && step kmbench 600 python3 bench.py --dot 0 --workloads kmeans --cpu-baseline 0 --steps 2 --warmup 1 \
+        > $O/kmbench.json 2> $O/kmbench.err ;;
+    kmtrace)
+      cd /tmp && step kmtrace 300 rocprofv3 --kernel-trace --stats -d $O/kmtrace -o p --output-format csv \
+        -- python3 $R/bench.py --dot 0 --workloads kmeans --cpu-baseline 0 --steps 2 --warmup 1 > $O/kmtrace.log 2>&1 ;;
+    kfspmc)
+      # counter passes over the fused k-means step (one group per pass: the box rejects overfull groups)
+      cd /tmp
+      step kfs_a 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE \
+        -d $O/kfs_a -o p --output-format csv -- python3 $R/tools/km_step_once.py 100000000 2 > $O/kfs_a.log 2>&1
+      step kfs_b 120 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_VALU_MFMA_BUSY_CYCLES SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE \
+        -d $O/kfs_b -o p --output-format csv -- python3 $R/tools/km_step_once.py 100000000 2 > $O/kfs_b.log 2>&1 ;;
+    gemmseg)
+      cd $R && step gemmseg 600 ./tools/bin/gemm_tune 32768 2 seg > $O/gemmseg.txt 2>&1 ;;
     bench)
       cd $R && step bench 600 python3 bench.py > $O/bench.json 2> $O/bench.err ;;
     trace2)
@@ -50,7 +68,7 @@ for s in $STEPS; do
         -- python3 $R/tools/km_iter.py 100000000 2 > $O/kmw.log 2>&1 ;;
     *)
       # anything else: a python script under tools/ with its arguments joined by ':'
-      cd $R && step "$s" 600 python3 ${s//:/ } > $O/$(basename ${s%%:*}).log 2>&1 ;;
+      cd $R && step "$s" 600 python3 ${s//:/ } > $O/$(echo "$s" | tr '/:' '__').log 2>&1 ;;
   esac
 done
 echo "[$(date +%T)] session done" | tee -a $O/steps.log
