@@ -749,6 +749,16 @@ class HipBackend:
                                  ctypes.c_void_p(counts.data_ptr()), 1 if zero_first else 0, self.stream()),
            'spx_bincount')
 
+  def kmeans_counters(self, D):
+    """Diagnostic (tests, tools): the four u32 counters of the last
+    spx_kmeans_assign / spx_kmeans_step workspace in the certified screens'
+    layout (K <= 256; spx.hip KmWs): [rows sent to the all-centre exact
+    kernel, candidate rows, rows left undecided by the bf16x3 pass, rows left
+    undecided by the fp16 screen]."""
+    import torch
+    off = (D * 256 * 4 + 15) // 16 * 16 + 256 * 8 + 32
+    return self._ws[off:off + 16].view(torch.int32).cpu().tolist()
+
   def _workspace(self, nbytes, device):
     """Grow-only scratch buffer on ``device`` (reuse is stream-ordered)."""
     import torch

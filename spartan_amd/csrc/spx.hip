@@ -2288,9 +2288,17 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fscreen(
     } else {
       *(kfs_h4*)hrow = (kfs_h4){hv[0], hv[1], hv[2], hv[3]};
     }
-    // the row's |x'|^2 over its 16 threads (one DPP row): only the bound reads it (1.001 slack)
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) p2 += __shfl_xor(p2, o, 64);
+    // the row's |x'|^2 over its 16 threads (one DPP row: quad_perm swaps,
+    // row_half_mirror, row_mirror -- VALU moves, no LDS round trip); only the
+    // bound reads it (1.001 slack)
+    auto dpp_add = [&](auto ctl) __attribute__((always_inline)) {
+      p2 += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, p2),
+                                                                   decltype(ctl)::value, 0xF, 0xF, false));
+    };
+    dpp_add(std::integral_constant<int, 0xB1>{});   // quad_perm [1, 0, 3, 2]
+    dpp_add(std::integral_constant<int, 0x4E>{});   // quad_perm [2, 3, 0, 1]
+    dpp_add(std::integral_constant<int, 0x141>{});  // row_half_mirror
+    dpp_add(std::integral_constant<int, 0x140>{});  // row_mirror
     if ((t & 15) == 0) p2s[b3 * 32 + srow] = p2;
   };
 
@@ -2324,10 +2332,15 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fscreen(
     // bound: xk0 / xk1 above), so the top-2 fold carries its argument along
     // (plain C on the fresh accumulators: MFMA -> VALU wait states; asm on the
     // tagged values: no canonicalisation of bit-built operands)
+    // (each element copied out first: __builtin_bit_cast of an ext-vector
+    // element lvalue reads element 0 whatever the index -- it made every tag
+    // carry acc[0], so no row was ever decided)
     float tv[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q)
-      tv[q] = __builtin_bit_cast(float, (__builtin_bit_cast(unsigned int, acc[q]) & ~15u) | (unsigned int)q);
+    for (int q = 0; q < 16; ++q) {
+      const float a = acc[q];
+      tv[q] = __builtin_bit_cast(float, (__builtin_bit_cast(unsigned int, a) & ~15u) | (unsigned int)q);
+    }
     float lo = ks_max(tv[0], tv[1]), sec = ks_med3(tv[0], tv[1], -INFINITY);
 #pragma unroll
     for (int q = 2; q < 16; q += 2) {
@@ -2339,7 +2352,15 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fscreen(
     const float lo2 = __shfl_xor(lo, 32, 64), sec2 = __shfl_xor(sec, 32, 64);
     const float b1 = ks_max(lo, lo2);
     const float b2 = ks_med3(lo, lo2, ks_max(sec, sec2));
-    const int ib = lo >= lo2 ? il : __shfl_xor(il, 32, 64);  // equal tagged values: undecided anyway
+    // (the partner's index read by every lane, outside the select: a
+    // bpermute under a branch reads 0 from the inactive partner)
+    const int ilp = __shfl_xor(il, 32, 64);
+    const int ib = lo >= lo2 ? il : ilp;  // equal tagged values: undecided anyway
+#ifdef KFS_DEBUG
+    if (bk == 0 && w == 0 && it == 3 && (lane == 0 || lane == 32))
+      printf("scr lane %d acc %g %g %g %g tv %g %g lo %g sec %g lo2 %g sec2 %g b1 %g b2 %g\n", lane, acc[0], acc[1],
+             acc[2], acc[3], tv[0], tv[1], lo, sec, lo2, sec2, b1, b2);
+#endif
     if (h == 0) {
       float* ev = exv + ((size_t)(it & 1) * W + w) * 64;
       ev[j] = b1;
@@ -2358,6 +2379,9 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fscreen(
       const float* ev = exv + ((size_t)(it & 1) * W + v) * 64;
       const float a = ev[j], as = ev[32 + j];
       const int ai = exi[((size_t)(it & 1) * W + v) * 32 + j];
+#ifdef KFS_DEBUG
+      if (bk == 0 && w == 0 && it == 3 && lane == 0) printf("dec v %d a %g as %g ai %d\n", v, a, as, ai);
+#endif
       b2 = __builtin_amdgcn_fmed3f(b1, a, fmaxf(b2, as));
       ib = a > b1 ? ai : ib;  // strict: the lower centre index keeps a tie (undecided anyway)
       b1 = fmaxf(b1, a);
@@ -2369,6 +2393,11 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fscreen(
     const i64 row = tl * 32 + j;
     const bool live = it < nit && h == 0 && row < N;  // it >= nit: a ghost iteration
     const bool dec = fin && b1 - b2 > 1.0001f * e;
+#ifdef KFS_DEBUG
+    if (bk == 0 && w == 0 && it == 3 && lane < 4)
+      printf("kfs lane %d b1 %g b2 %g e %g p2 %g pn %g fin %d dec %d ib %d kq %g %g %g cok %d\n", lane, b1, b2, e, p2f,
+             pn, (int)fin, (int)dec, ib, kq[0], kq[1], kq[2], (int)cok);
+#endif
     // labels and the undecided bits go to the window buffers in LDS; no
     // global store inside the tile loop (drain writes them)
     if (w == 0 && it < nit) {

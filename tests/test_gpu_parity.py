@@ -1284,6 +1284,11 @@ def test_kmeans_step_matches_two_passes(ex, kind, ddt):
   sums = torch.full((K, D), 5.0, dtype=torch.float64, device='cuda')
   cnt = torch.full((K,), 9, dtype=torch.int64, device='cuda')
   be.kmeans_step(P, Cd, lab, sums, cnt, zero_first=True, dist_dtype=ddt)
+  if kind in ('uniform', 'd64'):
+    # the fused screen does decide: well-separated rows never reach the list
+    # passes (a screen that decides nothing is still exact, only slow)
+    und = be.kmeans_counters(D)[3]
+    assert und <= 0.2 * N, 'fused screen left %d of %d rows undecided' % (und, N)
   want = torch.empty_like(lab)
   be.kmeans_assign(P, Cd, want, dist_dtype=ddt)
   exact = torch.empty_like(lab)
