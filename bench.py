@@ -428,8 +428,7 @@ def bench_kmeans_api(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
 
 
 def check_lreg(Xe, Ye, w, expr, comm, chunk=1 << 23):
-  """The fused gradient sum(x * (dot(x, w) - y), axis=0) at the final w
-  against a chunked fp64 restatement over the local row strips (torch fp64
+  """The fused gradient sum(x * (dot(x, w) - y), axis=0) at w against a chunked fp64 restatement over the local row strips (torch fp64
   on the device, a checker only), all-reduced over ranks: per column within
   1e-5 of sum_i |x_ij| |r_i| (the condition of the sum)."""
   import torch
@@ -470,7 +469,11 @@ def bench_lreg(npts, ctx, expr, comm, sync, D=64, iters=30):
   sync()
   comm.barrier()
   el = comm.max_over_ranks(time.perf_counter() - t0) / iters
-  checked = check_lreg(Xe, Ye, w_end, expr, comm)
+  # checked at the starting w: the reference's step size (sgd.py:14, alpha =
+  # 1e-6) diverges at this N, so after 30 steps w and the gradient have left
+  # the fp32 range; the replayed plan and kernel are the ones timed
+  checked = check_lreg(Xe, Ye, w, expr, comm)
+  del w_end
   n = npts * ctx.world_size
   nbytes = 4.0 * n * D + 4.0 * n   # one pass: X and y read once (DotReduceFusion)
   out = {'ms_per_iter': round(el * 1e3, 3), 'algorithmic_GBps': round(nbytes / el / 1e9, 1),

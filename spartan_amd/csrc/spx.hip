@@ -2146,68 +2146,86 @@ static void ks_launch_n(int nct, hipStream_t s, i64 N, i64 D, const float* P, i6
 // the points a second time (51 GB at cfg3).  Here the roles are swapped
 // (B-stationary): wave w < NCT keeps ITS 32 centres in registers -- the MFMA A
 // operand, fp16(c') exactly as the screen stages them, plus the -cc/2 pieces
-// -- and every point tile passes through all of the block's waves from LDS.
-// Per 32-point tile:
-//   stage     512 threads convert the tile (16 KiB fp32, register prefetch
-//             ring KFS_R tiles deep) to x' = fl(x - mu) and fp16(x') in LDS,
-//             |x'|^2 per row, and keep the raw fp32 rows in LDS;
-//   screen    wave w: 8 fp16 MFMAs + 1 bf16 MFMA (-cc/2) give the 32 x 32
-//             block S - cc/2 = -a''/2 (rows = its centres, columns = the
-//             points), a per-lane top-2 over the lane's 16 centres, one
-//             half-swap, and (b1, b2, index) per point into LDS;
-//   decide    every wave reads the NCT candidates per point: the certified
-//             rule of the screen (b1 - b2 > e(|x'|), the same bound kq and
-//             the same finiteness checks as k_kmeans_filter_as MODE 1, whose
-//             arithmetic this is with A and B exchanged);
-//   accumulate wave w adds the decided rows whose centre it owns from the
-//             fp32 rows in LDS into fp32 register sums (32 centres x D / 64
-//             dims per lane) in point order.
-// Every KFS_FW tiles (a window) the labels / undecided bits buffered in LDS go
-// to global memory and every fp32 chain is added to the block's private fp64
-// partial (no-return fp64 atomics, one writer per address, so program order
-// fixes the result: deterministic); a chain therefore spans at most the rows
-// one block sees of one centre in one window (~32 at cfg3).  Keeping every
-// global store out of the tile loop lets the prefetch ring stay in flight
-// across the barriers (a pending store would make the compiler wait
-// vmcnt(0) at each staging).
-// One barrier per tile: tile t's decision / accumulation, tile t+1's screen
-// and tile t+2's staging share an iteration (fp32 rows triple-buffered, fp16
-// rows and the exchange double-buffered).  Undecided rows (near-ties,
-// non-finite or fp16-overflowing rows) are not added: they go through the
-// list passes of spx_kmeans_assign and a gathered accumulation afterwards.
-typedef _Float16 kfs_h4 __attribute__((ext_vector_type(4)));
+// -- and every unit of 64 points (two 32-point MFMA tiles) passes through all
+// of the block's waves from LDS.  One loop iteration per unit, two barriers:
+//   phase 1   screen (waves < NCT): two independent chains of 8 fp16 MFMAs +
+//             1 bf16 MFMA (-cc/2) give the 32 x 32 blocks S - cc/2 = -a''/2
+//             of the unit's two tiles (rows = the wave's centres, columns =
+//             points); a per-lane top-2 over the lane's 16 centres, ONE
+//             half-swap that leaves lane (j, h) with tile h's point j, and
+//             (b1, b2, index) per point into LDS;
+//             accumulate (waves < NCT) the previous unit's decided rows whose
+//             centre the wave owns, from the fp32 rows in LDS, into fp32
+//             register sums (32 centres x D / 64 dims per lane), in point
+//             order, KFS_AR rows' LDS reads in flight at a time;
+//   phase 2   decide: wave w takes rows 8w .. 8w + 7, one lane per (row,
+//             centre wave): the top-2 over the NCT candidates by three DPP
+//             exchanges, then the certified rule of the screen (b1 - b2 >
+//             e(|x'|), the same bound kq and finiteness checks as
+//             k_kmeans_filter_as MODE 1, whose arithmetic this is with A and B
+//             exchanged) -- every row decided exactly once;
+//             stage the next unit: 512 threads convert it (32 KiB fp32, a
+//             register prefetch ring KFS_R units deep) to x' = fl(x - mu) and
+//             fp16(x') in LDS, |x'|^2 per row, and keep the raw fp32 rows.
+// Every KFS_FW units (a window) the labels / undecided flags buffered in LDS
+// go to global memory and every fp32 chain is added to the block's private
+// fp64 partial (no-return fp64 atomics, one writer per address, so program
+// order fixes the result: deterministic); a chain therefore spans at most the
+// rows one block sees of one centre in one window.  Keeping every global
+// store out of the unit loop lets the prefetch ring stay in flight across the
+// barriers (a pending store makes the compiler wait vmcnt(0) at each staging).
+// Undecided rows (near-ties, non-finite or fp16-overflowing rows) are not
+// added: they go through the list passes of spx_kmeans_assign and a gathered
+// accumulation afterwards.
 typedef float kfs_f2 __attribute__((ext_vector_type(2)));
 constexpr int KFS_WAVES = 8;
+constexpr int KFS_U = 64;  // rows per unit (two 32-row MFMA tiles)
 #ifndef KFS_RING
-#define KFS_RING 6  // prefetch ring depth in tiles (registers, 8 per tile): the loads of tiles it+2 .. it+KFS_R+1 fly during iteration it
+#define KFS_RING 2  // prefetch ring depth in units (D / 8 floats per thread and unit, in registers)
 #endif
 constexpr int KFS_R = KFS_RING;
-constexpr int KFS_NB = 3;      // fp32 row buffers in LDS (staged, waiting, being accumulated)
-constexpr int KFS_FW = 252;    // tiles per window (a multiple of KFS_R): labels / bits buffered in LDS, fp32 chains flushed per window
-static_assert(KFS_R % KFS_NB == 0 && KFS_FW % KFS_R == 0, "buffer / drain indices must be compile-time in the unrolled ring");
+constexpr int KFS_UN = KFS_R % 2 == 0 ? KFS_R : 2 * KFS_R;  // unroll: ring slot and fp32 buffer compile-time
+constexpr int KFS_FW = 120;
+#ifndef KFS_AR
+#define KFS_AR 8  // accumulated rows per round (their LDS reads issued together)
+#endif
+// exchange strides per screening wave: +64 B / +32 B so the 8 lanes of a
+// decide row group (one per screening wave) read 8 different bank groups
+constexpr int KFS_EXV_S = 2 * KFS_U + 16, KFS_EXI_S = KFS_U + 8;  // units per window (a multiple of KFS_UN): labels / flags in LDS, fp32 chains flushed
+static_assert(KFS_FW % KFS_UN == 0, "the drain points must fall on the unrolled body's first copy");
 __host__ __device__ constexpr int kfs_rs(int D) { return 2 * D + 16; }  // fp16 row stride: +16 B keeps ds_read_b128 conflict-free
 static size_t kfs_lds_bytes(int D) {
-  return (size_t)KFS_NB * 32 * D * 4 + (size_t)2 * 32 * kfs_rs(D) + KFS_NB * 32 * 4 + 2 * KFS_WAVES * 32 * 12 +
-         (size_t)D * 4 + 2 * KFS_FW * 4 + 2 * KFS_FW * 32;
+  return (size_t)2 * KFS_U * D * 4 + (size_t)KFS_U * kfs_rs(D) + 2 * KFS_U * 4 + (size_t)KFS_WAVES * (KFS_EXV_S + KFS_EXI_S) * 4 +
+         (size_t)D * 4 + KFS_U * 4 + (size_t)2 * KFS_FW * KFS_U * 2;
 }
 
-template <int KS, int NCT, bool ACC>
+template <int CTL>
+__device__ __forceinline__ float kfs_dppf(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTL, 0xF, 0xF, false));
+}
+template <int CTL>
+__device__ __forceinline__ int kfs_dppi(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTL, 0xF, 0xF, false);
+}
+
+template <int KS, int NCT>
 __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fscreen(
     i64 N, i64 K, const float* __restrict__ P, i64 ldp, const __bf16* __restrict__ CBh,
     const __bf16* __restrict__ CBl, const float* __restrict__ cnf2, const double* cmax_p,
     const float* __restrict__ muf, i64* __restrict__ labels, unsigned long long* __restrict__ und_mask,
     double* __restrict__ psum, unsigned long long* __restrict__ pcnt) {
-  constexpr int D = 16 * KS, EPT = KS, DPL = D / 64, RS = kfs_rs(D), W = KFS_WAVES;
-  static_assert(EPT % 4 == 0 && (DPL == 1 || DPL == 2), "D = 64 or 128");
+  constexpr int D = 16 * KS, EPT = D / 8, DPL = D / 64, RS = kfs_rs(D), W = KFS_WAVES, U = KFS_U;
+  static_assert(EPT % 8 == 0 && (DPL == 1 || DPL == 2), "D = 64 or 128");
   extern __shared__ __attribute__((aligned(16))) unsigned char kfs_lds[];
-  float* xs = (float*)kfs_lds;                                     // [KFS_NB][32][D] raw fp32 rows
-  unsigned char* xh = kfs_lds + (size_t)KFS_NB * 32 * D * 4;       // [2][32][RS] fp16 x'
-  float* p2s = (float*)(xh + 2 * 32 * RS);                         // [KFS_NB][32] |x'|^2
-  float* exv = p2s + KFS_NB * 32;                                  // [2][W][2][32] (b1, b2)
-  int* exi = (int*)(exv + 2 * W * 2 * 32);                         // [2][W][32] best centre
-  float* mus = (float*)(exi + 2 * W * 32);                         // [D] centre mean
-  unsigned int* und32 = (unsigned int*)(mus + D);                  // [2 KFS_FW] undecided bits per tile
-  unsigned char* lab8 = (unsigned char*)(und32 + 2 * KFS_FW);      // [2 KFS_FW][32] labels (K <= 256)
+  float* xs = (float*)kfs_lds;                                // [2][U][D] raw fp32 rows
+  unsigned char* xh = kfs_lds + (size_t)2 * U * D * 4;        // [U][RS] fp16 x'
+  float* p2s = (float*)(xh + (size_t)U * RS);                 // [2][U] |x'|^2
+  float* exv = p2s + 2 * U;                                   // [W][KFS_EXV_S] (b1, b2) per row
+  int* exi = (int*)(exv + W * KFS_EXV_S);                     // [W][KFS_EXI_S] best centre
+  float* mus = (float*)(exi + W * KFS_EXI_S);                 // [D] centre mean
+  int* dl = (int*)(mus + D);                                  // [U] decided label, -1: not decided
+  unsigned char* lab8 = (unsigned char*)(dl + U);             // [2 KFS_FW][U] labels (K <= 256)
+  unsigned char* und8 = lab8 + 2 * KFS_FW * U;                // [2 KFS_FW][U] undecided flags
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, j = lane & 31, h = lane >> 5;
   for (int i = t; i < D; i += W * 64) mus[i] = muf[i];
 
@@ -2254,52 +2272,49 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fscreen(
   const bool cok = cmax * cmax < 1e36 && mun * cmax < 1e36 && cmax < 3.0e4 && dcmax == dcmax;
   const float pn_lim = (float)(cmax > 0.0 ? 1e36 / cmax : 1e36);
 
-  const i64 ntiles = (N + 31) / 32, G = gridDim.x, bk = blockIdx.x;
-  const i64 nit = bk < ntiles ? (ntiles - 1 - bk) / G + 1 : 0;
-  // this thread's slice of a tile: row t / 16, EPT columns from (t % 16) EPT
-  const int srow = t >> 4, scol = (t & 15) * EPT;
+  const int G = gridDim.x, bk = blockIdx.x;
+  const i64 nunits = (N + U - 1) / U, ntiles = (N + 31) / 32;
+  const int nit = bk < nunits ? (int)((nunits - 1 - bk) / G + 1) : 0;
+  // this thread's slice of a unit: row t / 8, EPT columns from (t % 8) EPT
+  const int srow = t >> 3, scol = (t & 7) * EPT;
   kb_f4 ring[KFS_R][EPT / 4];
-  auto load = [&](kb_f4 (&r)[EPT / 4], i64 it) __attribute__((always_inline)) {  // clamped: always a valid address
-    const i64 tl = bk + (it < nit ? it : nit - 1) * G;
-    i64 row = tl * 32 + srow;
+  auto load = [&](kb_f4 (&r)[EPT / 4], int it) __attribute__((always_inline)) {  // clamped: always a valid address
+    const i64 un = bk + (i64)(it < nit ? it : nit - 1) * G;
+    i64 row = un * U + srow;
     row = row < N ? row : N - 1;
     const float* p = P + row * ldp + scol;
 #pragma unroll
     for (int q = 0; q < EPT / 4; ++q) r[q] = *(const kb_f4*)(p + 4 * q);
   };
-  auto stage = [&](const kb_f4 (&r)[EPT / 4], i64 it, int b3) __attribute__((always_inline)) {  // ring slot -> LDS (buffers of iteration it)
-    float* xrow = xs + ((size_t)b3 * 32 + srow) * D + scol;
+  auto stage = [&](const kb_f4 (&r)[EPT / 4], int b) __attribute__((always_inline)) {  // ring slot -> LDS buffer b
+    float* xrow = xs + ((size_t)b * U + srow) * D + scol;
     _Float16 hv[EPT];
-    float p2 = 0.f;
+    kfs_f2 p2v = (kfs_f2){0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < EPT / 4; ++q) {
       *(kb_f4*)(xrow + 4 * q) = r[q];
       const kb_f4 mu4 = *(const kb_f4*)(mus + scol + 4 * q);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float x = r[q][e] - mu4[e];  // x' = fl(x - mu), as the screen
-        p2 = __builtin_fmaf(x, x, p2);
-        hv[4 * q + e] = (_Float16)x;
+      for (int e = 0; e < 4; e += 2) {
+        // x' = fl(x - mu), as the screen (packed fp32: v_pk_add / v_pk_fma)
+        const kfs_f2 x = (kfs_f2){r[q][e], r[q][e + 1]} - (kfs_f2){mu4[e], mu4[e + 1]};
+        p2v = __builtin_elementwise_fma(x, x, p2v);
+        hv[4 * q + e] = (_Float16)x[0];
+        hv[4 * q + e + 1] = (_Float16)x[1];
       }
     }
-    unsigned char* hrow = xh + ((size_t)(it & 1) * 32 + srow) * RS + 2 * scol;
-    if constexpr (EPT == 8) {
-      *(kh_f8*)hrow = (kh_f8){hv[0], hv[1], hv[2], hv[3], hv[4], hv[5], hv[6], hv[7]};
-    } else {
-      *(kfs_h4*)hrow = (kfs_h4){hv[0], hv[1], hv[2], hv[3]};
-    }
-    // the row's |x'|^2 over its 16 threads (one DPP row: quad_perm swaps,
-    // row_half_mirror, row_mirror -- VALU moves, no LDS round trip); only the
-    // bound reads it (1.001 slack)
-    auto dpp_add = [&](auto ctl) __attribute__((always_inline)) {
-      p2 += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, p2),
-                                                                   decltype(ctl)::value, 0xF, 0xF, false));
-    };
-    dpp_add(std::integral_constant<int, 0xB1>{});   // quad_perm [1, 0, 3, 2]
-    dpp_add(std::integral_constant<int, 0x4E>{});   // quad_perm [2, 3, 0, 1]
-    dpp_add(std::integral_constant<int, 0x141>{});  // row_half_mirror
-    dpp_add(std::integral_constant<int, 0x140>{});  // row_mirror
-    if ((t & 15) == 0) p2s[b3 * 32 + srow] = p2;
+    unsigned char* hrow = xh + (size_t)srow * RS + 2 * scol;
+#pragma unroll
+    for (int g = 0; g < EPT / 8; ++g)
+      *(kh_f8*)(hrow + 16 * g) = (kh_f8){hv[8 * g], hv[8 * g + 1], hv[8 * g + 2], hv[8 * g + 3],
+                                         hv[8 * g + 4], hv[8 * g + 5], hv[8 * g + 6], hv[8 * g + 7]};
+    // the row's |x'|^2 over its 8 threads (quad_perm swaps, row_half_mirror:
+    // VALU moves, no LDS round trip); only the bound reads it (1.001 slack)
+    float p2 = p2v[0] + p2v[1];
+    p2 += kfs_dppf<0xB1>(p2);
+    p2 += kfs_dppf<0x4E>(p2);
+    p2 += kfs_dppf<0x141>(p2);
+    if ((t & 7) == 0) p2s[b * U + srow] = p2;
   };
 
   // fp32 sums of this wave's 32 centres: lane = DPL dims, register = centre
@@ -2313,227 +2328,253 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fscreen(
       unsafeAtomicAdd(pbase + (i64)cl * D, (double)s0[cl]);
       if constexpr (DPL == 2) unsafeAtomicAdd(pbase + (i64)cl * D + 1, (double)s1[cl]);
     }
-    s0[cl] = 0.f;
-    s1[cl] = 0.f;
   };
 
-  // screen of iteration it's tile (waves < NCT): top-2 + best centre per point into the exchange
-  auto screen = [&](i64 it) __attribute__((always_inline)) {
-    const unsigned char* bp = xh + ((size_t)(it & 1) * 32 + j) * RS + 16 * h;
-    kb_acc acc = (kb_acc){};
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const kh_f8 bv = *(const kh_f8*)(bp + 32 * ks);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[ks], bv, acc, 0, 0, 0);
-    }
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ccp, ones, acc, 0, 0, 0);
-    // acc[q] = S - cc/2 = -a''/2 of point j and centre i(q) = (q & 3) + 8 (q >> 2) + 4 h,
-    // tagged with q in its 4 low mantissa bits (<= 15 ulp, priced in the
-    // bound: xk0 / xk1 above), so the top-2 fold carries its argument along
-    // (plain C on the fresh accumulators: MFMA -> VALU wait states; asm on the
-    // tagged values: no canonicalisation of bit-built operands)
-    // (each element copied out first: __builtin_bit_cast of an ext-vector
-    // element lvalue reads element 0 whatever the index -- it made every tag
-    // carry acc[0], so no row was ever decided)
+  // top-2 of one accumulator block's 16 values per lane, each tagged with
+  // its register q in the 4 low mantissa bits (<= 15 ulp, priced in the
+  // bound: xk0 / xk1 above) so the fold carries its argument along.  Every
+  // element is copied out first: __builtin_bit_cast of an ext-vector element
+  // lvalue reads element 0 whatever the index.
+  auto fold16 = [&](const kb_acc& acc, float& lo, float& sec, int& il) __attribute__((always_inline)) {
     float tv[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const float a = acc[q];
       tv[q] = __builtin_bit_cast(float, (__builtin_bit_cast(unsigned int, a) & ~15u) | (unsigned int)q);
     }
-    float lo = ks_max(tv[0], tv[1]), sec = ks_med3(tv[0], tv[1], -INFINITY);
+    lo = ks_max(tv[0], tv[1]);
+    sec = ks_med3(tv[0], tv[1], -INFINITY);
 #pragma unroll
     for (int q = 2; q < 16; q += 2) {
       sec = ks_max(sec, ks_med3(lo, tv[q], tv[q + 1]));
       lo = ks_max3(lo, tv[q], tv[q + 1]);
     }
     const unsigned int qb = __builtin_bit_cast(unsigned int, lo) & 15u;
-    const int il = 32 * w + (int)((qb & 3) + 8 * (qb >> 2)) + 4 * h;
-    const float lo2 = __shfl_xor(lo, 32, 64), sec2 = __shfl_xor(sec, 32, 64);
-    const float b1 = ks_max(lo, lo2);
-    const float b2 = ks_med3(lo, lo2, ks_max(sec, sec2));
-    // (the partner's index read by every lane, outside the select: a
-    // bpermute under a branch reads 0 from the inactive partner)
-    const int ilp = __shfl_xor(il, 32, 64);
-    const int ib = lo >= lo2 ? il : ilp;  // equal tagged values: undecided anyway
-#ifdef KFS_DEBUG
-    if (bk == 0 && w == 0 && it == 3 && (lane == 0 || lane == 32))
-      printf("scr lane %d acc %g %g %g %g tv %g %g lo %g sec %g lo2 %g sec2 %g b1 %g b2 %g\n", lane, acc[0], acc[1],
-             acc[2], acc[3], tv[0], tv[1], lo, sec, lo2, sec2, b1, b2);
-#endif
-    if (h == 0) {
-      float* ev = exv + ((size_t)(it & 1) * W + w) * 64;
-      ev[j] = b1;
-      ev[32 + j] = b2;
-      exi[((size_t)(it & 1) * W + w) * 32 + j] = ib;
-    }
+    il = 32 * w + (int)((qb & 3) + 8 * (qb >> 2)) + 4 * h;  // acc[q] is centre (q & 3) + 8 (q >> 2) + 4 h
   };
 
-  // decision + accumulation of iteration it's tile
-  auto decide = [&](i64 it, int b3) __attribute__((always_inline)) {
-    const i64 tl = bk + it * G;
+  // phase 1: the screen of the unit in xh (waves < NCT): (b1, b2, best) per
+  // point.  Split in two so the accumulation of the previous unit (VALU /
+  // LDS) runs while the matrix pipe works through the two MFMA chains.
+  auto screen_mfma = [&](kb_acc& a0, kb_acc& a1) __attribute__((always_inline)) {
+    const unsigned char* bpa = xh + (size_t)j * RS + 16 * h;
+    const unsigned char* bpb = bpa + (size_t)32 * RS;
+    a0 = (kb_acc){};
+    a1 = (kb_acc){};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const kh_f8 va = *(const kh_f8*)(bpa + 32 * ks);
+      const kh_f8 vb = *(const kh_f8*)(bpb + 32 * ks);
+      a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[ks], va, a0, 0, 0, 0);
+      a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[ks], vb, a1, 0, 0, 0);
+    }
+    a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ccp, ones, a0, 0, 0, 0);
+    a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ccp, ones, a1, 0, 0, 0);
+  };
+  auto screen_fold = [&](const kb_acc& a0, const kb_acc& a1) __attribute__((always_inline)) {
+    float loa, seca, lob, secb;
+    int ila, ilb;
+    fold16(a0, loa, seca, ila);
+    fold16(a1, lob, secb, ilb);
+    // half-swap: lane (j, 0) keeps tile 0's point j and receives the other
+    // half's candidates for it; lane (j, 1) the same for tile 1 (every lane
+    // takes part in the exchange: a bpermute under a branch reads 0 from an
+    // inactive partner)
+    const float sl = h ? loa : lob, ss = h ? seca : secb;
+    const int si = h ? ila : ilb;
+    const float rl = __shfl_xor(sl, 32, 64), rs = __shfl_xor(ss, 32, 64);
+    const int ri = __shfl_xor(si, 32, 64);
+    const float ml = h ? lob : loa, ms = h ? secb : seca;
+    const int mi = h ? ilb : ila;
+    const float b1 = ks_max(ml, rl);
+    const float b2 = ks_med3(ml, rl, ks_max(ms, rs));
+    const int ib = ml >= rl ? mi : ri;  // equal tagged values: undecided anyway
+    // lane (j, h) holds unit row 32 h + j = lane
+    *(kfs_f2*)(exv + w * KFS_EXV_S + 2 * lane) = (kfs_f2){b1, b2};
+    exi[w * KFS_EXI_S + lane] = ib;
+  };
+
+  // phase 2: decision of unit it (its |x'|^2 in p2s[b]); wave w: rows 8 w .. + 7
+  auto decide = [&](int it, int b) __attribute__((always_inline)) {
+    const int r = lane >> 3, v = lane & 7, row = 8 * w + r;
     float b1 = -INFINITY, b2 = -INFINITY;
     int ib = 0;
-#pragma unroll
-    for (int v = 0; v < NCT; ++v) {
-      const float* ev = exv + ((size_t)(it & 1) * W + v) * 64;
-      const float a = ev[j], as = ev[32 + j];
-      const int ai = exi[((size_t)(it & 1) * W + v) * 32 + j];
-#ifdef KFS_DEBUG
-      if (bk == 0 && w == 0 && it == 3 && lane == 0) printf("dec v %d a %g as %g ai %d\n", v, a, as, ai);
-#endif
-      b2 = __builtin_amdgcn_fmed3f(b1, a, fmaxf(b2, as));
-      ib = a > b1 ? ai : ib;  // strict: the lower centre index keeps a tie (undecided anyway)
-      b1 = fmaxf(b1, a);
+    if (v < NCT) {
+      const kfs_f2 e2 = *(const kfs_f2*)(exv + v * KFS_EXV_S + 2 * row);
+      b1 = e2[0];
+      b2 = e2[1];
+      ib = exi[v * KFS_EXI_S + row];
     }
-    const float p2f = p2s[b3 * 32 + j];
+    // top-2 over the row's 8 lanes: xor 1, xor 2 (quad_perm), then the
+    // other quad (row_half_mirror); equal tagged values leave b2 = b1
+    // (undecided), so which index survives a tie does not matter
+    auto merge = [&](auto ctl) __attribute__((always_inline)) {
+      constexpr int C = decltype(ctl)::value;
+      const float pb1 = kfs_dppf<C>(b1), pb2 = kfs_dppf<C>(b2);
+      const int pib = kfs_dppi<C>(ib);
+      b2 = ks_med3(b1, pb1, ks_max(b2, pb2));
+      ib = pb1 > b1 ? pib : ib;
+      b1 = ks_max(b1, pb1);
+    };
+    merge(std::integral_constant<int, 0xB1>{});
+    merge(std::integral_constant<int, 0x4E>{});
+    merge(std::integral_constant<int, 0x141>{});
+    const float p2f = p2s[b * U + row];
     const float pn = __builtin_amdgcn_sqrtf(__builtin_fmaf(p2f, 1.001f, 1e-37f)) * 1.0001f;
     const float e = __builtin_fmaf(__builtin_fmaf(kq[2], pn, kq[1]), pn, kq[0]) * 1.0001f;
     const bool fin = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim && isfinite(b1) && isfinite(b2);
-    const i64 row = tl * 32 + j;
-    const bool live = it < nit && h == 0 && row < N;  // it >= nit: a ghost iteration
+    const i64 grow = (bk + (i64)it * G) * U + row;
+    const bool live = it < nit && grow < N;  // it >= nit: a ghost iteration
     const bool dec = fin && b1 - b2 > 1.0001f * e;
-#ifdef KFS_DEBUG
-    if (bk == 0 && w == 0 && it == 3 && lane < 4)
-      printf("kfs lane %d b1 %g b2 %g e %g p2 %g pn %g fin %d dec %d ib %d kq %g %g %g cok %d\n", lane, b1, b2, e, p2f,
-             pn, (int)fin, (int)dec, ib, kq[0], kq[1], kq[2], (int)cok);
-#endif
-    // labels and the undecided bits go to the window buffers in LDS; no
-    // global store inside the tile loop (drain writes them)
-    if (w == 0 && it < nit) {
-      const int u = (int)(it % (2 * KFS_FW));
-      if (h == 0) lab8[u * 32 + j] = (unsigned char)ib;
-      const unsigned long long und = __ballot(live && !dec);
-      if (lane == 0) und32[u] = (unsigned int)und;  // bit j <-> row 32 tl + j
+    if (v == 0) {
+      dl[row] = live && dec ? ib : -1;
+      // labels and the undecided flags go to the window buffers in LDS; no
+      // global store inside the unit loop (drain writes them)
+      if (it < nit) {
+        const int u = it % (2 * KFS_FW);
+        lab8[u * U + row] = (unsigned char)ib;
+        und8[u * U + row] = live && !dec ? 1 : 0;
+      }
     }
-    if constexpr (ACC) {
-      if (w < NCT) {
-        unsigned long long m = __ballot(live && dec && (ib >> 5) == w);
-        const float* xb = xs + (size_t)b3 * 32 * D + DPL * lane;
-        while (m) {  // wave-uniform, in point order; two rows per step (both reads in flight)
-          const int p = __builtin_ctzll(m);
-          m &= m - 1;
-          const bool two = m != 0;
-          const int p2 = two ? __builtin_ctzll(m) : p;
-          if (two) m &= m - 1;
-          const int cl = __builtin_amdgcn_readlane(ib, p) & 31;
-          const int cl2 = __builtin_amdgcn_readlane(ib, p2) & 31;
+  };
+
+  // phase 1: the decided rows of the unit in xs[b] whose centre this wave
+  // owns (waves < NCT), in point order, KFS_AR rows' reads in flight per round
+  auto accumulate = [&](int b) __attribute__((always_inline)) {
+    const int d = dl[lane];
+    unsigned long long m = __ballot(d >= 0 && (d >> 5) == w);
+    const float* xb = xs + (size_t)b * U * D + DPL * lane;
+    while (m) {  // wave-uniform
+      int p[KFS_AR];
+      bool ok[KFS_AR];
+      p[0] = __builtin_ctzll(m);
+      ok[0] = true;
+      m &= m - 1;
+#pragma unroll
+      for (int k = 1; k < KFS_AR; ++k) {
+        ok[k] = m != 0;
+        p[k] = ok[k] ? __builtin_ctzll(m) : p[0];
+        if (ok[k]) m &= m - 1;
+      }
+      kfs_f2 x2[KFS_AR];
+      float x1[KFS_AR];
+#pragma unroll
+      for (int k = 0; k < KFS_AR; ++k) {
+        if constexpr (DPL == 2) x2[k] = *(const kfs_f2*)(xb + p[k] * D);
+        else x1[k] = xb[p[k] * D];
+      }
+#pragma unroll
+      for (int k = 0; k < KFS_AR; ++k) {
+        if (ok[k]) {
+          const int cl = __builtin_amdgcn_readlane(d, p[k]) & 31;
           if constexpr (DPL == 2) {
-            const kfs_f2 x = *(const kfs_f2*)(xb + p * D);
-            const kfs_f2 x2 = *(const kfs_f2*)(xb + p2 * D);
-            s0[cl] += x[0];
-            s1[cl] += x[1];
-            if (two) {
-              s0[cl2] += x2[0];
-              s1[cl2] += x2[1];
-            }
+            s0[cl] += x2[k][0];
+            s1[cl] += x2[k][1];
           } else {
-            const float x = xb[p * D], x2 = xb[p2 * D];
-            s0[cl] += x;
-            if (two) s0[cl2] += x2;
+            s0[cl] += x1[k];
           }
-          cnt += (lane == cl ? 1u : 0u) + (two && lane == cl2 ? 1u : 0u);
+          cnt += lane == cl ? 1u : 0u;
         }
       }
     }
   };
-  // window k (tiles k KFS_FW .. + KFS_FW) to global memory: labels of the
-  // decided rows, the undecided bits, and (ACC) every fp32 chain into the
-  // block's fp64 partial; then wait for the stores, so that no store is
-  // pending while the prefetch ring is in flight (a pending store makes the
-  // compiler drain the ring at every staging: vmcnt(0))
-  auto drain = [&](i64 k) __attribute__((always_inline)) {
-    const i64 i0 = k * KFS_FW, i1 = i0 + KFS_FW < nit ? i0 + KFS_FW : nit;
-    for (i64 ip = i0 + w; ip < i1; ip += W) {
-      const i64 tl = bk + ip * G;
-      const int u = (int)(ip % (2 * KFS_FW));
-      const unsigned int und = und32[u];
-      const i64 row = tl * 32 + j;
-      if (h == 0 && row < N && !((und >> j) & 1u)) labels[row] = lab8[u * 32 + j];
-      if (lane == 0) und_mask[tl] = und;
-    }
-    if constexpr (ACC) {
-      if (w < NCT) {
-#pragma unroll 1
-        for (int c = 0; c < 32; ++c) flush(c);  // rolled: the 64 converted sums are not all held at once
+
+  // window k (units k KFS_FW .. + KFS_FW) to global memory: labels of the
+  // decided rows, the undecided bits (two 32-row tiles per unit), and every
+  // fp32 chain into the block's fp64 partial; then wait for the stores, so
+  // that no store is pending while the prefetch ring is in flight
+  auto drain = [&](int k) __attribute__((always_inline)) {
+    const int i0 = k * KFS_FW, i1 = i0 + KFS_FW < nit ? i0 + KFS_FW : nit;
+    for (int ip = i0 + w; ip < i1; ip += W) {
+      const int u = ip % (2 * KFS_FW);
+      const i64 un = bk + (i64)ip * G;
+      const i64 row = un * U + lane;
+      const bool und = und8[u * U + lane] != 0;
+      const unsigned long long m = __ballot(und);
+      if (row < N && !und) labels[row] = lab8[u * U + lane];
+      if (lane == 0) {
+        und_mask[2 * un] = (unsigned int)m;  // bit l <-> row 32 (2 un) + l
+        if (2 * un + 1 < ntiles) und_mask[2 * un + 1] = (unsigned int)(m >> 32);
       }
+    }
+    if (w < NCT) {
+#pragma unroll 1
+      for (int c = 0; c < 32; ++c) flush(c);  // rolled: the 64 converted sums are not all held at once
+#pragma unroll
+      for (int c = 0; c < 32; ++c) s0[c] = s1[c] = 0.f;  // unrolled: no indexed writes
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   };
 
-  // iterations it = 0 .. nrun - 1 (tile it screened, tile it - 1 decided,
-  // tile it + 1 staged): every unrolled copy issues its loads unconditionally
-  // (clamped addresses; iterations >= nit are ghosts whose rows are never
-  // live) -- a skipped load on any path makes the compiler's count of the
-  // loads in flight unknown, and it then drains the ring (vmcnt(0))
-  const i64 nrun = nit > 0 ? (nit + KFS_R) / KFS_R * KFS_R : 0;
+  // iterations it = 0 .. nrun - 1 (unit it screened and decided, unit it - 1
+  // accumulated, unit it + 1 staged): every unrolled copy issues its loads
+  // unconditionally (clamped addresses; iterations >= nit are ghosts whose
+  // rows are never live) -- a skipped load on any path makes the compiler's
+  // count of the loads in flight unknown, and it then drains the ring
+  const int nrun = nit > 0 ? (nit + KFS_UN) / KFS_UN * KFS_UN : 0;  // >= nit + 1
+  __syncthreads();  // mus
   if (nit > 0) {
     load(ring[0], 0);
-    stage(ring[0], 0, 0);
+    stage(ring[0], 0);
 #pragma unroll
     for (int r = 1; r <= KFS_R; ++r) load(ring[r % KFS_R], r);
   }
-  for (i64 it0 = 0; it0 < nrun; it0 += KFS_R) {
-    // KFS_R iterations with compile-time ring slots (tile T lives in slot T % KFS_R)
+  for (int it0 = 0; it0 < nrun; it0 += KFS_UN) {
+    // unit T lives in ring slot T % KFS_R and fp32 buffer T % 2
     ks_unroll([&](auto sc) __attribute__((always_inline)) {
       constexpr int s = decltype(sc)::value;
-      constexpr int sl = (s + 1) % KFS_R;   // ring slot of tile it + 1
-      constexpr int bn = (s + 1) % KFS_NB;  // fp32 buffer of tile it + 1
-      const i64 it = it0 + s;
+      constexpr int sl = (s + 1) % KFS_R, bc = s % 2, bn = (s + 1) % 2;
+      const int it = it0 + s;
       __syncthreads();
-      // window k = (it - KFS_R) / KFS_FW - 1 is complete in LDS since this
-      // barrier (tiles <= it - 2 are decided); one drain site, s == 0 (KFS_FW
-      // is a multiple of KFS_R, so the drain points fall on it0)
+      // window k = it / KFS_FW - 1 is complete in LDS since this barrier
+      // (units <= it - 1 are decided); one drain site, s == 0
       if constexpr (s == 0)
-        if (it >= KFS_FW + KFS_R && (it - KFS_R) % KFS_FW == 0) drain((it - KFS_R) / KFS_FW - 1);
-      // waves w and w + 4 share a SIMD: they run the latency-bound decide /
-      // accumulate and the MFMA screen in opposite orders
-      if (w < 4) {
-        if (it >= 1) decide(it - 1, (s + KFS_NB - 1) % KFS_NB);
-        if (w < NCT) screen(it);
-      } else {
-        if (w < NCT) screen(it);
-        if (it >= 1) decide(it - 1, (s + KFS_NB - 1) % KFS_NB);
+        if (it >= KFS_FW && it % KFS_FW == 0) drain(it / KFS_FW - 1);
+      if (w < NCT) {
+        kb_acc a0, a1;
+        screen_mfma(a0, a1);
+        if (it >= 1) accumulate(bn);  // unit it - 1 (buffer (it - 1) % 2 = (it + 1) % 2)
+        screen_fold(a0, a1);
       }
-      stage(ring[sl], it + 1, bn);
+      __syncthreads();
+      decide(it, bc);
+      stage(ring[sl], bn);
       load(ring[sl], it + 1 + KFS_R);
-    }, std::make_integer_sequence<int, KFS_R>{});
+    }, std::make_integer_sequence<int, KFS_UN>{});
   }
-  // the windows not drained yet: the last one (its drain point lies past the
-  // loop), and the one before it when the loop ended before its drain point
+  // the windows not drained yet: the last one, and the one before it when
+  // the loop ended before its drain point (a window drained twice writes the
+  // same labels again and flushes only what was added since)
   __syncthreads();
   if (nit > 0) {
-    const i64 last = (nit - 1) / KFS_FW;
-    if (last >= 1 && last * KFS_FW + KFS_R >= nrun) drain(last - 1);
+    const int last = (nit - 1) / KFS_FW;
+    if (last >= 1 && last * KFS_FW >= nrun) drain(last - 1);
     drain(last);
   }
-  if constexpr (ACC) {
-    if (w < NCT && lane < 32 && 32 * w + lane < K) pcnt[(i64)bk * K + 32 * w + lane] = cnt;
-  }
+  if (w < NCT && lane < 32 && 32 * w + lane < K) pcnt[(i64)bk * K + 32 * w + lane] = cnt;
 }
 
-template <int KS, int NCT, bool ACC>
+template <int KS, int NCT>
 static void kfs_launch(hipStream_t s, int grid, i64 N, i64 K, const float* P, i64 ldp, const __bf16* CBh,
                        const __bf16* CBl, const float* cnf2, const double* cmax, const float* muf, i64* labels,
                        unsigned long long* und_mask, double* psum, unsigned long long* pcnt) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_kmeans_fscreen<KS, NCT, ACC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)k_kmeans_fscreen<KS, NCT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)kfs_lds_bytes(16 * KS));
     attr = true;
   }
-  k_kmeans_fscreen<KS, NCT, ACC><<<grid, KFS_WAVES * 64, kfs_lds_bytes(16 * KS), s>>>(
+  k_kmeans_fscreen<KS, NCT><<<grid, KFS_WAVES * 64, kfs_lds_bytes(16 * KS), s>>>(
       N, K, P, ldp, CBh, CBl, cnf2, cmax, muf, labels, und_mask, psum, pcnt);
 }
 
-template <bool ACC>
 static void kfs_launch_n(int nct, int KS, hipStream_t s, int grid, i64 N, i64 K, const float* P, i64 ldp,
                          const __bf16* CBh, const __bf16* CBl, const float* cnf2, const double* cmax, const float* muf,
                          i64* labels, unsigned long long* und_mask, double* psum, unsigned long long* pcnt) {
-#define KFS_CASE(KSV, NC)                                                                                        \
-  if (KS == KSV && nct == NC) {                                                                                  \
-    kfs_launch<KSV, NC, ACC>(s, grid, N, K, P, ldp, CBh, CBl, cnf2, cmax, muf, labels, und_mask, psum, pcnt); \
-    return;                                                                                                      \
+#define KFS_CASE(KSV, NC)                                                                                   \
+  if (KS == KSV && nct == NC) {                                                                             \
+    kfs_launch<KSV, NC>(s, grid, N, K, P, ldp, CBh, CBl, cnf2, cmax, muf, labels, und_mask, psum, pcnt); \
+    return;                                                                                                 \
   }
   KFS_CASE(8, 8) KFS_CASE(8, 4) KFS_CASE(8, 2) KFS_CASE(8, 1)
   KFS_CASE(4, 8) KFS_CASE(4, 4) KFS_CASE(4, 2) KFS_CASE(4, 1)
@@ -3270,9 +3311,9 @@ extern "C" int spx_kmeans_accumulate(int dtype, int64_t N, int64_t D, int64_t K,
 // Workspace: spx_kmeans_assign's | spx_kmeans_accumulate's | fused partial
 // sums (G x K x D f64) | fused partial counts (G x K u64) | compaction block
 // counts.
-static i64 kfs_grid(i64 N) {
-  const i64 ntiles = (N + 31) / 32, ncu = num_cus();
-  return ntiles < ncu ? (ntiles < 1 ? 1 : ntiles) : ncu;
+static i64 kfs_grid(i64 N) {  // one block per CU, at most one per 64-row unit
+  const i64 nunits = (N + 63) / 64, ncu = num_cus();
+  return nunits < ncu ? (nunits < 1 ? 1 : nunits) : ncu;
 }
 
 static i64 kfs_nblk(i64 N) { return ((N + 31) / 32 + 256 * 16 - 1) / (256 * 16); }
@@ -3324,7 +3365,7 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
   HIP_TRY(hipMemsetAsync(psumF, 0, (size_t)G * K * D * sizeof(double), S(stream)));
   k_kmeans_prep_b3<<<1, 1024, 0, S(stream)>>>(D, K, 32 * nct, centers, CBh, CBl, cnf, w.cmax, mcoef, cnf2, w.muf);
   LAUNCH_CHECK("spx_kmeans_step(prep)");
-  kfs_launch_n<true>(nct, (int)(D / 16), S(stream), (int)G, N, K, Pf, ldp, CBh, CBl, cnf2, w.cmax, w.muf, labels,
+  kfs_launch_n(nct, (int)(D / 16), S(stream), (int)G, N, K, Pf, ldp, CBh, CBl, cnf2, w.cmax, w.muf, labels,
                      w.und_mask, psumF, pcntF);
   LAUNCH_CHECK("spx_kmeans_step(fused screen + accumulate)");
   // the screen's undecided rows, in row order (the gathered accumulation's order)

@@ -49,6 +49,8 @@ for s in $STEPS; do
         -d $O/kfs_a -o p --output-format csv -- python3 $R/tools/km_step_once.py 100000000 2 > $O/kfs_a.log 2>&1
       step kfs_b 120 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_VALU_MFMA_BUSY_CYCLES SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE \
         -d $O/kfs_b -o p --output-format csv -- python3 $R/tools/km_step_once.py 100000000 2 > $O/kfs_b.log 2>&1 ;;
+    lregtune)
+      cd $R && step lregtune 300 ./tools/bin/lreg_tune 100000000 3 > $O/lregtune.txt 2>&1 ;;
     gemmseg)
       cd $R && step gemmseg 600 ./tools/bin/gemm_tune 32768 2 seg > $O/gemmseg.txt 2>&1 ;;
     bench)
@@ -66,9 +68,9 @@ for s in $STEPS; do
         -- python3 $R/bench.py --dot 0 --workloads lreg --cpu-baseline 0 --steps 2 --warmup 1 > $O/lregw.log 2>&1 ;;
     kmpmc)
       cd /tmp && step kmf 300 rocprofv3 --pmc FETCH_SIZE -d $O/kmf -o p --output-format csv \
-        -- python3 $R/tools/km_iter.py 100000000 2 > $O/kmf.log 2>&1
+        -- python3 $R/tools/km_step_once.py 100000000 2 > $O/kmf.log 2>&1
       cd /tmp && step kmw 300 rocprofv3 --pmc WRITE_SIZE -d $O/kmw -o p --output-format csv \
-        -- python3 $R/tools/km_iter.py 100000000 2 > $O/kmw.log 2>&1 ;;
+        -- python3 $R/tools/km_step_once.py 100000000 2 > $O/kmw.log 2>&1 ;;
     *)
       # anything else: a python script under tools/ with its arguments joined by ':'
       cd $R && step "$s" 600 python3 ${s//:/ } > $O/$(echo "$s" | tr '/:' '__').log 2>&1 ;;
