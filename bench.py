@@ -146,7 +146,8 @@ def main():
   achieved = bytes_launch / avg / 1e9 if red else None
 
   traffic = None
-  tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r02s2_pmc_traffic.json')
+  tname = 'r03_cfg2_pmc_traffic.json'
+  tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', tname)
   if os.path.exists(tpath) and rows_local == 32768 and S == 32768:
     with open(tpath) as f:
       traffic = json.load(f)['hbm_bytes_per_launch']
@@ -173,7 +174,7 @@ def main():
                    'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                    'frac': round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                    'traffic': traffic,
-                   'traffic_source': 'profiles/r02s2_pmc_traffic.json (FETCH_SIZE/WRITE_SIZE passes)' if traffic
+                   'traffic_source': 'profiles/%s (FETCH_SIZE/WRITE_SIZE passes)' % tname if traffic
                    else None,
                    'kernel': 'generated fused map+reduce: %s' % ' / '.join(knames),
                    'bytes_per_launch': bytes_launch,
@@ -358,9 +359,10 @@ def check_kmeans(X, labels, centers, comm, n_check=1 << 20, dist_dtype=np.float6
 
 
 def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
-  """configs[2]: one k-means iteration (certified fp16-screen + bf16x3
-  filters + exact-order fp64 recompute = scipy-exact labels, fp64 centroid
-  accumulation, all-reduce) over npts x 128 fp32 points, k=256."""
+  """configs[2]: one k-means iteration (spx_kmeans_step: the certified
+  fp16 screen fused with the centroid accumulation, bf16x3 / exact-order
+  passes over its undecided rows = scipy-exact labels, fp64 centroid sums,
+  all-reduce) over npts x 128 fp32 points, k=256."""
   import torch
   from spartan_amd import workloads
   X = expr.rand(npts * ctx.world_size, D, dtype=np.float32, seed=21).force()
@@ -377,17 +379,18 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
   n = npts * ctx.world_size
   out = {'ms_per_iter': round(el * 1e3, 3), 'points_per_s': round(n / el, 1),
          'gemm_form_tflops': round(2.0 * n * K * D / el / 1e12, 2),
-         # the first pass runs the distance GEMM once on fp16 MFMAs (the
-         # screen; the bf16x3 pass re-runs only its few % undecided rows), so
-         # the GEMM-form rate over the dense fp16/bf16 peak is its matrix-core
-         # share of the whole iteration; the iteration also streams X twice
-         # (assign + accumulate: 2 * 4 * N * D bytes)
+         # the screen runs the distance GEMM once on fp16 MFMAs (the bf16x3
+         # pass re-runs only its few % undecided rows), so the GEMM-form rate
+         # over the dense fp16/bf16 peak is its matrix-core share of the whole
+         # iteration; the fused step reads X once (4 N D bytes; FETCH_SIZE:
+         # 1.16 x that, profiles/r03_kmeans_step_pmc.json)
          'f16_mfma_frac_per_gpu': round(2.0 * n * K * D / el / 1e12 / (2500.0 * ctx.world_size), 4),
-         'hbm_GBps_two_passes': round(2.0 * 4.0 * n * D / el / 1e9, 1),
+         'hbm_GBps_one_pass': round(4.0 * n * D / el / 1e9, 1),
          'checked': checked,
          'config': 'cfg3: %d x %d fp32 points (U[0,1), seed 21) per GPU, k=%d, centres = first %d points; '
-                   'assign = certified fp16-MFMA screen, bf16x3-MFMA pass over its undecided rows, exact-order '
-                   'fp64 recompute of the rest (bit-exact labels), fp64 centroid sums' % (npts, D, K, K)}
+                   'spx_kmeans_step: certified fp16-MFMA screen + per-centre sums of the rows it decides in one '
+                   'pass over X, bf16x3-MFMA pass + exact-order fp64 recompute of its undecided rows (bit-exact '
+                   'labels) + their gathered sums, fp64 centroid sums' % (npts, D, K, K)}
   del X, labels
   torch.cuda.empty_cache()
   return out

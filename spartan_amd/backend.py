@@ -492,7 +492,7 @@ class HipBackend:
       # exactly two resident blocks per CU (cfg2 axis 0: 512 blocks 1.80 ms,
       # 1024 1.87, 2048 1.87, 4096 1.90); one narrow column tile (cfg5's 64
       # columns) with eight (2048: 4.06 ms per lreg iteration, 512: 4.15)
-      # -- tools/cfg2_knobs.py, profiles/r02_cfg2_grid.txt
+      # -- profiles/r02_cfg2_grid.txt
       tb = (2 if CT > 1 else 8) * _num_cus()
       if base < tb:
         P = max(1, min(-(-tb // base), -(-R // (rows_per_step * 4))))

@@ -13,6 +13,9 @@ are registered joins (expr/join.py), so each runs as device work:
                         or fp32 distances (the argmin of the values rounded to
                         the target dtype): certified bf16x3-MFMA filter +
                         exact recompute, no (N, K) matrix (102-205 GB at cfg3);
+                        in spx_kmeans_step's domain the fused step, whose
+                        centre sums / counts the two joins below then take
+                        (one pass over X per iteration);
   kmeans_count_mapper   map2(labels, 0)        -> spx_bincount per label tile
                         + RCCL all-reduce;
   kmeans_center_mapper  map2((X, labels), (0, 0)) -> spx_kmeans_accumulate
@@ -118,6 +121,11 @@ def _count_join(kind, arrays, axes, fn_kw, target):
   be = backend.get()
   K = int(fn_kw['centers_count'])
   labels = arrays[0]
+  pre = _take_step(_STEP.get('X'), labels, K, 'counts')
+  if pre is not None:
+    comm.all_reduce(pre, 'sum')
+    _deliver_full(target, pre)
+    return
   counts = torch.zeros((K,), dtype=torch.int64, device=ctx.device)
   for ex, tile in labels.local.items():
     lab = be.contiguous(tile.data, np.int64).reshape(-1)
@@ -133,6 +141,11 @@ def _center_join(kind, arrays, axes, fn_kw, target):
   K = int(fn_kw['centers_count'])
   X, labels = arrays
   D = X.shape[1]
+  pre = _take_step(X, labels, K, 'sums')
+  if pre is not None:  # the fused step of this labels array already summed X
+    comm.all_reduce(pre, 'sum')
+    _deliver_full(target, pre)
+    return
   sums = torch.zeros((K, D), dtype=torch.float64, device=ctx.device)
   counts = torch.zeros((K,), dtype=torch.int64, device=ctx.device)
   blocks, got = _row_blocks(X, D)
@@ -152,20 +165,41 @@ def _center_join(kind, arrays, axes, fn_kw, target):
   _deliver_full(target, sums)
 
 
+# The last fused assignment's per-rank centre sums and counts (one entry):
+# argmin(outer(X, C)) runs spx_kmeans_step, which produces the iteration's
+# sums and counts from the same single pass over X, and the centre / count
+# joins of THAT labels array over THAT X take them instead of reading X again.
+_STEP = {}
+
+
+def _step_domain(X, K):
+  """True where spx_kmeans_step fuses (fp32 rows of 64 / 128 dims, K <= 256,
+  row-strip tiles): decided from global metadata, so every rank agrees."""
+  return (np.dtype(X.dtype) == np.float32 and len(X.shape) == 2 and X.shape[1] in (64, 128) and K <= 256
+          and all(ex.ul[1] == 0 and ex.lr[1] == X.shape[1] for ex in X.tiles))
+
+
 def _assign_fused(arrays, fn_kw, target, dist_dtype):
   """argmin(outer((X, C), (0, 0), kmeans_dist_mapper), axis=1): the outer's
   target holds the cdist values rounded to its dtype (fp64, or fp32 for fp32
   points: map2 / outer dtype None -> arrays[0].dtype); spx_kmeans_assign per
   X row block gives the argmin of exactly those values (first index on
-  ties, first NaN wins) without materialising them."""
+  ties, first NaN wins) without materialising them.  In spx_kmeans_step's
+  domain the same labels come from the fused step, which also leaves this
+  rank's centre sums and counts in _STEP for _center_join / _count_join."""
   import torch
   from ..expr.join import _scatter_updates
   X, C = arrays
   ctx = runtime.get()
   be = backend.get()
   c = _replicated_f64(C)
-  D = c.shape[1]
+  K, D = c.shape
   blocks, got = _row_blocks(X, D)
+  fused = _step_domain(X, K)
+  _STEP.clear()
+  if fused:
+    sums = torch.zeros((K, D), dtype=torch.float64, device=ctx.device)
+    counts = torch.zeros((K,), dtype=torch.int64, device=ctx.device)
   updates = []
   for qi, (src, region) in enumerate(blocks):
     tex = ext.create((region.ul[0],), (region.lr[0],), target.shape)
@@ -175,9 +209,21 @@ def _assign_fused(arrays, fn_kw, target, dist_dtype):
       if pts.stride(-1) != 1:
         pts = be.contiguous(pts)
       lab = torch.empty((tex.shape[0],), dtype=torch.int64, device=ctx.device)
-      be.kmeans_assign(pts, c, lab, dist_dtype=dist_dtype)
+      if fused:
+        be.kmeans_step(pts, c, lab, sums, counts, zero_first=False, dist_dtype=dist_dtype)
+      else:
+        be.kmeans_assign(pts, c, lab, dist_dtype=dist_dtype)
     updates.append((qi, tex, src, lab))
   _scatter_updates(target, updates)
+  if fused:
+    _STEP.update(labels=target, X=X, K=K, sums=sums, counts=counts)
+
+
+def _take_step(X, labels, K, what):
+  """This rank's fused sums / counts for (X, labels), once each, or None."""
+  if _STEP.get('labels') is labels and _STEP.get('X') is X and _STEP.get('K') == K and what in _STEP:
+    return _STEP.pop(what)
+  return None
 
 
 register_join(kmeans_dist_mapper, _dist_join)

@@ -345,6 +345,49 @@ def test_plan_cache_keeps_shared_node_ids(host_ctx):
   assert calls == [np.float32] * 4
 
 
+def test_kmeans_api_one_pass(host_ctx):
+  """The drop-in KMeans loop in spx_kmeans_step's domain (fp32, D = 64,
+  K <= 256): the fused argmin runs the step, and the centre / count joins of
+  that labels array take its sums and counts instead of reading X again --
+  same centres and labels as the two-pass joins."""
+  host_ctx(1)
+  from spartan_amd import backend, expr
+  from spartan_amd.examples import kmeans as km
+  from oracle import rng
+  pts = rng.rand((600, 64), 23, np.float32)
+  X = expr.from_numpy(pts).force()
+  c0 = pts[:6].astype(np.float64)
+  be = backend.get()
+  calls = {'kmeans_step': 0, 'kmeans_accumulate': 0, 'bincount': 0, 'kmeans_assign': 0}
+  origs = {n: getattr(be, n) for n in calls}
+
+  def counted(n):
+    def f(*a, **k):
+      calls[n] += 1
+      return origs[n](*a, **k)
+    return f
+  for n in calls:
+    setattr(be, n, counted(n))
+  try:
+    c1, l1 = km.KMeans(6, 3).fit(X, c0)
+    fused = dict(calls)
+    for n in calls:
+      calls[n] = 0
+    dom = km._step_domain
+    km._step_domain = lambda X, K: False
+    try:
+      c2, l2 = km.KMeans(6, 3).fit(X, c0)
+    finally:
+      km._step_domain = dom
+  finally:
+    for n, f in origs.items():
+      setattr(be, n, f)
+  assert fused['kmeans_step'] == 3 and fused['kmeans_accumulate'] == 3 and fused['bincount'] == 0
+  assert calls['kmeans_step'] == 0 and calls['kmeans_assign'] == 3 and calls['bincount'] == 3
+  np.testing.assert_array_equal(c1, c2)
+  np.testing.assert_array_equal(l1.glom(), l2.glom())
+
+
 def _host_mapper_cases(expr):
   """(name, expression, NumPy result) for mappers that cannot be traced into
   a kernel -- data-dependent control flow, non-ufunc NumPy calls on the tile

@@ -66,6 +66,11 @@ for s in $STEPS; do
         -- python3 $R/bench.py --dot 0 --workloads lreg --cpu-baseline 0 --steps 2 --warmup 1 > $O/lregf.log 2>&1
       cd /tmp && step lregw 300 rocprofv3 --pmc WRITE_SIZE -d $O/lregw -o p --output-format csv \
         -- python3 $R/bench.py --dot 0 --workloads lreg --cpu-baseline 0 --steps 2 --warmup 1 > $O/lregw.log 2>&1 ;;
+    cfg2pmc)
+      cd /tmp && step c2f 300 rocprofv3 --pmc FETCH_SIZE -d $O/c2f -o p --output-format csv \
+        -- python3 $R/bench.py --dot 0 --workloads 0 --cpu-baseline 0 --steps 3 --warmup 1 > $O/c2f.log 2>&1
+      cd /tmp && step c2w 300 rocprofv3 --pmc WRITE_SIZE -d $O/c2w -o p --output-format csv \
+        -- python3 $R/bench.py --dot 0 --workloads 0 --cpu-baseline 0 --steps 3 --warmup 1 > $O/c2w.log 2>&1 ;;
     kmpmc)
       cd /tmp && step kmf 300 rocprofv3 --pmc FETCH_SIZE -d $O/kmf -o p --output-format csv \
         -- python3 $R/tools/km_step_once.py 100000000 2 > $O/kmf.log 2>&1
