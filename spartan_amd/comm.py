@@ -2,7 +2,11 @@
 
 Data plane, by ``ctx.dist_backend``:
 
-* ``'rccl'`` (the GPU default at N > 1): every collective is a libspx.so
+* ``'nccl'`` (the GPU default at N > 1): torch.distributed's own RCCL
+  process group (PyTorch's librccl); also the fallback when the libspx
+  communicator fails its start-up self-test (``selftest``).
+* ``'rccl'`` (opt-in, ``SPARTAN_DIST_BACKEND=rccl``, until a multi-GPU run
+  has validated it): every collective is a libspx.so
   C-ABI call (``spx_allreduce`` / ``spx_reduce_scatter`` / ``spx_allgather``
   / ``spx_broadcast`` / ``spx_reduce`` / ``spx_sendrecv``, include/spx.h) on
   the RCCL communicator the runtime created, enqueued on the current HIP
@@ -11,9 +15,6 @@ Data plane, by ``ctx.dist_backend``:
 * ``'gloo'``: CPU tests, and the one-GPU multi-rank rehearsal
   (``SPARTAN_DIST_BACKEND=gloo``), where device tensors are staged through
   host memory.
-* ``'nccl'``: torch.distributed's own RCCL process group
-  (``SPARTAN_COMM=torch``; also the fallback when the libspx communicator
-  fails its start-up self-test, ``selftest``).
 
 Replaces the reference's pickled ZeroMQ point-to-point messages
 (spartan/rpc/common.py:52-62, spartan/blob_ctx.py:127-179): every exchange

@@ -62,15 +62,18 @@ def initialize(argv=None, device=None):
   """Bring up this rank (reference spartan.initialize, spartan/__init__.py:42-56).
 
   Reads RANK / WORLD_SIZE / LOCAL_RANK from the torchrun environment and
-  selects cuda:LOCAL_RANK.  With more than one rank on GPUs the data plane is
-  an RCCL communicator created through libspx.so (spx_comm_init; every device
-  collective is a C-ABI call, comm.py) and torch.distributed runs gloo as the
-  host control plane (the unique-id hand-off, barriers, host maxima).
+  selects cuda:LOCAL_RANK.  With more than one rank on GPUs the data plane
+  is, by default, torch.distributed's own RCCL process group ('nccl' -- the
+  same librccl, the collective path PyTorch validates on every multi-GPU
+  job).  ``SPARTAN_DIST_BACKEND=rccl`` opts in to the libspx.so C-ABI
+  communicator instead (spx_comm_init; every device collective a C-ABI call,
+  comm.py; torch.distributed then runs gloo as the host control plane: the
+  unique-id hand-off, barriers, host maxima), checked by a start-up
+  self-test that falls back to the torch group.  It stays opt-in until a
+  multi-GPU run has validated it (so far it has run at world 1 only).
   ``SPARTAN_DIST_BACKEND=gloo`` rehearses N ranks on fewer GPUs (device
-  tensors staged through the host); ``SPARTAN_COMM=torch`` uses
-  torch.distributed's own RCCL group instead of libspx's.  ``device``
-  overrides the device (tests run the host logic on 'cpu' with a test
-  backend and gloo)."""
+  tensors staged through the host).  ``device`` overrides the device (tests
+  run the host logic on 'cpu' with a test backend and gloo)."""
   global _ctx
   import torch
   if argv is not None:
@@ -88,8 +91,10 @@ def initialize(argv=None, device=None):
   rccl = None
   if world > 1:
     import torch.distributed as dist
-    backend = os.environ.get('SPARTAN_DIST_BACKEND', 'rccl' if device.type == 'cuda' else 'gloo')
-    if backend == 'nccl' or (backend == 'rccl' and os.environ.get('SPARTAN_COMM') == 'torch'):
+    backend = os.environ.get('SPARTAN_DIST_BACKEND', 'nccl' if device.type == 'cuda' else 'gloo')
+    if backend not in ('nccl', 'rccl', 'gloo'):
+      raise ValueError('SPARTAN_DIST_BACKEND must be nccl, rccl or gloo, not %r' % backend)
+    if backend == 'rccl' and os.environ.get('SPARTAN_COMM') == 'torch':
       backend = 'nccl'
     pg = 'nccl' if backend == 'nccl' else 'gloo'   # torch.distributed: control plane (or the torch RCCL path)
     if not dist.is_initialized():
