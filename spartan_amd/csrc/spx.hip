@@ -2581,6 +2581,507 @@ static void kfs_launch_n(int nct, int KS, hipStream_t s, int grid, i64 N, i64 K,
 #undef KFS_CASE
 }
 
+// ---------------------------------------------------------------------------
+// Fused k-means step, LDS-sum form (k_kmeans_fs2, the default of
+// spx_kmeans_step).  The same screen and decision as k_kmeans_fscreen (the
+// same fp16 / bf16 MFMAs, tags, top-2 and certified bound), but the
+// accumulation no longer goes through run-time-indexed registers (a
+// readlane, two s_set_gpr_idx pairs and their hazards per row and dim pair,
+// ~4 ms of the 20.5 ms kernel at cfg3):
+//   * the per-centre sums of the block live in LDS as fp32 [256][D] (128 KiB
+//     at D = 128; column XOR-swizzled by the centre so that the 64 rows of one
+//     add instruction spread over the banks) and the decided rows are added
+//     with no-return ds_add_f32 straight from the registers their loads
+//     landed in -- no fp32 row copy in LDS;
+//   * for that the unit is loaded column-split: wave w holds columns
+//     w D/8 .. + D/8 of ALL 64 rows (lane = row), so two lanes of one wave
+//     that add to the same address (two rows of one centre) are ordered by
+//     the LDS unit inside one instruction, waves never share an address, and
+//     the rows of one wave are added in unit order: the sums are
+//     deterministic without an owner wave per centre;
+//   * |x'|^2 comes as 8 column partials per row, summed in a fixed DPP tree
+//     in the decision (all 8 lanes of a row get the same bits);
+//   * labels (a coalesced 64 B store per wave) and the undecided-row mask go
+//     out one unit behind the decision from the label array in LDS; every
+//     store is issued unconditionally (ghost / tail rows write to a dummy
+//     word), so the compiler's count of the loads in flight stays static.
+// Every KF2_FW units the fp32 sums are added to the block's private fp64
+// partial (no-return fp64 atomics, one writer per address) and cleared: an
+// fp32 chain covers at most ~KF2_FW / 4 rows of one centre (~64 here).
+// Ring: unit u lives in register slot u % KF2_NS from its load (two units
+// ahead) through its staging until its add one iteration after its decision.
+#ifndef KF2_DEV
+#define KF2_DEV 0
+#endif
+#ifndef KFS_V2
+#define KFS_V2 1  // 1: spx_kmeans_step runs k_kmeans_fs2 (LDS sums), 0: k_kmeans_fscreen (register sums)
+#endif
+constexpr int KF2_NS = 4;
+#ifndef KF2_FWV
+#define KF2_FWV 256
+#endif
+constexpr int KF2_FW = KF2_FWV;
+static_assert(KF2_FW % KF2_NS == 0, "the flush points must fall on the unrolled body's first copy");
+static size_t kf2_lds_bytes(int D) {
+  return (size_t)256 * D * 4 + 256 * 4 + (size_t)KFS_U * kfs_rs(D) + (size_t)2 * KFS_WAVES * KFS_U * 4 +
+         (size_t)KFS_WAVES * (KFS_EXV_S + KFS_EXI_S) * 4 + KFS_U * 4 + KFS_WAVES * 256 + 64 * 16;
+}
+
+#ifndef KF2_PRIO
+#define KF2_PRIO 0
+#endif
+#ifndef KF2_PROF
+#define KF2_PROF 0  // dev builds: per-wave cycles per loop segment (s_memtime) -> spx_dev_kf2_prof
+#endif
+#if KF2_PROF
+__device__ unsigned long long g_kf2_prof[256 * 8 * 9];
+extern "C" int spx_dev_kf2_prof(unsigned long long* host_out) {
+  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_kf2_prof), sizeof(g_kf2_prof)) == hipSuccess ? 0 : 1;
+}
+#endif
+template <int KS, int NCT>
+__global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
+    i64 N, i64 K, const float* __restrict__ P, i64 ldp, const __bf16* __restrict__ CBh,
+    const __bf16* __restrict__ CBl, const float* __restrict__ cnf2, const double* cmax_p,
+    const float* __restrict__ muf, i64* __restrict__ labels, unsigned long long* __restrict__ und_mask,
+    float* __restrict__ part, int nwin, unsigned long long* __restrict__ pcnt, unsigned long long* __restrict__ dummy) {
+  constexpr int D = 16 * KS, CPW = D / 8, RS = kfs_rs(D), W = KFS_WAVES, U = KFS_U, NS = KF2_NS;
+  static_assert(CPW % 8 == 0, "D = 64 or 128");
+  extern __shared__ __attribute__((aligned(16))) unsigned char kf2_lds[];
+  float* sums = (float*)kf2_lds;                         // [256][D] fp32, column c of centre d at c ^ (d & (D - 4))
+  unsigned int* cnts = (unsigned int*)(sums + 256 * D);  // [256] decided rows per centre
+  unsigned char* xh = (unsigned char*)(cnts + 256);      // [U][RS] fp16 x'
+  float* p2p = (float*)(xh + (size_t)U * RS);            // [2][W][U] |x'|^2 over wave w's columns
+  float* exv = p2p + 2 * W * U;                          // [W][KFS_EXV_S] (b1, b2) per row
+  int* exi = (int*)(exv + W * KFS_EXV_S);                // [W][KFS_EXI_S] best centre
+  short* dl = (short*)(exi + W * KFS_EXI_S);             // [2][U] label of a decided row, -1 otherwise (by unit parity)
+  unsigned char* tbl = (unsigned char*)(dl + 2 * U);       // [W][256] per-wave winner table of the add rounds
+  float* ldum = (float*)(tbl + W * 256);                 // [64][4] per-lane dummy slot of the straight-line rounds
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, j = lane & 31, h = lane >> 5;
+  const int col0 = w * CPW;
+  for (int i = t; i < 256 * D + 256; i += W * 64) sums[i] = 0.f;  // (cnts: the same bits)
+  if (t < 2 * U) dl[t] = -1;
+  float mu[CPW];
+#pragma unroll
+  for (int e = 0; e < CPW; ++e) mu[e] = muf[col0 + e];
+
+  kh_f8 ca[KS];
+  kb_bf8 ccp;
+  {
+    const i64 c = 32 * (i64)(w < NCT ? w : 0) + j;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const i64 d = 16 * ks + 8 * h + e;
+        ca[ks][e] = (_Float16)((float)CBh[c * D + d] + (float)CBl[c * D + d]);
+      }
+    const float v = -0.5f * cnf2[c];
+    const __bf16 b1 = (__bf16)v;
+    const float v1 = v - (float)b1;
+    const __bf16 b2 = (__bf16)v1;
+    const __bf16 b3 = (__bf16)(v1 - (float)b2);
+    const __bf16 z = (__bf16)0.f;
+    ccp = h == 0 ? (kb_bf8){b1, b2, b3, z, z, z, z, z} : (kb_bf8){z, z, z, z, z, z, z, z};
+  }
+  const __bf16 one = (__bf16)1.f;
+  const kb_bf8 ones = (kb_bf8){one, one, one, one, one, one, one, one};
+
+  // the certified bound of k_kmeans_fscreen / k_kmeans_filter_as MODE 1
+  const double cmax = cmax_p[0], mcoef = cmax_p[1], mun = cmax_p[2], dcmax = cmax_p[3];
+  const double u32 = 5.9604644775390625e-08;
+  const double chain = 16.0 * (double)KS;
+  const double eS = (u32 * cmax + 4.8828125e-04 * cmax + 1.001 * dcmax +
+                     2.0 * (chain + 3.0) * u32 * 1.001 * (cmax + dcmax)) * 1.01;
+  double xk1 = 64.0 * u32 * cmax, xk0 = 32.0 * u32 * (cmax * cmax + 2.0 * mun * cmax);
+  xk0 += sqrt((double)D) * 1.1920928955078125e-07 * (cmax + dcmax) + (double)D * 3.552713678800501e-15;
+  xk1 += 14.0 * 1.1920928955078125e-07 * cmax;
+  xk0 += 7.0 * 1.1920928955078125e-07 * (cmax * cmax + 2.0 * mun * cmax);
+  float kq[3];
+  kc_coef(eS, cmax, mun, mcoef, D, kq, xk1, xk0);
+  const bool cok = cmax * cmax < 1e36 && mun * cmax < 1e36 && cmax < 3.0e4 && dcmax == dcmax;
+  const float pn_lim = (float)(cmax > 0.0 ? 1e36 / cmax : 1e36);
+
+  const int G = gridDim.x, bk = blockIdx.x;
+  const i64 nunits = (N + U - 1) / U, ntiles = (N + 31) / 32;
+  const int nit = bk < nunits ? (int)((nunits - 1 - bk) / G + 1) : 0;
+  kb_f4 ring[NS][CPW / 4];
+  auto load = [&](kb_f4 (&r)[CPW / 4], int it) __attribute__((always_inline)) {  // clamped: always a valid address
+    const i64 un = bk + (i64)(it < nit ? it : nit - 1) * G;
+    i64 row = un * U + lane;
+    row = row < N ? row : N - 1;
+    const float* p = P + row * ldp + col0;
+#pragma unroll
+    for (int q = 0; q < CPW / 4; ++q) r[q] = *(const kb_f4*)(p + 4 * q);
+  };
+  auto stage = [&](const kb_f4 (&r)[CPW / 4], int b) __attribute__((always_inline)) {  // slot -> xh, p2p[b]
+    _Float16 hv[CPW];
+    kfs_f2 p2v = (kfs_f2){0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < CPW / 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        const kfs_f2 x = (kfs_f2){r[q][e], r[q][e + 1]} - (kfs_f2){mu[4 * q + e], mu[4 * q + e + 1]};
+        p2v = __builtin_elementwise_fma(x, x, p2v);
+        hv[4 * q + e] = (_Float16)x[0];
+        hv[4 * q + e + 1] = (_Float16)x[1];
+      }
+    unsigned char* hrow = xh + (size_t)lane * RS + 2 * col0;
+#pragma unroll
+    for (int g = 0; g < CPW / 8; ++g)
+      *(kh_f8*)(hrow + 16 * g) = (kh_f8){hv[8 * g], hv[8 * g + 1], hv[8 * g + 2], hv[8 * g + 3],
+                                         hv[8 * g + 4], hv[8 * g + 5], hv[8 * g + 6], hv[8 * g + 7]};
+    p2p[(b * W + w) * U + lane] = p2v[0] + p2v[1];
+  };
+
+  auto fold16 = [&](const kb_acc& acc, float& lo, float& sec, int& il) __attribute__((always_inline)) {
+    float tv[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float a = acc[q];
+      tv[q] = __builtin_bit_cast(float, (__builtin_bit_cast(unsigned int, a) & ~15u) | (unsigned int)q);
+    }
+    lo = ks_max(tv[0], tv[1]);
+    sec = ks_med3(tv[0], tv[1], -INFINITY);
+#pragma unroll
+    for (int q = 2; q < 16; q += 2) {
+      sec = ks_max(sec, ks_med3(lo, tv[q], tv[q + 1]));
+      lo = ks_max3(lo, tv[q], tv[q + 1]);
+    }
+    const unsigned int qb = __builtin_bit_cast(unsigned int, lo) & 15u;
+    il = 32 * w + (int)((qb & 3) + 8 * (qb >> 2)) + 4 * h;
+  };
+  auto screen_fold = [&](const kb_acc& a0, const kb_acc& a1) __attribute__((always_inline)) {
+    float loa, seca, lob, secb;
+    int ila, ilb;
+    fold16(a0, loa, seca, ila);
+    fold16(a1, lob, secb, ilb);
+    // half-swap by v_permlane32_swap (VALU, no LDS round trip): lanes 0-31
+    // end with tile 0's candidates of point j from both halves, lanes 32-63
+    // with tile 1's; the top-2 merge is symmetric in the two, and on equal
+    // values the row stays undecided, so the index tie-break does not matter
+    auto sw32 = [](float x, float y, float& r0, float& r1) __attribute__((always_inline)) {
+      const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned int, x),
+                                                      __builtin_bit_cast(unsigned int, y), false, false);
+      r0 = __builtin_bit_cast(float, (unsigned int)r[0]);
+      r1 = __builtin_bit_cast(float, (unsigned int)r[1]);
+    };
+    float l0, l1, s0, s1, f0, f1;
+    sw32(loa, lob, l0, l1);
+    sw32(seca, secb, s0, s1);
+    sw32(__builtin_bit_cast(float, ila), __builtin_bit_cast(float, ilb), f0, f1);
+    const float b1 = ks_max(l0, l1);
+    const float b2 = ks_med3(l0, l1, ks_max(s0, s1));
+    const int ib = l0 >= l1 ? __builtin_bit_cast(int, f0) : __builtin_bit_cast(int, f1);
+    // lane (j, h) holds unit row 32 h + j = lane
+    *(kfs_f2*)(exv + w * KFS_EXV_S + 2 * lane) = (kfs_f2){b1, b2};
+    exi[w * KFS_EXI_S + lane] = ib;
+  };
+
+  // decision of unit it (its |x'|^2 partials in p2p[b]); wave w: rows 8 w .. + 7
+  auto decide = [&](int it, int b) __attribute__((always_inline)) {
+    const int r = lane >> 3, v = lane & 7, row = 8 * w + r;
+    float b1 = -INFINITY, b2 = -INFINITY;
+    int ib = 0;
+    if (v < NCT) {
+      const kfs_f2 e2 = *(const kfs_f2*)(exv + v * KFS_EXV_S + 2 * row);
+      b1 = e2[0];
+      b2 = e2[1];
+      ib = exi[v * KFS_EXI_S + row];
+    }
+    float p2f = p2p[(b * W + v) * U + row];
+    auto merge = [&](auto ctl) __attribute__((always_inline)) {
+      constexpr int C = decltype(ctl)::value;
+      const float pb1 = kfs_dppf<C>(b1), pb2 = kfs_dppf<C>(b2);
+      const int pib = kfs_dppi<C>(ib);
+      b2 = ks_med3(b1, pb1, ks_max(b2, pb2));
+      ib = pb1 > b1 ? pib : ib;
+      b1 = ks_max(b1, pb1);
+      p2f += kfs_dppf<C>(p2f);  // a fixed tree: the row's 8 lanes end with the same bits
+    };
+    merge(std::integral_constant<int, 0xB1>{});
+    merge(std::integral_constant<int, 0x4E>{});
+    merge(std::integral_constant<int, 0x141>{});
+    const float pn = __builtin_amdgcn_sqrtf(__builtin_fmaf(p2f, 1.001f, 1e-37f)) * 1.0001f;
+    const float e = __builtin_fmaf(__builtin_fmaf(kq[2], pn, kq[1]), pn, kq[0]) * 1.0001f;
+    const bool fin = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim && isfinite(b1) && isfinite(b2);
+    const i64 grow = (bk + (i64)it * G) * U + row;
+    const bool live = it < nit && grow < N;
+    const bool dec = fin && b1 - b2 > 1.0001f * e;
+    if (v == 0) dl[b * U + row] = (short)(live && dec ? ib : -1);
+  };
+
+  // Unit it - 1's decided rows go into the LDS sums by plain read-add-writes.
+  // Rows of one centre in one unit would race there, so the adds go in
+  // rounds: a row joins round k when its lane wins its centre's slot in this
+  // wave's table at the k-th write / read-back (one winner per centre and
+  // round; which lane wins is the LDS unit's fixed choice).  The table
+  // rounds (three dependent LDS round trips) are woven between unit it's
+  // MFMAs in phase 1, where the wave's issue would otherwise wait on the
+  // matrix pipe; the read-add-writes of rounds 0 and 1 run in phase 2 beside
+  // the decision (straight-line code: lanes outside a round read and write
+  // their own dummy slot), then the rare rows of a centre's third and later
+  // add in a loop.
+  typedef __attribute__((address_space(3))) unsigned char lds_u8;
+  // (relaxed atomics on the table: not folded into the lane's own store like
+  // plain accesses, and not waited for at once like volatile ones)
+  auto tput = [](lds_u8* p, int v) __attribute__((always_inline)) {
+    __hip_atomic_store(p, (unsigned char)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  auto tget = [](lds_u8* p) __attribute__((always_inline)) {
+    return (int)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  float* const dum = ldum + 4 * lane;
+  lds_u8* const tb = (lds_u8*)(tbl + w * 256);
+  lds_u8* const tdum = (lds_u8*)dum;
+  struct Rounds {
+    int d;          // the row's label (< 0: not decided)
+    int dlr;        // label of row 8 w + lane / 8 (out_labels' store)
+    bool w0, w1;    // the row adds in round 0 / 1
+    bool more;      // the row adds after round 1
+  };
+  auto screen_tbl = [&](kb_acc& a0, kb_acc& a1, int bp) __attribute__((always_inline)) {
+    const bool scr = NCT == 8 || w < NCT;
+    const unsigned char* bpa = xh + (size_t)j * RS + 16 * h;
+    const unsigned char* bpb = bpa + (size_t)32 * RS;
+    a0 = (kb_acc){};
+    a1 = (kb_acc){};
+    Rounds R{0, 0, false, false, false};
+    bool act = false, rem = false;
+    int tv = 0;  // the table byte read back (compared one step later)
+    auto step = [&](auto kc) __attribute__((always_inline)) {
+      constexpr int k = decltype(kc)::value;
+      if constexpr (k == 0) {
+        R.d = dl[bp * U + lane];
+        R.dlr = dl[bp * U + 8 * w + (lane >> 3)];
+      } else if constexpr (k == 1) {
+        act = R.d >= 0;
+        tput(act ? tb + R.d : tdum, lane);
+      } else if constexpr (k == 2) {
+        tv = tget(act ? tb + R.d : tdum);
+      } else if constexpr (k == 3) {  // (no short-circuit: a branch would split the straight-line block)
+        R.w0 = act & (tv == lane);
+        rem = act & !R.w0;
+        tput(rem ? tb + R.d : tdum, lane);
+      } else if constexpr (k == 4) {
+        tv = tget(rem ? tb + R.d : tdum);
+      } else if constexpr (k == 5) {
+        R.w1 = rem & (tv == lane);
+        R.more = rem & !R.w1;
+      }
+    };
+    // B fragments one k-step ahead: an MFMA's wait for its operands then
+    // covers only LDS operations issued a step earlier
+    kh_f8 va = *(const kh_f8*)bpa, vb = *(const kh_f8*)bpb;
+    auto mf = [&](auto kc) __attribute__((always_inline)) {
+      constexpr int ks = decltype(kc)::value;
+      kh_f8 na = va, nb = vb;
+      if constexpr (ks + 1 < KS) {
+        na = *(const kh_f8*)(bpa + 32 * (ks + 1));
+        nb = *(const kh_f8*)(bpb + 32 * (ks + 1));
+      }
+      if (scr) {
+        a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[ks], va, a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[ks], vb, a1, 0, 0, 0);
+      }
+      va = na;
+      vb = nb;
+      if constexpr (KS == 8) {
+        if constexpr (ks < 6) step(std::integral_constant<int, ks>{});
+      } else {
+        step(std::integral_constant<int, 2 * ks>{});
+        if constexpr (2 * ks + 1 < 6) step(std::integral_constant<int, 2 * ks + 1>{});
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    ks_unroll(mf, std::make_integer_sequence<int, KS>{});
+    if (scr) {
+      a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ccp, ones, a0, 0, 0, 0);
+      a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ccp, ones, a1, 0, 0, 0);
+    }
+    return R;
+  };
+
+  // the read-add-writes of unit it - 1 (raw columns in r), in rounds; each
+  // round exec-masked to its rows (LDS time goes by the active lanes).
+  // Round 0's reads are issued before the decision of unit it (add_begin),
+  // whose DPP chain then covers their latency.
+  kb_f4 v0[CPW / 4];
+  auto add_begin = [&](const Rounds& R) __attribute__((always_inline)) {
+    if (R.w0) {
+      float* const srow = sums + R.d * D;
+      const int sw = R.d & (D - 4);  // XOR by a multiple of 4: the lane's 4-column groups stay whole
+#pragma unroll
+      for (int q = 0; q < CPW / 4; ++q) v0[q] = *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw));
+    }
+  };
+  auto add_end = [&](const Rounds& R, const kb_f4 (&r)[CPW / 4]) __attribute__((always_inline)) {
+    float* const srow = sums + R.d * D;
+    const int sw = R.d & (D - 4);
+    if (R.w0) {
+#pragma unroll
+      for (int q = 0; q < CPW / 4; ++q) *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw)) = v0[q] + r[q];
+      if (w == 0) cnts[R.d] += 1u;
+    }
+    auto rmw = [&]() __attribute__((always_inline)) {
+      kb_f4 v[CPW / 4];
+#pragma unroll
+      for (int q = 0; q < CPW / 4; ++q) v[q] = *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw));
+#pragma unroll
+      for (int q = 0; q < CPW / 4; ++q) *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw)) = v[q] + r[q];
+      if (w == 0) cnts[R.d] += 1u;
+    };
+    if (R.w1) rmw();
+    bool more = R.more;
+    while (__ballot(more)) {
+      tput(more ? tb + R.d : tdum, lane);
+      if (more && tget(tb + R.d) == lane) {
+        rmw();
+        more = false;
+      }
+    }
+  };
+
+  // labels and undecided bits of unit it - 1 (d: its label array entry of this lane's row)
+  auto out_labels = [&](int d, int dlr, int it) __attribute__((always_inline)) {
+    const int up = it - 1;
+    const i64 unp = bk + (i64)up * G;
+    const bool ulive = up >= 0 && up < nit;
+    const int lr = 8 * w + (lane >> 3);
+    const i64 glr = unp * U + lr;
+    i64* la = ulive && glr < N ? labels + glr : (i64*)dummy;
+    *la = (i64)dlr;  // -1 for an undecided row: the list passes write it
+    const unsigned long long m = __ballot(d < 0 && ulive && unp * U + lane < N);
+    const i64 tile = 2 * unp + (lane & 1);
+    unsigned long long* ma = ulive && tile < ntiles ? und_mask + tile : dummy;
+    *ma = (lane & 1) ? (m >> 32) : (m & 0xffffffffull);
+  };
+
+  // window win of the block's fp32 sums into its own partial slot (plain
+  // 16-byte stores, every slot written once: no atomics, no ordering), then
+  // cleared (all waves, between barriers); the slots are summed in a fixed
+  // order in fp64 after the kernel
+  auto flush = [&](int win) __attribute__((always_inline)) {
+    float* pb = part + ((i64)bk * nwin + win) * K * D;
+    for (int i = 4 * t; i < K * D; i += 4 * W * 64) {
+      const int d = i / D, c = i % D;
+      kb_f4* src = (kb_f4*)(sums + d * D + (c ^ (d & (D - 4))));
+      *(kb_f4*)(pb + i) = *src;
+      *src = (kb_f4){0.f, 0.f, 0.f, 0.f};
+    }
+  };
+
+#if KF2_PROF
+  unsigned long long pacc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, plast = __builtin_amdgcn_s_memtime();
+#define KF2_T(k)                                                   \
+  {                                                                \
+    const unsigned long long now = __builtin_amdgcn_s_memtime();  \
+    pacc[k] += now - plast;                                        \
+    plast = now;                                                   \
+  }
+#else
+#define KF2_T(k)
+#endif
+  const int nrun = nit > 0 ? (nit + NS) / NS * NS : 0;  // >= nit + 1: unit nit - 1 is added at iteration nit
+#if KF2_PRIO
+  // the younger wave of each SIMD pair gets the issue priority (arbitration
+  // otherwise favours the older one, which then waits at the barrier)
+  if (w >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
+  __syncthreads();  // sums, dl
+  if (nit > 0) {
+    // the loads in the order the loop keeps them in flight (two stores after
+    // each unit, as an iteration issues them), so the compiler's count of the
+    // loads outstanding at the loop head is the same on entry and on the back edge
+#pragma unroll
+    for (int r = 0; r < NS - 1; ++r) {
+      load(ring[r], r);
+      dummy[lane & 1] = 0ull;
+      dummy[lane & 1] = 0ull;
+    }
+    stage(ring[0], 0);
+  }
+  for (int it0 = 0; it0 < nrun; it0 += NS) {
+    ks_unroll([&](auto sc) __attribute__((always_inline)) {
+      constexpr int s = decltype(sc)::value;
+      constexpr int sp = (s + NS - 1) % NS, sn = (s + 1) % NS;  // slots of units it - 1 and it + 1
+      const int it = it0 + s;
+      KF2_T(0);
+      __syncthreads();
+      KF2_T(1);
+      if constexpr (s == 0)
+        if (it >= KF2_FW && it % KF2_FW == 0) {
+          flush(it / KF2_FW - 1);
+          __syncthreads();
+          __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        }
+      // (add_out outside the screen's branch: its stores on one path only,
+      // so the compiler keeps an exact count of the loads in flight)
+      kb_acc a0, a1;
+      const Rounds R = screen_tbl(a0, a1, (s + 1) % 2);
+      KF2_T(2);
+      out_labels(R.d, R.dlr, it);
+      KF2_T(3);
+      if (w < NCT) screen_fold(a0, a1);
+      KF2_T(4);
+      __syncthreads();
+      KF2_T(5);
+      add_begin(R);
+      decide(it, s % 2);
+      KF2_T(6);
+      add_end(R, ring[sp]);
+      KF2_T(7);
+      stage(ring[sn], (s + 1) % 2);
+      KF2_T(8);
+      load(ring[sp], it + NS - 1);  // unit it + 3 into the slot unit it - 1 left
+    }, std::make_integer_sequence<int, NS>{});
+  }
+#if KF2_PROF
+  if (lane == 0)
+    for (int k = 0; k < 9; ++k) g_kf2_prof[(blockIdx.x * W + w) * 9 + k] = pacc[k];
+#endif
+  __syncthreads();
+  {
+    // the last window (nrun - 1 >= nit: at least one loop iteration ran if
+    // nit > 0), then zero slots for windows this block does not have
+    const int wdone = nrun > 0 ? (nrun - 1) / KF2_FW : 0;
+    flush(wdone);
+    for (int win = wdone + 1; win < nwin; ++win)
+      for (int i = 4 * t; i < K * D; i += 4 * W * 64)
+        *(kb_f4*)(part + ((i64)bk * nwin + win) * K * D + i) = (kb_f4){0.f, 0.f, 0.f, 0.f};
+  }
+  if (t < K) pcnt[(i64)bk * K + t] = cnts[t];
+}
+
+template <int KS, int NCT>
+static void kf2_launch(hipStream_t s, int grid, i64 N, i64 K, const float* P, i64 ldp, const __bf16* CBh,
+                       const __bf16* CBl, const float* cnf2, const double* cmax, const float* muf, i64* labels,
+                       unsigned long long* und_mask, float* part, int nwin, unsigned long long* pcnt,
+                       unsigned long long* dummy) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_kmeans_fs2<KS, NCT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kf2_lds_bytes(16 * KS));
+    attr = true;
+  }
+  k_kmeans_fs2<KS, NCT><<<grid, KFS_WAVES * 64, kf2_lds_bytes(16 * KS), s>>>(
+      N, K, P, ldp, CBh, CBl, cnf2, cmax, muf, labels, und_mask, part, nwin, pcnt, dummy);
+}
+
+static void kf2_launch_n(int nct, int KS, hipStream_t s, int grid, i64 N, i64 K, const float* P, i64 ldp,
+                         const __bf16* CBh, const __bf16* CBl, const float* cnf2, const double* cmax, const float* muf,
+                         i64* labels, unsigned long long* und_mask, float* part, int nwin, unsigned long long* pcnt,
+                         unsigned long long* dummy) {
+#define KF2_CASE(KSV, NC)                                                                                         \
+  if (KS == KSV && nct == NC) {                                                                                   \
+    kf2_launch<KSV, NC>(s, grid, N, K, P, ldp, CBh, CBl, cnf2, cmax, muf, labels, und_mask, part, nwin, pcnt, dummy); \
+    return;                                                                                                       \
+  }
+  KF2_CASE(8, 8) KF2_CASE(8, 4) KF2_CASE(8, 2) KF2_CASE(8, 1)
+  KF2_CASE(4, 8) KF2_CASE(4, 4) KF2_CASE(4, 2) KF2_CASE(4, 1)
+#undef KF2_CASE
+}
+
 // Deterministic compaction of lane masks (LAYOUT 2: bit j <-> row 32 tile + j)
 // into an index-ordered row list: per-block counts, one exclusive scan, then
 // k_ks_compact at the scanned bases (the summation order of the gathered
@@ -3017,15 +3518,15 @@ __global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(4 * 
 
 // 256 lanes = 64 outputs x 4 g-slices; slice s sums g = s, s+4, ... in order,
 // then the four slice sums are added in order 0..3 (deterministic).
-template <typename T>
-__global__ __launch_bounds__(256) void k_kmeans_reduce(i64 n, i64 G, const T* __restrict__ part, T* __restrict__ out,
+template <typename T, typename P = T>
+__global__ __launch_bounds__(256) void k_kmeans_reduce(i64 n, i64 G, const P* __restrict__ part, T* __restrict__ out,
                                                        int add) {
   __shared__ T red[4][64];
   const int j = threadIdx.x & 63, sl = threadIdx.x >> 6;
   const i64 i = (i64)blockIdx.x * 64 + j;
   T s = T(0);
   if (i < n)
-    for (i64 g = sl; g < G; g += 4) s += part[g * n + i];
+    for (i64 g = sl; g < G; g += 4) s += (T)part[g * n + i];
   red[sl][j] = s;
   __syncthreads();
   if (sl == 0 && i < n) {
@@ -3318,12 +3819,26 @@ static i64 kfs_grid(i64 N) {  // one block per CU, at most one per 64-row unit
 
 static i64 kfs_nblk(i64 N) { return ((N + 31) / 32 + 256 * 16 - 1) / (256 * 16); }
 
+// windows of k_kmeans_fs2's fp32 partials per block (the block with the most units)
+static i64 kf2_nwin(i64 N) {
+  const i64 nunits = (N + 63) / 64, G = kfs_grid(N);
+  const i64 nit = (nunits + G - 1) / G, nrun = (nit + KF2_NS) / KF2_NS * KF2_NS;
+  return (nrun - 1) / KF2_FW + 1;
+}
+
+// bytes of the fused step's block partials: k_kmeans_fs2's fp32 windows (or
+// k_kmeans_fscreen's fp64 sums)
+static i64 kfs_part_bytes(i64 N, i64 D, i64 K) {
+  const i64 G = kfs_grid(N), a = G * kf2_nwin(N) * K * D * 4, b = G * K * D * 8;
+  return KFS_V2 ? a : b;
+}
+
 extern "C" int64_t spx_kmeans_step_workspace(int dtype, int64_t N, int64_t D, int64_t K) {
   const int64_t a = spx_kmeans_assign_workspace(dtype, N, D, K);
   const int64_t c = spx_kmeans_accumulate_workspace(dtype, N, D, K);
   if (a < 0 || c < 0) return -1;
   const i64 G = kfs_grid(N);
-  return (a + 255) / 256 * 256 + (c + 255) / 256 * 256 + G * K * D * 8 + G * K * 8 + (kfs_nblk(N) + 1) * 4 + 256;
+  return (a + 255) / 256 * 256 + (c + 255) / 256 * 256 + kfs_part_bytes(N, D, K) + G * K * 8 + (kfs_nblk(N) + 1) * 4 + 256;
 }
 
 extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
@@ -3350,7 +3865,7 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
   }
   const i64 Kp = kf_kp(K), G = kfs_grid(N), nb = kfs_nblk(N), ntiles = (N + 31) / 32;
   double* psumF = (double*)(wc + (nc + 255) / 256 * 256);
-  unsigned long long* pcntF = (unsigned long long*)(psumF + G * K * D);
+  unsigned long long* pcntF = (unsigned long long*)((unsigned char*)psumF + kfs_part_bytes(N, D, K));
   unsigned int* bcnt = (unsigned int*)(pcntF + G * K);
   const KmWs w = km_carve(wa, N, D, Kp);
   const int r32 = dist_dtype == SPX_F32;
@@ -3362,11 +3877,20 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
   float* cnf = (float*)w.cn;
   float* cnf2 = cnf + KF_BN;
   HIP_TRY(hipMemsetAsync(w.counters, 0, 4 * sizeof(unsigned int), S(stream)));
+#if !KFS_V2
   HIP_TRY(hipMemsetAsync(psumF, 0, (size_t)G * K * D * sizeof(double), S(stream)));
+#endif
   k_kmeans_prep_b3<<<1, 1024, 0, S(stream)>>>(D, K, 32 * nct, centers, CBh, CBl, cnf, w.cmax, mcoef, cnf2, w.muf);
   LAUNCH_CHECK("spx_kmeans_step(prep)");
+#if KFS_V2
+  unsigned long long* dummy = (unsigned long long*)(((uintptr_t)(bcnt + nb + 1) + 63) & ~(uintptr_t)63);
+  const i64 nwin = kf2_nwin(N);
+  kf2_launch_n(nct, (int)(D / 16), S(stream), (int)G, N, K, Pf, ldp, CBh, CBl, cnf2, w.cmax, w.muf, labels,
+               w.und_mask, (float*)psumF, (int)nwin, pcntF, dummy);
+#else
   kfs_launch_n(nct, (int)(D / 16), S(stream), (int)G, N, K, Pf, ldp, CBh, CBl, cnf2, w.cmax, w.muf, labels,
                      w.und_mask, psumF, pcntF);
+#endif
   LAUNCH_CHECK("spx_kmeans_step(fused screen + accumulate)");
   // the screen's undecided rows, in row order (the gathered accumulation's order)
   k_ks_count<16><<<(unsigned)nb, 256, 0, S(stream)>>>(N, w.und_mask, bcnt);
@@ -3386,7 +3910,12 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
       N, D, K, Pf, ldp, labels, psum2, pcnt2, (int)ndb, w.scr_list, w.counters + 3);
   LAUNCH_CHECK("spx_kmeans_step(accumulate undecided rows)");
   const i64 n = K * D;
+#if KFS_V2
+  k_kmeans_reduce<double, float><<<(unsigned)((n + 63) / 64), 256, 0, S(stream)>>>(n, G * nwin, (const float*)psumF,
+                                                                                   sums, zero_first ? 0 : 1);
+#else
   k_kmeans_reduce<double><<<(unsigned)((n + 63) / 64), 256, 0, S(stream)>>>(n, G, psumF, sums, zero_first ? 0 : 1);
+#endif
   k_kmeans_reduce<double><<<(unsigned)((n + 63) / 64), 256, 0, S(stream)>>>(n, G2, psum2, sums, 1);
   k_kmeans_reduce<unsigned long long><<<(unsigned)((K + 63) / 64), 256, 0, S(stream)>>>(
       K, G, pcntF, (unsigned long long*)counts, zero_first ? 0 : 1);

@@ -39,6 +39,10 @@ for s in $STEPS; do
     kmtrace)
       cd /tmp && step kmtrace 300 rocprofv3 --kernel-trace --stats -d $O/kmtrace -o p --output-format csv \
         -- python3 $R/bench.py --dot 0 --workloads kmeans --cpu-baseline 0 --steps 2 --warmup 1 > $O/kmtrace.log 2>&1 ;;
+    kstrace)
+      # kernel trace of the fused step alone (tools/km_step_once.py at cfg3, second-iteration centres)
+      cd /tmp && step kstrace 300 rocprofv3 --kernel-trace --stats -d $O/kstrace -o p --output-format csv \
+        -- python3 $R/tools/km_step_once.py 100000000 5 > $O/kstrace.log 2>&1 ;;
     kundtrace)
       cd /tmp && step kundtrace 300 rocprofv3 --kernel-trace --stats -d $O/kundtrace -o p --output-format csv \
         -- python3 $R/tools/km_und.py 100000000 > $O/kundtrace.log 2>&1 ;;

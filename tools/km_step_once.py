@@ -26,8 +26,12 @@ def main():
   sums = torch.empty((K, D), dtype=torch.float64, device=dev)
   cnt = torch.empty((K,), dtype=torch.int64, device=dev)
   cen = pts[:K].to(torch.float64).contiguous()
-  be.kmeans_step(pts, cen, lab, sums, cnt)
+  # second-iteration centres from the two-pass path, so that variant builds of
+  # the fused step are timed on the same centres whatever their sums
+  be.kmeans_assign(pts, cen, lab)
+  be.kmeans_accumulate(pts, lab, sums, cnt)
   cen = (sums / cnt.clamp(min=1).to(torch.float64).reshape(K, 1)).contiguous()
+  be.kmeans_step(pts, cen, lab, sums, cnt)
   torch.cuda.synchronize()
   ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
   ev[0].record()
