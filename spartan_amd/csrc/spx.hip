@@ -2038,7 +2038,7 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
 // KC_TPT tiles per thread: 16 for the sparse full-row pass (~5 % of rows at
 // cfg3), 1 for the dense list pass (~20 % of its slots): a thread's rows are
 // written one after another, so a dense mask wants few tiles per thread.
-// LAYOUT 2 (k_kmeans_fscreen): bit l < 32 <-> row 32 tile + l.  base_in (the
+// LAYOUT 2 (k_kmeans_fs2): bit l < 32 <-> row 32 tile + l.  base_in (the
 // deterministic form, k_ks_count + k_exscan_u32): the block's first list slot
 // instead of an atomic on cnt -- the list is then in row order.
 template <int KC_TPT, int LAYOUT = 0>
@@ -2085,7 +2085,7 @@ __global__ __launch_bounds__(256) void k_ks_compact(i64 N, const unsigned long l
       if (LAYOUT == 0) {  // 32x32 output layout (k_kmeans_filter_as)
         const int q = (l & 31) >> 1, h = l >> 5;
         slot = tl * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-      } else {  // point order (k_kmeans_fscreen)
+      } else {  // point order (k_kmeans_fs2)
         slot = tl * 32 + l;
       }
       out[pos++] = rows_in ? rows_in[slot] : slot;
@@ -2136,68 +2136,16 @@ static void ks_launch_n(int nct, hipStream_t s, i64 N, i64 D, const float* P, i6
 }
 
 // ---------------------------------------------------------------------------
-// Fused k-means step: the fp16 screen AND the centroid accumulation in ONE
-// pass over the points (spx_kmeans_step; kmeans_dist_mapper + argmin +
-// kmeans_count_mapper + kmeans_center_mapper, k_means_.py:52-89, 126-136).
-//
-// The A-stationary screen above holds a wave's 32-point tile in registers
-// and sweeps all 256 centres through it; its registers are full, so the
-// per-centre sums cannot live next to it and the accumulation had to read
-// the points a second time (51 GB at cfg3).  Here the roles are swapped
-// (B-stationary): wave w < NCT keeps ITS 32 centres in registers -- the MFMA A
-// operand, fp16(c') exactly as the screen stages them, plus the -cc/2 pieces
-// -- and every unit of 64 points (two 32-point MFMA tiles) passes through all
-// of the block's waves from LDS.  One loop iteration per unit, two barriers:
-//   phase 1   screen (waves < NCT): two independent chains of 8 fp16 MFMAs +
-//             1 bf16 MFMA (-cc/2) give the 32 x 32 blocks S - cc/2 = -a''/2
-//             of the unit's two tiles (rows = the wave's centres, columns =
-//             points); a per-lane top-2 over the lane's 16 centres, ONE
-//             half-swap that leaves lane (j, h) with tile h's point j, and
-//             (b1, b2, index) per point into LDS;
-//             accumulate (waves < NCT) the previous unit's decided rows whose
-//             centre the wave owns, from the fp32 rows in LDS, into fp32
-//             register sums (32 centres x D / 64 dims per lane), in point
-//             order, KFS_AR rows' LDS reads in flight at a time;
-//   phase 2   decide: wave w takes rows 8w .. 8w + 7, one lane per (row,
-//             centre wave): the top-2 over the NCT candidates by three DPP
-//             exchanges, then the certified rule of the screen (b1 - b2 >
-//             e(|x'|), the same bound kq and finiteness checks as
-//             k_kmeans_filter_as MODE 1, whose arithmetic this is with A and B
-//             exchanged) -- every row decided exactly once;
-//             stage the next unit: 512 threads convert it (32 KiB fp32, a
-//             register prefetch ring KFS_R units deep) to x' = fl(x - mu) and
-//             fp16(x') in LDS, |x'|^2 per row, and keep the raw fp32 rows.
-// Every KFS_FW units (a window) the labels / undecided flags buffered in LDS
-// go to global memory and every fp32 chain is added to the block's private
-// fp64 partial (no-return fp64 atomics, one writer per address, so program
-// order fixes the result: deterministic); a chain therefore spans at most the
-// rows one block sees of one centre in one window.  Keeping every global
-// store out of the unit loop lets the prefetch ring stay in flight across the
-// barriers (a pending store makes the compiler wait vmcnt(0) at each staging).
-// Undecided rows (near-ties, non-finite or fp16-overflowing rows) are not
-// added: they go through the list passes of spx_kmeans_assign and a gathered
-// accumulation afterwards.
+// Shared by the fused k-means step (k_kmeans_fs2 below): 8 waves per block,
+// 64-row units (two 32-row MFMA tiles), the per-screening-wave exchange rows
+// of the decision, the fp16 row stride and the DPP helpers.
 typedef float kfs_f2 __attribute__((ext_vector_type(2)));
 constexpr int KFS_WAVES = 8;
 constexpr int KFS_U = 64;  // rows per unit (two 32-row MFMA tiles)
-#ifndef KFS_RING
-#define KFS_RING 2  // prefetch ring depth in units (D / 8 floats per thread and unit, in registers)
-#endif
-constexpr int KFS_R = KFS_RING;
-constexpr int KFS_UN = KFS_R % 2 == 0 ? KFS_R : 2 * KFS_R;  // unroll: ring slot and fp32 buffer compile-time
-constexpr int KFS_FW = 120;
-#ifndef KFS_AR
-#define KFS_AR 8  // accumulated rows per round (their LDS reads issued together)
-#endif
 // exchange strides per screening wave: +64 B / +32 B so the 8 lanes of a
 // decide row group (one per screening wave) read 8 different bank groups
-constexpr int KFS_EXV_S = 2 * KFS_U + 16, KFS_EXI_S = KFS_U + 8;  // units per window (a multiple of KFS_UN): labels / flags in LDS, fp32 chains flushed
-static_assert(KFS_FW % KFS_UN == 0, "the drain points must fall on the unrolled body's first copy");
+constexpr int KFS_EXV_S = 2 * KFS_U + 16, KFS_EXI_S = KFS_U + 8;
 __host__ __device__ constexpr int kfs_rs(int D) { return 2 * D + 16; }  // fp16 row stride: +16 B keeps ds_read_b128 conflict-free
-static size_t kfs_lds_bytes(int D) {
-  return (size_t)2 * KFS_U * D * 4 + (size_t)KFS_U * kfs_rs(D) + 2 * KFS_U * 4 + (size_t)KFS_WAVES * (KFS_EXV_S + KFS_EXI_S) * 4 +
-         (size_t)D * 4 + KFS_U * 4 + (size_t)2 * KFS_FW * KFS_U * 2;
-}
 
 template <int CTL>
 __device__ __forceinline__ float kfs_dppf(float x) {
@@ -2208,428 +2156,58 @@ __device__ __forceinline__ int kfs_dppi(int x) {
   return __builtin_amdgcn_update_dpp(0, x, CTL, 0xF, 0xF, false);
 }
 
-template <int KS, int NCT>
-__global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fscreen(
-    i64 N, i64 K, const float* __restrict__ P, i64 ldp, const __bf16* __restrict__ CBh,
-    const __bf16* __restrict__ CBl, const float* __restrict__ cnf2, const double* cmax_p,
-    const float* __restrict__ muf, i64* __restrict__ labels, unsigned long long* __restrict__ und_mask,
-    double* __restrict__ psum, unsigned long long* __restrict__ pcnt) {
-  constexpr int D = 16 * KS, EPT = D / 8, DPL = D / 64, RS = kfs_rs(D), W = KFS_WAVES, U = KFS_U;
-  static_assert(EPT % 8 == 0 && (DPL == 1 || DPL == 2), "D = 64 or 128");
-  extern __shared__ __attribute__((aligned(16))) unsigned char kfs_lds[];
-  float* xs = (float*)kfs_lds;                                // [2][U][D] raw fp32 rows
-  unsigned char* xh = kfs_lds + (size_t)2 * U * D * 4;        // [U][RS] fp16 x'
-  float* p2s = (float*)(xh + (size_t)U * RS);                 // [2][U] |x'|^2
-  float* exv = p2s + 2 * U;                                   // [W][KFS_EXV_S] (b1, b2) per row
-  int* exi = (int*)(exv + W * KFS_EXV_S);                     // [W][KFS_EXI_S] best centre
-  float* mus = (float*)(exi + W * KFS_EXI_S);                 // [D] centre mean
-  int* dl = (int*)(mus + D);                                  // [U] decided label, -1: not decided
-  unsigned char* lab8 = (unsigned char*)(dl + U);             // [2 KFS_FW][U] labels (K <= 256)
-  unsigned char* und8 = lab8 + 2 * KFS_FW * U;                // [2 KFS_FW][U] undecided flags
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, j = lane & 31, h = lane >> 5;
-  for (int i = t; i < D; i += W * 64) mus[i] = muf[i];
-
-  // this wave's centres (A operand): lane (j, h) = centre 32 w + j, dims
-  // 16 ks + 8 h .. + 7 of k-step ks; fp16(hi + lo) as the screen stages them
-  kh_f8 ca[KS];
-  kb_bf8 ccp;
-  {
-    const i64 c = 32 * (i64)(w < NCT ? w : 0) + j;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const i64 d = 16 * ks + 8 * h + e;
-        ca[ks][e] = (_Float16)((float)CBh[c * D + d] + (float)CBl[c * D + d]);
-      }
-    // -cc/2 as three bf16 pieces (8 + 8 + 8 significant bits, exact) in the
-    // h = 0 lanes, zeros in the h = 1 lanes: one bf16 MFMA against ones adds it
-    const float v = -0.5f * cnf2[c];
-    const __bf16 b1 = (__bf16)v;
-    const float v1 = v - (float)b1;
-    const __bf16 b2 = (__bf16)v1;
-    const __bf16 b3 = (__bf16)(v1 - (float)b2);
-    const __bf16 z = (__bf16)0.f;
-    ccp = h == 0 ? (kb_bf8){b1, b2, b3, z, z, z, z, z} : (kb_bf8){z, z, z, z, z, z, z, z};
-  }
-  const __bf16 one = (__bf16)1.f;
-  const kb_bf8 ones = (kb_bf8){one, one, one, one, one, one, one, one};
-
-  // the certified bound of k_kmeans_filter_as MODE 1 (same arithmetic)
-  const double cmax = cmax_p[0], mcoef = cmax_p[1], mun = cmax_p[2], dcmax = cmax_p[3];
-  const double u32 = 5.9604644775390625e-08;
-  const double chain = 16.0 * (double)KS;
-  const double eS = (u32 * cmax + 4.8828125e-04 * cmax + 1.001 * dcmax +
-                     2.0 * (chain + 3.0) * u32 * 1.001 * (cmax + dcmax)) * 1.01;
-  double xk1 = 64.0 * u32 * cmax, xk0 = 32.0 * u32 * (cmax * cmax + 2.0 * mun * cmax);
-  xk0 += sqrt((double)D) * 1.1920928955078125e-07 * (cmax + dcmax) + (double)D * 3.552713678800501e-15;
-  // the 4-bit tag (15 ulp of |S - cc/2| <= |p| cmax + cm2 / 2, i.e. 30 eps (|p|
-  // cmax + cm2 / 2) in a'' units) where kc_coef's 8 eps amax covers 16 eps (..)
-  xk1 += 14.0 * 1.1920928955078125e-07 * cmax;
-  xk0 += 7.0 * 1.1920928955078125e-07 * (cmax * cmax + 2.0 * mun * cmax);
-  float kq[3];
-  kc_coef(eS, cmax, mun, mcoef, D, kq, xk1, xk0);
-  const bool cok = cmax * cmax < 1e36 && mun * cmax < 1e36 && cmax < 3.0e4 && dcmax == dcmax;
-  const float pn_lim = (float)(cmax > 0.0 ? 1e36 / cmax : 1e36);
-
-  const int G = gridDim.x, bk = blockIdx.x;
-  const i64 nunits = (N + U - 1) / U, ntiles = (N + 31) / 32;
-  const int nit = bk < nunits ? (int)((nunits - 1 - bk) / G + 1) : 0;
-  // this thread's slice of a unit: row t / 8, EPT columns from (t % 8) EPT
-  const int srow = t >> 3, scol = (t & 7) * EPT;
-  kb_f4 ring[KFS_R][EPT / 4];
-  auto load = [&](kb_f4 (&r)[EPT / 4], int it) __attribute__((always_inline)) {  // clamped: always a valid address
-    const i64 un = bk + (i64)(it < nit ? it : nit - 1) * G;
-    i64 row = un * U + srow;
-    row = row < N ? row : N - 1;
-    const float* p = P + row * ldp + scol;
-#pragma unroll
-    for (int q = 0; q < EPT / 4; ++q) r[q] = *(const kb_f4*)(p + 4 * q);
-  };
-  auto stage = [&](const kb_f4 (&r)[EPT / 4], int b) __attribute__((always_inline)) {  // ring slot -> LDS buffer b
-    float* xrow = xs + ((size_t)b * U + srow) * D + scol;
-    _Float16 hv[EPT];
-    kfs_f2 p2v = (kfs_f2){0.f, 0.f};
-#pragma unroll
-    for (int q = 0; q < EPT / 4; ++q) {
-      *(kb_f4*)(xrow + 4 * q) = r[q];
-      const kb_f4 mu4 = *(const kb_f4*)(mus + scol + 4 * q);
-#pragma unroll
-      for (int e = 0; e < 4; e += 2) {
-        // x' = fl(x - mu), as the screen (packed fp32: v_pk_add / v_pk_fma)
-        const kfs_f2 x = (kfs_f2){r[q][e], r[q][e + 1]} - (kfs_f2){mu4[e], mu4[e + 1]};
-        p2v = __builtin_elementwise_fma(x, x, p2v);
-        hv[4 * q + e] = (_Float16)x[0];
-        hv[4 * q + e + 1] = (_Float16)x[1];
-      }
-    }
-    unsigned char* hrow = xh + (size_t)srow * RS + 2 * scol;
-#pragma unroll
-    for (int g = 0; g < EPT / 8; ++g)
-      *(kh_f8*)(hrow + 16 * g) = (kh_f8){hv[8 * g], hv[8 * g + 1], hv[8 * g + 2], hv[8 * g + 3],
-                                         hv[8 * g + 4], hv[8 * g + 5], hv[8 * g + 6], hv[8 * g + 7]};
-    // the row's |x'|^2 over its 8 threads (quad_perm swaps, row_half_mirror:
-    // VALU moves, no LDS round trip); only the bound reads it (1.001 slack)
-    float p2 = p2v[0] + p2v[1];
-    p2 += kfs_dppf<0xB1>(p2);
-    p2 += kfs_dppf<0x4E>(p2);
-    p2 += kfs_dppf<0x141>(p2);
-    if ((t & 7) == 0) p2s[b * U + srow] = p2;
-  };
-
-  // fp32 sums of this wave's 32 centres: lane = DPL dims, register = centre
-  float s0[32], s1[32];
-#pragma unroll
-  for (int c = 0; c < 32; ++c) s0[c] = s1[c] = 0.f;
-  unsigned int cnt = 0u;  // lane c < 32: decided rows of centre 32 w + c in this block
-  double* pbase = psum + ((i64)bk * K + 32 * (i64)w) * D + DPL * lane;
-  auto flush = [&](int cl) __attribute__((always_inline)) {  // centre cl's fp32 chain into the block's fp64 partial
-    if (32 * w + cl < K) {
-      unsafeAtomicAdd(pbase + (i64)cl * D, (double)s0[cl]);
-      if constexpr (DPL == 2) unsafeAtomicAdd(pbase + (i64)cl * D + 1, (double)s1[cl]);
-    }
-  };
-
-  // top-2 of one accumulator block's 16 values per lane, each tagged with
-  // its register q in the 4 low mantissa bits (<= 15 ulp, priced in the
-  // bound: xk0 / xk1 above) so the fold carries its argument along.  Every
-  // element is copied out first: __builtin_bit_cast of an ext-vector element
-  // lvalue reads element 0 whatever the index.
-  auto fold16 = [&](const kb_acc& acc, float& lo, float& sec, int& il) __attribute__((always_inline)) {
-    float tv[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const float a = acc[q];
-      tv[q] = __builtin_bit_cast(float, (__builtin_bit_cast(unsigned int, a) & ~15u) | (unsigned int)q);
-    }
-    lo = ks_max(tv[0], tv[1]);
-    sec = ks_med3(tv[0], tv[1], -INFINITY);
-#pragma unroll
-    for (int q = 2; q < 16; q += 2) {
-      sec = ks_max(sec, ks_med3(lo, tv[q], tv[q + 1]));
-      lo = ks_max3(lo, tv[q], tv[q + 1]);
-    }
-    const unsigned int qb = __builtin_bit_cast(unsigned int, lo) & 15u;
-    il = 32 * w + (int)((qb & 3) + 8 * (qb >> 2)) + 4 * h;  // acc[q] is centre (q & 3) + 8 (q >> 2) + 4 h
-  };
-
-  // phase 1: the screen of the unit in xh (waves < NCT): (b1, b2, best) per
-  // point.  Split in two so the accumulation of the previous unit (VALU /
-  // LDS) runs while the matrix pipe works through the two MFMA chains.
-  auto screen_mfma = [&](kb_acc& a0, kb_acc& a1) __attribute__((always_inline)) {
-    const unsigned char* bpa = xh + (size_t)j * RS + 16 * h;
-    const unsigned char* bpb = bpa + (size_t)32 * RS;
-    a0 = (kb_acc){};
-    a1 = (kb_acc){};
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const kh_f8 va = *(const kh_f8*)(bpa + 32 * ks);
-      const kh_f8 vb = *(const kh_f8*)(bpb + 32 * ks);
-      a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[ks], va, a0, 0, 0, 0);
-      a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[ks], vb, a1, 0, 0, 0);
-    }
-    a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ccp, ones, a0, 0, 0, 0);
-    a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ccp, ones, a1, 0, 0, 0);
-  };
-  auto screen_fold = [&](const kb_acc& a0, const kb_acc& a1) __attribute__((always_inline)) {
-    float loa, seca, lob, secb;
-    int ila, ilb;
-    fold16(a0, loa, seca, ila);
-    fold16(a1, lob, secb, ilb);
-    // half-swap: lane (j, 0) keeps tile 0's point j and receives the other
-    // half's candidates for it; lane (j, 1) the same for tile 1 (every lane
-    // takes part in the exchange: a bpermute under a branch reads 0 from an
-    // inactive partner)
-    const float sl = h ? loa : lob, ss = h ? seca : secb;
-    const int si = h ? ila : ilb;
-    const float rl = __shfl_xor(sl, 32, 64), rs = __shfl_xor(ss, 32, 64);
-    const int ri = __shfl_xor(si, 32, 64);
-    const float ml = h ? lob : loa, ms = h ? secb : seca;
-    const int mi = h ? ilb : ila;
-    const float b1 = ks_max(ml, rl);
-    const float b2 = ks_med3(ml, rl, ks_max(ms, rs));
-    const int ib = ml >= rl ? mi : ri;  // equal tagged values: undecided anyway
-    // lane (j, h) holds unit row 32 h + j = lane
-    *(kfs_f2*)(exv + w * KFS_EXV_S + 2 * lane) = (kfs_f2){b1, b2};
-    exi[w * KFS_EXI_S + lane] = ib;
-  };
-
-  // phase 2: decision of unit it (its |x'|^2 in p2s[b]); wave w: rows 8 w .. + 7
-  auto decide = [&](int it, int b) __attribute__((always_inline)) {
-    const int r = lane >> 3, v = lane & 7, row = 8 * w + r;
-    float b1 = -INFINITY, b2 = -INFINITY;
-    int ib = 0;
-    if (v < NCT) {
-      const kfs_f2 e2 = *(const kfs_f2*)(exv + v * KFS_EXV_S + 2 * row);
-      b1 = e2[0];
-      b2 = e2[1];
-      ib = exi[v * KFS_EXI_S + row];
-    }
-    // top-2 over the row's 8 lanes: xor 1, xor 2 (quad_perm), then the
-    // other quad (row_half_mirror); equal tagged values leave b2 = b1
-    // (undecided), so which index survives a tie does not matter
-    auto merge = [&](auto ctl) __attribute__((always_inline)) {
-      constexpr int C = decltype(ctl)::value;
-      const float pb1 = kfs_dppf<C>(b1), pb2 = kfs_dppf<C>(b2);
-      const int pib = kfs_dppi<C>(ib);
-      b2 = ks_med3(b1, pb1, ks_max(b2, pb2));
-      ib = pb1 > b1 ? pib : ib;
-      b1 = ks_max(b1, pb1);
-    };
-    merge(std::integral_constant<int, 0xB1>{});
-    merge(std::integral_constant<int, 0x4E>{});
-    merge(std::integral_constant<int, 0x141>{});
-    const float p2f = p2s[b * U + row];
-    const float pn = __builtin_amdgcn_sqrtf(__builtin_fmaf(p2f, 1.001f, 1e-37f)) * 1.0001f;
-    const float e = __builtin_fmaf(__builtin_fmaf(kq[2], pn, kq[1]), pn, kq[0]) * 1.0001f;
-    const bool fin = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim && isfinite(b1) && isfinite(b2);
-    const i64 grow = (bk + (i64)it * G) * U + row;
-    const bool live = it < nit && grow < N;  // it >= nit: a ghost iteration
-    const bool dec = fin && b1 - b2 > 1.0001f * e;
-    if (v == 0) {
-      dl[row] = live && dec ? ib : -1;
-      // labels and the undecided flags go to the window buffers in LDS; no
-      // global store inside the unit loop (drain writes them)
-      if (it < nit) {
-        const int u = it % (2 * KFS_FW);
-        lab8[u * U + row] = (unsigned char)ib;
-        und8[u * U + row] = live && !dec ? 1 : 0;
-      }
-    }
-  };
-
-  // phase 1: the decided rows of the unit in xs[b] whose centre this wave
-  // owns (waves < NCT), in point order, KFS_AR rows' reads in flight per round
-  auto accumulate = [&](int b) __attribute__((always_inline)) {
-    const int d = dl[lane];
-    unsigned long long m = __ballot(d >= 0 && (d >> 5) == w);
-    const float* xb = xs + (size_t)b * U * D + DPL * lane;
-    while (m) {  // wave-uniform
-      int p[KFS_AR];
-      bool ok[KFS_AR];
-      p[0] = __builtin_ctzll(m);
-      ok[0] = true;
-      m &= m - 1;
-#pragma unroll
-      for (int k = 1; k < KFS_AR; ++k) {
-        ok[k] = m != 0;
-        p[k] = ok[k] ? __builtin_ctzll(m) : p[0];
-        if (ok[k]) m &= m - 1;
-      }
-      kfs_f2 x2[KFS_AR];
-      float x1[KFS_AR];
-#pragma unroll
-      for (int k = 0; k < KFS_AR; ++k) {
-        if constexpr (DPL == 2) x2[k] = *(const kfs_f2*)(xb + p[k] * D);
-        else x1[k] = xb[p[k] * D];
-      }
-#pragma unroll
-      for (int k = 0; k < KFS_AR; ++k) {
-        if (ok[k]) {
-          const int cl = __builtin_amdgcn_readlane(d, p[k]) & 31;
-          if constexpr (DPL == 2) {
-            s0[cl] += x2[k][0];
-            s1[cl] += x2[k][1];
-          } else {
-            s0[cl] += x1[k];
-          }
-          cnt += lane == cl ? 1u : 0u;
-        }
-      }
-    }
-  };
-
-  // window k (units k KFS_FW .. + KFS_FW) to global memory: labels of the
-  // decided rows, the undecided bits (two 32-row tiles per unit), and every
-  // fp32 chain into the block's fp64 partial; then wait for the stores, so
-  // that no store is pending while the prefetch ring is in flight
-  auto drain = [&](int k) __attribute__((always_inline)) {
-    const int i0 = k * KFS_FW, i1 = i0 + KFS_FW < nit ? i0 + KFS_FW : nit;
-    for (int ip = i0 + w; ip < i1; ip += W) {
-      const int u = ip % (2 * KFS_FW);
-      const i64 un = bk + (i64)ip * G;
-      const i64 row = un * U + lane;
-      const bool und = und8[u * U + lane] != 0;
-      const unsigned long long m = __ballot(und);
-      if (row < N && !und) labels[row] = lab8[u * U + lane];
-      if (lane == 0) {
-        und_mask[2 * un] = (unsigned int)m;  // bit l <-> row 32 (2 un) + l
-        if (2 * un + 1 < ntiles) und_mask[2 * un + 1] = (unsigned int)(m >> 32);
-      }
-    }
-    if (w < NCT) {
-#pragma unroll 1
-      for (int c = 0; c < 32; ++c) flush(c);  // rolled: the 64 converted sums are not all held at once
-#pragma unroll
-      for (int c = 0; c < 32; ++c) s0[c] = s1[c] = 0.f;  // unrolled: no indexed writes
-    }
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  };
-
-  // iterations it = 0 .. nrun - 1 (unit it screened and decided, unit it - 1
-  // accumulated, unit it + 1 staged): every unrolled copy issues its loads
-  // unconditionally (clamped addresses; iterations >= nit are ghosts whose
-  // rows are never live) -- a skipped load on any path makes the compiler's
-  // count of the loads in flight unknown, and it then drains the ring
-  const int nrun = nit > 0 ? (nit + KFS_UN) / KFS_UN * KFS_UN : 0;  // >= nit + 1
-  __syncthreads();  // mus
-  if (nit > 0) {
-    load(ring[0], 0);
-    stage(ring[0], 0);
-#pragma unroll
-    for (int r = 1; r <= KFS_R; ++r) load(ring[r % KFS_R], r);
-  }
-  for (int it0 = 0; it0 < nrun; it0 += KFS_UN) {
-    // unit T lives in ring slot T % KFS_R and fp32 buffer T % 2
-    ks_unroll([&](auto sc) __attribute__((always_inline)) {
-      constexpr int s = decltype(sc)::value;
-      constexpr int sl = (s + 1) % KFS_R, bc = s % 2, bn = (s + 1) % 2;
-      const int it = it0 + s;
-      __syncthreads();
-      // window k = it / KFS_FW - 1 is complete in LDS since this barrier
-      // (units <= it - 1 are decided); one drain site, s == 0
-      if constexpr (s == 0)
-        if (it >= KFS_FW && it % KFS_FW == 0) drain(it / KFS_FW - 1);
-      if (w < NCT) {
-        kb_acc a0, a1;
-        screen_mfma(a0, a1);
-        if (it >= 1) accumulate(bn);  // unit it - 1 (buffer (it - 1) % 2 = (it + 1) % 2)
-        screen_fold(a0, a1);
-      }
-      __syncthreads();
-      decide(it, bc);
-      stage(ring[sl], bn);
-      load(ring[sl], it + 1 + KFS_R);
-    }, std::make_integer_sequence<int, KFS_UN>{});
-  }
-  // the windows not drained yet: the last one, and the one before it when
-  // the loop ended before its drain point (a window drained twice writes the
-  // same labels again and flushes only what was added since)
-  __syncthreads();
-  if (nit > 0) {
-    const int last = (nit - 1) / KFS_FW;
-    if (last >= 1 && last * KFS_FW >= nrun) drain(last - 1);
-    drain(last);
-  }
-  if (w < NCT && lane < 32 && 32 * w + lane < K) pcnt[(i64)bk * K + 32 * w + lane] = cnt;
-}
-
-template <int KS, int NCT>
-static void kfs_launch(hipStream_t s, int grid, i64 N, i64 K, const float* P, i64 ldp, const __bf16* CBh,
-                       const __bf16* CBl, const float* cnf2, const double* cmax, const float* muf, i64* labels,
-                       unsigned long long* und_mask, double* psum, unsigned long long* pcnt) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_kmeans_fscreen<KS, NCT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kfs_lds_bytes(16 * KS));
-    attr = true;
-  }
-  k_kmeans_fscreen<KS, NCT><<<grid, KFS_WAVES * 64, kfs_lds_bytes(16 * KS), s>>>(
-      N, K, P, ldp, CBh, CBl, cnf2, cmax, muf, labels, und_mask, psum, pcnt);
-}
-
-static void kfs_launch_n(int nct, int KS, hipStream_t s, int grid, i64 N, i64 K, const float* P, i64 ldp,
-                         const __bf16* CBh, const __bf16* CBl, const float* cnf2, const double* cmax, const float* muf,
-                         i64* labels, unsigned long long* und_mask, double* psum, unsigned long long* pcnt) {
-#define KFS_CASE(KSV, NC)                                                                                   \
-  if (KS == KSV && nct == NC) {                                                                             \
-    kfs_launch<KSV, NC>(s, grid, N, K, P, ldp, CBh, CBl, cnf2, cmax, muf, labels, und_mask, psum, pcnt); \
-    return;                                                                                                 \
-  }
-  KFS_CASE(8, 8) KFS_CASE(8, 4) KFS_CASE(8, 2) KFS_CASE(8, 1)
-  KFS_CASE(4, 8) KFS_CASE(4, 4) KFS_CASE(4, 2) KFS_CASE(4, 1)
-#undef KFS_CASE
-}
-
 // ---------------------------------------------------------------------------
-// Fused k-means step, LDS-sum form (k_kmeans_fs2, the default of
-// spx_kmeans_step).  The same screen and decision as k_kmeans_fscreen (the
-// same fp16 / bf16 MFMAs, tags, top-2 and certified bound), but the
-// accumulation no longer goes through run-time-indexed registers (a
-// readlane, two s_set_gpr_idx pairs and their hazards per row and dim pair,
-// ~4 ms of the 20.5 ms kernel at cfg3):
-//   * the per-centre sums of the block live in LDS as fp32 [256][D] (128 KiB
-//     at D = 128; column XOR-swizzled by the centre so that the 64 rows of one
-//     add instruction spread over the banks) and the decided rows are added
-//     with no-return ds_add_f32 straight from the registers their loads
-//     landed in -- no fp32 row copy in LDS;
-//   * for that the unit is loaded column-split: wave w holds columns
-//     w D/8 .. + D/8 of ALL 64 rows (lane = row), so two lanes of one wave
-//     that add to the same address (two rows of one centre) are ordered by
-//     the LDS unit inside one instruction, waves never share an address, and
-//     the rows of one wave are added in unit order: the sums are
-//     deterministic without an owner wave per centre;
-//   * |x'|^2 comes as 8 column partials per row, summed in a fixed DPP tree
-//     in the decision (all 8 lanes of a row get the same bits);
-//   * labels (a coalesced 64 B store per wave) and the undecided-row mask go
-//     out one unit behind the decision from the label array in LDS; every
-//     store is issued unconditionally (ghost / tail rows write to a dummy
-//     word), so the compiler's count of the loads in flight stays static.
-// Every KF2_FW units the fp32 sums are added to the block's private fp64
-// partial (no-return fp64 atomics, one writer per address) and cleared: an
-// fp32 chain covers at most ~KF2_FW / 4 rows of one centre (~64 here).
-// Ring: unit u lives in register slot u % KF2_NS from its load (two units
-// ahead) through its staging until its add one iteration after its decision.
-#ifndef KF2_DEV
-#define KF2_DEV 0
-#endif
-#ifndef KFS_V2
-#define KFS_V2 1  // 1: spx_kmeans_step runs k_kmeans_fs2 (LDS sums), 0: k_kmeans_fscreen (register sums)
-#endif
+// Fused k-means step (k_kmeans_fs2): the fp16 screen AND the centroid
+// accumulation in ONE pass over the points (spx_kmeans_step;
+// kmeans_dist_mapper + argmin + kmeans_count_mapper + kmeans_center_mapper,
+// k_means_.py:52-89, 126-136).  One block per CU, 8 waves, one loop
+// iteration per 64-row unit, two barriers:
+//   phase 1   screen: wave w < NCT keeps ITS 32 centres in registers (the
+//             MFMA A operand, fp16(c') as k_kmeans_filter_as MODE 1 stages
+//             them, plus the -cc/2 pieces); two chains of 8 fp16 MFMAs + 1
+//             bf16 MFMA (-cc/2) over the unit's fp16 x' in LDS give S - cc/2
+//             = -a''/2 for 32 centres x 64 points; a per-lane top-2 over the
+//             lane's 16 centres (4-bit register tags, priced in the bound),
+//             a v_permlane32_swap half-swap, (b1, b2, index) per point to
+//             LDS.  Woven between the MFMAs: the table rounds of the previous
+//             unit's adds (below) and its label / undecided-bit stores;
+//   phase 2   decide: wave w takes rows 8w .. 8w + 7, one lane per (row,
+//             screening wave): top-2 over the NCT candidates by three DPP
+//             exchanges, then the certified rule b1 - b2 > e(|x'|) (the same
+//             bound, kq and finiteness checks as MODE 1); add the previous
+//             unit's decided rows into the LDS sums; stage the next unit
+//             (x' = fl(x - mu), fp16(x') to LDS, |x'|^2 partials).
+// Accumulation: the block's per-centre sums live in LDS as fp32 [256][D]
+// (128 KiB at D = 128; columns XOR-swizzled by the centre to spread the
+// banks).  The unit is loaded column-split -- wave w holds columns w D/8 ..
+// + D/8 of ALL 64 rows (lane = row) -- so a wave adds its rows straight from
+// the registers their loads landed in, and waves never share an address.
+// Two rows of one centre in one unit would race in a plain read-add-write
+// (LDS float atomics measured ~3.5x slower for the whole step), so the adds
+// go in rounds: a row joins round k when its lane wins its centre's slot in
+// the wave's byte table at the k-th write / read-back (one winner per centre
+// and round, the LDS unit's fixed choice); rounds 0 and 1 cover all but the
+// rare third row of a centre, which loops.  The order of every add is fixed:
+// the sums are deterministic.  |x'|^2 comes as 8 column partials per row,
+// summed in a fixed DPP tree (all 8 lanes of a row get the same bits).
+// Labels (a coalesced 64 B store per wave) and the undecided-row mask go
+// out one unit behind the decision; every global store is issued
+// unconditionally (ghost / tail rows write to a dummy word), so the
+// compiler's count of the loads in flight stays static.  Every KF2_FW units
+// the fp32 sums go by plain stores to the block's partial slot for that
+// window and are cleared (an fp32 chain covers ~KF2_FW / 4 rows of one
+// centre, ~64 here); the slots are summed in fp64 in a fixed order after the
+// kernel.  Ring: unit u lives in register slot u % KF2_NS from its load (two
+// units ahead) through its staging until its add one iteration after its
+// decision.
 constexpr int KF2_NS = 4;
-#ifndef KF2_FWV
-#define KF2_FWV 256
-#endif
-constexpr int KF2_FW = KF2_FWV;
+constexpr int KF2_FW = 256;
 static_assert(KF2_FW % KF2_NS == 0, "the flush points must fall on the unrolled body's first copy");
 static size_t kf2_lds_bytes(int D) {
   return (size_t)256 * D * 4 + 256 * 4 + (size_t)KFS_U * kfs_rs(D) + (size_t)2 * KFS_WAVES * KFS_U * 4 +
          (size_t)KFS_WAVES * (KFS_EXV_S + KFS_EXI_S) * 4 + KFS_U * 4 + KFS_WAVES * 256 + 64 * 16;
 }
 
-#ifndef KF2_PRIO
-#define KF2_PRIO 0
-#endif
 #ifndef KF2_PROF
 #define KF2_PROF 0  // dev builds: per-wave cycles per loop segment (s_memtime) -> spx_dev_kf2_prof
 #endif
@@ -2687,7 +2265,7 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
   const __bf16 one = (__bf16)1.f;
   const kb_bf8 ones = (kb_bf8){one, one, one, one, one, one, one, one};
 
-  // the certified bound of k_kmeans_fscreen / k_kmeans_filter_as MODE 1
+  // the certified bound of k_kmeans_filter_as MODE 1 (same arithmetic)
   const double cmax = cmax_p[0], mcoef = cmax_p[1], mun = cmax_p[2], dcmax = cmax_p[3];
   const double u32 = 5.9604644775390625e-08;
   const double chain = 16.0 * (double)KS;
@@ -2779,17 +2357,21 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
   };
 
   // decision of unit it (its |x'|^2 partials in p2p[b]); wave w: rows 8 w .. + 7
-  auto decide = [&](int it, int b) __attribute__((always_inline)) {
+  // (pre: issued after the decision's own LDS loads -- round 0's reads of
+  // the adds, whose latency the DPP chain then covers; issued before them,
+  // they would delay the decision's loads, which return in order behind them)
+  auto decide = [&](int it, int b, auto&& pre) __attribute__((always_inline)) {
     const int r = lane >> 3, v = lane & 7, row = 8 * w + r;
     float b1 = -INFINITY, b2 = -INFINITY;
     int ib = 0;
-    if (v < NCT) {
+    if (NCT == 8 || v < NCT) {
       const kfs_f2 e2 = *(const kfs_f2*)(exv + v * KFS_EXV_S + 2 * row);
       b1 = e2[0];
       b2 = e2[1];
       ib = exi[v * KFS_EXI_S + row];
     }
     float p2f = p2p[(b * W + v) * U + row];
+    pre();
     auto merge = [&](auto ctl) __attribute__((always_inline)) {
       constexpr int C = decltype(ctl)::value;
       const float pb1 = kfs_dppf<C>(b1), pb2 = kfs_dppf<C>(b2);
@@ -2983,11 +2565,6 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
 #define KF2_T(k)
 #endif
   const int nrun = nit > 0 ? (nit + NS) / NS * NS : 0;  // >= nit + 1: unit nit - 1 is added at iteration nit
-#if KF2_PRIO
-  // the younger wave of each SIMD pair gets the issue priority (arbitration
-  // otherwise favours the older one, which then waits at the barrier)
-  if (w >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
   __syncthreads();  // sums, dl
   if (nit > 0) {
     // the loads in the order the loop keeps them in flight (two stores after
@@ -3026,8 +2603,7 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
       KF2_T(4);
       __syncthreads();
       KF2_T(5);
-      add_begin(R);
-      decide(it, s % 2);
+      decide(it, s % 2, [&]() __attribute__((always_inline)) { add_begin(R); });
       KF2_T(6);
       add_end(R, ring[sp]);
       KF2_T(7);
@@ -3805,7 +3381,7 @@ extern "C" int spx_kmeans_accumulate(int dtype, int64_t N, int64_t D, int64_t K,
 // spx_kmeans_step = spx_kmeans_assign + spx_kmeans_accumulate with the same
 // results (labels bit for bit; counts exact; sums deterministic, within the
 // fp32-chain bound below of the fp64 sums) and, in the certified screen's
-// domain, ONE pass over the points for the decided rows: k_kmeans_fscreen
+// domain, ONE pass over the points for the decided rows: k_kmeans_fs2
 // labels and accumulates them; the rows it leaves undecided (a few %) are
 // listed in row order, resolved by km_resolve and accumulated by
 // k_kmeans_accum over that list.  Partials are combined in a fixed order.
@@ -3826,12 +3402,8 @@ static i64 kf2_nwin(i64 N) {
   return (nrun - 1) / KF2_FW + 1;
 }
 
-// bytes of the fused step's block partials: k_kmeans_fs2's fp32 windows (or
-// k_kmeans_fscreen's fp64 sums)
-static i64 kfs_part_bytes(i64 N, i64 D, i64 K) {
-  const i64 G = kfs_grid(N), a = G * kf2_nwin(N) * K * D * 4, b = G * K * D * 8;
-  return KFS_V2 ? a : b;
-}
+// bytes of the fused step's block partials (k_kmeans_fs2's fp32 windows)
+static i64 kfs_part_bytes(i64 N, i64 D, i64 K) { return kfs_grid(N) * kf2_nwin(N) * K * D * 4; }
 
 extern "C" int64_t spx_kmeans_step_workspace(int dtype, int64_t N, int64_t D, int64_t K) {
   const int64_t a = spx_kmeans_assign_workspace(dtype, N, D, K);
@@ -3864,8 +3436,8 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
     return spx_kmeans_accumulate(dtype, N, D, K, points, ldp, labels, sums, counts, zero_first, wc, (size_t)nc, stream);
   }
   const i64 Kp = kf_kp(K), G = kfs_grid(N), nb = kfs_nblk(N), ntiles = (N + 31) / 32;
-  double* psumF = (double*)(wc + (nc + 255) / 256 * 256);
-  unsigned long long* pcntF = (unsigned long long*)((unsigned char*)psumF + kfs_part_bytes(N, D, K));
+  float* partF = (float*)(wc + (nc + 255) / 256 * 256);
+  unsigned long long* pcntF = (unsigned long long*)((unsigned char*)partF + kfs_part_bytes(N, D, K));
   unsigned int* bcnt = (unsigned int*)(pcntF + G * K);
   const KmWs w = km_carve(wa, N, D, Kp);
   const int r32 = dist_dtype == SPX_F32;
@@ -3877,20 +3449,12 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
   float* cnf = (float*)w.cn;
   float* cnf2 = cnf + KF_BN;
   HIP_TRY(hipMemsetAsync(w.counters, 0, 4 * sizeof(unsigned int), S(stream)));
-#if !KFS_V2
-  HIP_TRY(hipMemsetAsync(psumF, 0, (size_t)G * K * D * sizeof(double), S(stream)));
-#endif
   k_kmeans_prep_b3<<<1, 1024, 0, S(stream)>>>(D, K, 32 * nct, centers, CBh, CBl, cnf, w.cmax, mcoef, cnf2, w.muf);
   LAUNCH_CHECK("spx_kmeans_step(prep)");
-#if KFS_V2
   unsigned long long* dummy = (unsigned long long*)(((uintptr_t)(bcnt + nb + 1) + 63) & ~(uintptr_t)63);
   const i64 nwin = kf2_nwin(N);
   kf2_launch_n(nct, (int)(D / 16), S(stream), (int)G, N, K, Pf, ldp, CBh, CBl, cnf2, w.cmax, w.muf, labels,
-               w.und_mask, (float*)psumF, (int)nwin, pcntF, dummy);
-#else
-  kfs_launch_n(nct, (int)(D / 16), S(stream), (int)G, N, K, Pf, ldp, CBh, CBl, cnf2, w.cmax, w.muf, labels,
-                     w.und_mask, psumF, pcntF);
-#endif
+               w.und_mask, partF, (int)nwin, pcntF, dummy);
   LAUNCH_CHECK("spx_kmeans_step(fused screen + accumulate)");
   // the screen's undecided rows, in row order (the gathered accumulation's order)
   k_ks_count<16><<<(unsigned)nb, 256, 0, S(stream)>>>(N, w.und_mask, bcnt);
@@ -3910,12 +3474,8 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
       N, D, K, Pf, ldp, labels, psum2, pcnt2, (int)ndb, w.scr_list, w.counters + 3);
   LAUNCH_CHECK("spx_kmeans_step(accumulate undecided rows)");
   const i64 n = K * D;
-#if KFS_V2
-  k_kmeans_reduce<double, float><<<(unsigned)((n + 63) / 64), 256, 0, S(stream)>>>(n, G * nwin, (const float*)psumF,
-                                                                                   sums, zero_first ? 0 : 1);
-#else
-  k_kmeans_reduce<double><<<(unsigned)((n + 63) / 64), 256, 0, S(stream)>>>(n, G, psumF, sums, zero_first ? 0 : 1);
-#endif
+  k_kmeans_reduce<double, float><<<(unsigned)((n + 63) / 64), 256, 0, S(stream)>>>(n, G * nwin, partF, sums,
+                                                                                   zero_first ? 0 : 1);
   k_kmeans_reduce<double><<<(unsigned)((n + 63) / 64), 256, 0, S(stream)>>>(n, G2, psum2, sums, 1);
   k_kmeans_reduce<unsigned long long><<<(unsigned)((K + 63) / 64), 256, 0, S(stream)>>>(
       K, G, pcntF, (unsigned long long*)counts, zero_first ? 0 : 1);
