@@ -2419,8 +2419,8 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
   struct Rounds {
     int d;          // the row's label (< 0: not decided)
     int dlr;        // label of row 8 w + lane / 8 (out_labels' store)
-    bool w0, w1;    // the row adds in round 0 / 1
-    bool more;      // the row adds after round 1
+    bool w0, w1, w2;  // the row adds in round 0 / 1 / 2
+    bool more;        // the row adds after round 2 (a centre's fourth row in a unit: rare)
   };
   auto screen_tbl = [&](kb_acc& a0, kb_acc& a1, int bp) __attribute__((always_inline)) {
     const bool scr = NCT == 8 || w < NCT;
@@ -2428,7 +2428,7 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
     const unsigned char* bpb = bpa + (size_t)32 * RS;
     a0 = (kb_acc){};
     a1 = (kb_acc){};
-    Rounds R{0, 0, false, false, false};
+    Rounds R{0, 0, false, false, false, false};
     bool act = false, rem = false;
     int tv = 0;  // the table byte read back (compared one step later)
     auto step = [&](auto kc) __attribute__((always_inline)) {
@@ -2449,7 +2449,13 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
         tv = tget(rem ? tb + R.d : tdum);
       } else if constexpr (k == 5) {
         R.w1 = rem & (tv == lane);
-        R.more = rem & !R.w1;
+        rem = rem & !R.w1;
+        tput(rem ? tb + R.d : tdum, lane);
+      } else if constexpr (k == 6) {
+        tv = tget(rem ? tb + R.d : tdum);
+      } else if constexpr (k == 7) {
+        R.w2 = rem & (tv == lane);
+        R.more = rem & !R.w2;
       }
     };
     // B fragments one k-step ahead: an MFMA's wait for its operands then
@@ -2469,10 +2475,10 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
       va = na;
       vb = nb;
       if constexpr (KS == 8) {
-        if constexpr (ks < 6) step(std::integral_constant<int, ks>{});
+        step(std::integral_constant<int, ks>{});
       } else {
         step(std::integral_constant<int, 2 * ks>{});
-        if constexpr (2 * ks + 1 < 6) step(std::integral_constant<int, 2 * ks + 1>{});
+        step(std::integral_constant<int, 2 * ks + 1>{});
       }
       __builtin_amdgcn_sched_barrier(0);
     };
@@ -2489,12 +2495,14 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
   // Round 0's reads are issued before the decision of unit it (add_begin),
   // whose DPP chain then covers their latency.
   kb_f4 v0[CPW / 4];
+  unsigned int c0 = 0;
   auto add_begin = [&](const Rounds& R) __attribute__((always_inline)) {
     if (R.w0) {
       float* const srow = sums + R.d * D;
       const int sw = R.d & (D - 4);  // XOR by a multiple of 4: the lane's 4-column groups stay whole
 #pragma unroll
       for (int q = 0; q < CPW / 4; ++q) v0[q] = *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw));
+      if (w == 0) c0 = cnts[R.d];
     }
   };
   auto add_end = [&](const Rounds& R, const kb_f4 (&r)[CPW / 4]) __attribute__((always_inline)) {
@@ -2503,17 +2511,19 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
     if (R.w0) {
 #pragma unroll
       for (int q = 0; q < CPW / 4; ++q) *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw)) = v0[q] + r[q];
-      if (w == 0) cnts[R.d] += 1u;
+      if (w == 0) cnts[R.d] = c0 + 1u;
     }
     auto rmw = [&]() __attribute__((always_inline)) {
       kb_f4 v[CPW / 4];
 #pragma unroll
       for (int q = 0; q < CPW / 4; ++q) v[q] = *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw));
+      const unsigned int cv = w == 0 ? cnts[R.d] : 0u;
 #pragma unroll
       for (int q = 0; q < CPW / 4; ++q) *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw)) = v[q] + r[q];
-      if (w == 0) cnts[R.d] += 1u;
+      if (w == 0) cnts[R.d] = cv + 1u;
     };
     if (R.w1) rmw();
+    if (R.w2) rmw();
     bool more = R.more;
     while (__ballot(more)) {
       tput(more ? tb + R.d : tdum, lane);
@@ -3115,6 +3125,34 @@ __global__ __launch_bounds__(256) void k_kmeans_reduce(i64 n, i64 G, const P* __
   }
 }
 
+// Many fp32 partial slots (k_kmeans_fs2's windows: G x nwin = 6144 at cfg3,
+// 805 MB) -> KR_S fp64 slice sums: slice s adds slots s, s + KR_S, ... in
+// order, 4 consecutive elements per thread (16-byte loads, a wave reads 1 KiB
+// of one slot), so ~1 K blocks keep the stream busy where one thread per
+// output of k_kmeans_reduce ran latency-bound (0.63 ms at cfg3); the slices
+// then go through k_kmeans_reduce in a fixed order.  n % 4 == 0.
+constexpr int KR_S = 32;
+__global__ __launch_bounds__(256) void k_kmeans_slices(i64 n, i64 P, const float* __restrict__ part,
+                                                       double* __restrict__ out) {
+  const i64 e = ((i64)blockIdx.x * 256 + threadIdx.x) * 4;
+  const int sl = blockIdx.y;
+  if (e >= n) return;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+#pragma unroll 8
+  for (i64 p = sl; p < P; p += KR_S) {
+    const kb_f4 v = ld_stream((const kb_f4*)(part + p * n + e));
+    a0 += (double)v[0];
+    a1 += (double)v[1];
+    a2 += (double)v[2];
+    a3 += (double)v[3];
+  }
+  double* o = out + (i64)sl * n + e;
+  o[0] = a0;
+  o[1] = a1;
+  o[2] = a2;
+  o[3] = a3;
+}
+
 // Grid of the accumulation for (N, D, K): x = G point-chunk streams, y = tiles.
 static void ka_grid(int dtype, i64 N, i64 D, i64 K, i64* G, i64* ndb, i64* ncb) {
   const i64 ch = KA_THREADS * (dtype == SPX_F32 ? 4 : 2) / KA_DB;  // points per chunk (k_kmeans_accum CH)
@@ -3410,7 +3448,8 @@ extern "C" int64_t spx_kmeans_step_workspace(int dtype, int64_t N, int64_t D, in
   const int64_t c = spx_kmeans_accumulate_workspace(dtype, N, D, K);
   if (a < 0 || c < 0) return -1;
   const i64 G = kfs_grid(N);
-  return (a + 255) / 256 * 256 + (c + 255) / 256 * 256 + kfs_part_bytes(N, D, K) + G * K * 8 + (kfs_nblk(N) + 1) * 4 + 256;
+  return (a + 255) / 256 * 256 + (c + 255) / 256 * 256 + kfs_part_bytes(N, D, K) + G * K * 8 + (kfs_nblk(N) + 1) * 4 + 512 +
+         (int64_t)KR_S * K * D * 8;
 }
 
 extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
@@ -3465,6 +3504,8 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
   int rc = km_resolve(S(stream), N, D, K, Pf, ldp, centers, labels, w, nct, r32);
   if (rc) return rc;
   // the undecided rows' sums and counts, gathered through the row list
+  // (an LDS-sum form of this pass, k_kmeans_fs2's adds over gathered 64-row
+  // units, measured 1.18-2.27 ms against this kernel's 1.1 ms: not kept)
   i64 G2, ndb, ncb;
   ka_grid(dtype, N, D, K, &G2, &ndb, &ncb);
   if (ndb * ncb > 65535) return set_err(SPX_ENOTSUP, "spx_kmeans_step: K*D too large");
@@ -3474,8 +3515,16 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
       N, D, K, Pf, ldp, labels, psum2, pcnt2, (int)ndb, w.scr_list, w.counters + 3);
   LAUNCH_CHECK("spx_kmeans_step(accumulate undecided rows)");
   const i64 n = K * D;
-  k_kmeans_reduce<double, float><<<(unsigned)((n + 63) / 64), 256, 0, S(stream)>>>(n, G * nwin, partF, sums,
-                                                                                   zero_first ? 0 : 1);
+  // the slice sums live past the compaction counts and the dummy word
+  double* slices = (double*)(((uintptr_t)(bcnt + nb + 1) + 64 + 255) & ~(uintptr_t)255);
+  if (n % 4 == 0) {
+    k_kmeans_slices<<<dim3((unsigned)((n / 4 + 255) / 256), KR_S), 256, 0, S(stream)>>>(n, G * nwin, partF, slices);
+    k_kmeans_reduce<double><<<(unsigned)((n + 63) / 64), 256, 0, S(stream)>>>(n, KR_S, slices, sums,
+                                                                              zero_first ? 0 : 1);
+  } else {
+    k_kmeans_reduce<double, float><<<(unsigned)((n + 63) / 64), 256, 0, S(stream)>>>(n, G * nwin, partF, sums,
+                                                                                     zero_first ? 0 : 1);
+  }
   k_kmeans_reduce<double><<<(unsigned)((n + 63) / 64), 256, 0, S(stream)>>>(n, G2, psum2, sums, 1);
   k_kmeans_reduce<unsigned long long><<<(unsigned)((K + 63) / 64), 256, 0, S(stream)>>>(
       K, G, pcntF, (unsigned long long*)counts, zero_first ? 0 : 1);
