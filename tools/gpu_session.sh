@@ -30,6 +30,8 @@ for s in $STEPS; do
     tests)
       cd $R && step tests 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
         -p no:cacheprovider > $O/pytest.log 2>&1 ;;
+    smoke)
+      cd $R && step smoke 300 python3 -c 'import __graft_entry__ as g; g.smoke(); print("smoke ok")' > $O/smoke.log 2>&1 ;;
     kmtests)
       cd $R && step kmtests 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
         -p no:cacheprovider -k "kmeans" > $O/kmtests.log 2>&1 ;;
