@@ -2142,9 +2142,11 @@ static void ks_launch_n(int nct, hipStream_t s, i64 N, i64 D, const float* P, i6
 typedef float kfs_f2 __attribute__((ext_vector_type(2)));
 constexpr int KFS_WAVES = 8;
 constexpr int KFS_U = 64;  // rows per unit (two 32-row MFMA tiles)
-// exchange strides per screening wave: +64 B / +32 B so the 8 lanes of a
+// exchange strides per screening wave: +32 B / +32 B so the 8 lanes of a
 // decide row group (one per screening wave) read 8 different bank groups
-constexpr int KFS_EXV_S = 2 * KFS_U + 16, KFS_EXI_S = KFS_U + 8;
+// (ds_read_b64: bank (a / 4) mod 64, ds_read_b32: mod 32)
+constexpr int KFS_EXV_S = 2 * KFS_U + 8, KFS_EXI_S = KFS_U + 8;
+constexpr int KFS_PU = KFS_U + 4;  // |x'|^2 partial rows per wave: +16 B, the same for the decision's p2 reads
 __host__ __device__ constexpr int kfs_rs(int D) { return 2 * D + 16; }  // fp16 row stride: +16 B keeps ds_read_b128 conflict-free
 
 template <int CTL>
@@ -2204,8 +2206,8 @@ constexpr int KF2_NS = 4;
 constexpr int KF2_FW = 256;
 static_assert(KF2_FW % KF2_NS == 0, "the flush points must fall on the unrolled body's first copy");
 static size_t kf2_lds_bytes(int D) {
-  return (size_t)256 * D * 4 + 256 * 4 + (size_t)KFS_U * kfs_rs(D) + (size_t)2 * KFS_WAVES * KFS_U * 4 +
-         (size_t)KFS_WAVES * (KFS_EXV_S + KFS_EXI_S) * 4 + KFS_U * 4 + KFS_WAVES * 256 + 64 * 16;
+  return (size_t)256 * D * 4 + 256 * 4 + (size_t)KFS_U * kfs_rs(D) + (size_t)2 * KFS_WAVES * KFS_PU * 4 +
+         (size_t)KFS_WAVES * (KFS_EXV_S + KFS_EXI_S) * 4 + KFS_U * 4 + KFS_WAVES * 256 + 64;
 }
 
 #ifndef KF2_PROF
@@ -2229,12 +2231,12 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
   float* sums = (float*)kf2_lds;                         // [256][D] fp32, column c of centre d at c ^ (d & (D - 4))
   unsigned int* cnts = (unsigned int*)(sums + 256 * D);  // [256] decided rows per centre
   unsigned char* xh = (unsigned char*)(cnts + 256);      // [U][RS] fp16 x'
-  float* p2p = (float*)(xh + (size_t)U * RS);            // [2][W][U] |x'|^2 over wave w's columns
-  float* exv = p2p + 2 * W * U;                          // [W][KFS_EXV_S] (b1, b2) per row
+  float* p2p = (float*)(xh + (size_t)U * RS);            // [2][W][KFS_PU] |x'|^2 over wave w's columns
+  float* exv = p2p + 2 * W * KFS_PU;                     // [W][KFS_EXV_S] (b1, b2) per row
   int* exi = (int*)(exv + W * KFS_EXV_S);                // [W][KFS_EXI_S] best centre
   short* dl = (short*)(exi + W * KFS_EXI_S);             // [2][U] label of a decided row, -1 otherwise (by unit parity)
   unsigned char* tbl = (unsigned char*)(dl + 2 * U);       // [W][256] per-wave winner table of the add rounds
-  float* ldum = (float*)(tbl + W * 256);                 // [64][4] per-lane dummy slot of the straight-line rounds
+  unsigned char* ldum = tbl + W * 256;                   // [64] per-lane dummy byte of the straight-line table rounds
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, j = lane & 31, h = lane >> 5;
   const int col0 = w * CPW;
   for (int i = t; i < 256 * D + 256; i += W * 64) sums[i] = 0.f;  // (cnts: the same bits)
@@ -2309,7 +2311,7 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
     for (int g = 0; g < CPW / 8; ++g)
       *(kh_f8*)(hrow + 16 * g) = (kh_f8){hv[8 * g], hv[8 * g + 1], hv[8 * g + 2], hv[8 * g + 3],
                                          hv[8 * g + 4], hv[8 * g + 5], hv[8 * g + 6], hv[8 * g + 7]};
-    p2p[(b * W + w) * U + lane] = p2v[0] + p2v[1];
+    p2p[(b * W + w) * KFS_PU + lane] = p2v[0] + p2v[1];
   };
 
   auto fold16 = [&](const kb_acc& acc, float& lo, float& sec, int& il) __attribute__((always_inline)) {
@@ -2370,7 +2372,7 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
       b2 = e2[1];
       ib = exi[v * KFS_EXI_S + row];
     }
-    float p2f = p2p[(b * W + v) * U + row];
+    float p2f = p2p[(b * W + v) * KFS_PU + row];
     pre();
     auto merge = [&](auto ctl) __attribute__((always_inline)) {
       constexpr int C = decltype(ctl)::value;
@@ -2413,7 +2415,7 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
   auto tget = [](lds_u8* p) __attribute__((always_inline)) {
     return (int)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
-  float* const dum = ldum + 4 * lane;
+  unsigned char* const dum = ldum + lane;
   lds_u8* const tb = (lds_u8*)(tbl + w * 256);
   lds_u8* const tdum = (lds_u8*)dum;
   struct Rounds {

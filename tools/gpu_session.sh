@@ -55,6 +55,11 @@ for s in $STEPS; do
         -d $O/kfs_a -o p --output-format csv -- python3 $R/tools/km_step_once.py 100000000 2 > $O/kfs_a.log 2>&1
       step kfs_b 120 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_VALU_MFMA_BUSY_CYCLES SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE \
         -d $O/kfs_b -o p --output-format csv -- python3 $R/tools/km_step_once.py 100000000 2 > $O/kfs_b.log 2>&1 ;;
+    kfslds)
+      # LDS counters over the fused k-means step (bank conflicts vs all LDS-array cycles)
+      cd /tmp
+      step kfs_lds 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_WAVES GRBM_GUI_ACTIVE \
+        -d $O/kfs_lds -o p --output-format csv -- python3 $R/tools/km_step_once.py 100000000 2 > $O/kfs_lds.log 2>&1 ;;
     lregtune)
       cd $R && step lregtune 300 ./tools/bin/lreg_tune 100000000 3 > $O/lregtune.txt 2>&1 ;;
     gemmseg)
