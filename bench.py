@@ -482,9 +482,10 @@ def bench_lreg(npts, ctx, expr, comm, sync, D=64, iters=30):
   out = {'ms_per_iter': round(el * 1e3, 3), 'algorithmic_GBps': round(nbytes / el / 1e9, 1),
          'hbm_frac_per_gpu': round(nbytes / el / 1e9 / (HBM_PEAK_GBS * ctx.world_size), 4),
          'checked': checked,
-         'config': 'cfg5: X %d x %d fp32, y %d x 1, w 64 x 1 host; grad = sum(x * (dot(x, w) - y), axis=0): '
-                   'dot folded into the fused axis-0 reduction (one pass over X) + all-reduce of 64 fp32'
-                   % (n, D, n)}
+         'config': 'cfg5: X %d x %d fp32, y %d x 1, w 64 x 1 (device-resident between iterations, '
+                   'w - grad * alpha as a device map: no per-iteration host round trip); grad = sum(x * (dot(x, '
+                   'w) - y), axis=0): dot folded into the fused axis-0 reduction (one pass over X) + all-reduce of '
+                   '64 fp32' % (n, D, n)}
   del X, Y, Xe, Ye
   torch.cuda.empty_cache()
   return out

@@ -121,8 +121,9 @@ def _subst(op, var, repl):
 
 
 class DotReduceFusion(OptimizePass):
-  """reduce(f(x, dot(x, w)), axis=0) with a small host (K, 1) operand ``w``
-  -> one fused kernel that reads ``x`` once.
+  """reduce(f(x, dot(x, w)), axis=0) with a small (K, 1) operand ``w`` (a
+  host array, or a device-resident array / expression) -> one fused kernel
+  that reads ``x`` once.
 
   The reference evaluates ``dot(x, w)`` as its own pass (dot_map2_np_mapper,
   spartan/expr/dot.py:172-187), materialising yp, and the map+reduce that
@@ -153,12 +154,16 @@ class DotReduceFusion(OptimizePass):
       if not isinstance(d, DotExpr):  # (its tile_hint is moot: a fused dot has no output array)
         continue
       w, a = d.matrix_b, d.matrix_a
-      if not isinstance(w, np.ndarray) or w.ndim != 2 or w.shape[1] != 1:
+      # w: a host (K, 1) array, or a device-resident (K, 1) array / expression
+      # (an iterative driver that keeps w on the GPU: no host round trip)
+      host = isinstance(w, np.ndarray)
+      wshape = tuple(w.shape) if host or isinstance(w, Expr) else None
+      if wshape is None or len(wshape) != 2 or wshape[1] != 1:
         continue
-      K = w.shape[0]
+      K = wshape[0]
       if not (2 <= K <= ROWDOT_MAX_K) or tuple(a.shape) != it_shape or it_shape[1] != K:
         continue
-      if w.dtype.kind != 'f' or np.dtype(a.dtype) != w.dtype:
+      if np.dtype(w.dtype).kind != 'f' or np.dtype(a.dtype) != np.dtype(w.dtype):
         continue
       var_a = None
       for c, v in zip(vals, vars_):
@@ -170,7 +175,11 @@ class DotReduceFusion(OptimizePass):
         vals.append(a)
         vars_.append(var_a)
       var_w = make_var()
-      vals.append(AsArray(val=np.ascontiguousarray(w.reshape(1, K))))
+      if host:
+        vals.append(AsArray(val=np.ascontiguousarray(w.reshape(1, K))))
+      else:
+        from .reshape import reshape
+        vals.append(reshape(w, (1, K)))
       vars_.append(var_w)
       op = _subst(op, vars_[i], LocalRowDot(deps=[LocalInput(var_a), LocalInput(var_w)]))
       vals[i] = None

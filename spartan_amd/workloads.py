@@ -28,11 +28,27 @@ def linear_regression_update(x, y, w, alpha):
   return w - grad * alpha
 
 
-def sgd_train(x, y, w, alpha, iterations):
-  """SGDRegressor.train (sgd.py:34-39): repeated full-batch updates."""
+def sgd_train(x, y, w, alpha, iterations, device_w=True):
+  """SGDRegressor.train (sgd.py:34-39): repeated full-batch updates.
+
+  ``device_w`` (default): w stays on the GPU between iterations -- the same
+  update ``w - grad * alpha`` in the same fp32 operations (bit-identical to
+  the host form, linear_regression_update), but as a device map, so no
+  iteration waits for a device-to-host copy of the gradient and the host
+  builds iteration i + 1 while the GPU runs iteration i.  w comes back to
+  the host once, at the end.  ``device_w=False``: the reference's form, one
+  host round trip per iteration."""
+  if not device_w:
+    for _ in range(iterations):
+      w = linear_regression_update(x, y, w, alpha)
+    return w
+  w = np.asarray(w)
+  W = expr.from_numpy(w)
   for _ in range(iterations):
-    w = linear_regression_update(x, y, w, alpha)
-  return w
+    W = expr.lazify(W)
+    grad = expr.sum(x * (expr.dot(x, W) - y), axis=0)
+    W = (W - expr.reshape(grad, w.shape) * alpha).optimized().force()
+  return expr.glom(W)
 
 
 def kmeans_fit(X, n_clusters, n_iter, centers=None, seed=0, info=None):

@@ -188,6 +188,34 @@ def test_dot_reduce_fusion_rewrites_lreg(host_ctx):
     FLAGS.opt_dot_fusion = True
 
 
+def test_dot_reduce_fusion_device_w(host_ctx):
+  """DotReduceFusion with w a device-resident (K, 1) array (sgd_train keeps w
+  on the GPU): the dot is still folded into the axis-0 reduction, and the
+  device-w SGD loop is bit-identical to the host form (the same fp32 update,
+  linear_regression_update) -- it only drops the per-iteration host round
+  trip."""
+  host_ctx(3)
+  from spartan_amd import expr, workloads
+  from spartan_amd.expr.dot import DotExpr
+  from spartan_amd.expr.reduce import ReduceExpr
+  n, d = 300, 16
+  X = rng.rand((n, d), 41, np.float32)
+  Yv = rng.rand((n, 1), 42, np.float32)
+  w = rng.rand((d, 1), 43, np.float32)
+  x = expr.lazify(expr.from_numpy(X).force())
+  y = expr.lazify(expr.from_numpy(Yv).force())
+  W = expr.lazify(expr.from_numpy(w).force())
+  opt = expr.sum(x * (expr.dot(x, W) - y), axis=0).optimized()
+  assert isinstance(opt, ReduceExpr)
+  assert not any(isinstance(c, DotExpr) for c in opt.children)
+  assert 'rowdot' in opt.op.pretty_str()
+  np.testing.assert_array_equal(opt.glom(), expr.sum(x * (expr.dot(x, w) - y), axis=0).optimized().glom())
+  w_dev = workloads.sgd_train(x, y, w, 1e-3, 5)
+  w_host = workloads.sgd_train(x, y, w, 1e-3, 5, device_w=False)
+  assert w_dev.dtype == w_host.dtype and w_dev.shape == w_host.shape
+  np.testing.assert_array_equal(w_dev, w_host)
+
+
 def test_automatic_tiling(host_ctx):
   """AutomaticTiling (optimize.py:454-890): a new 2-d array reduced over axis
   0 is partitioned by columns (each worker reduces whole columns: no partial

@@ -32,6 +32,11 @@ for s in $STEPS; do
         -p no:cacheprovider > $O/pytest.log 2>&1 ;;
     smoke)
       cd $R && step smoke 300 python3 -c 'import __graft_entry__ as g; g.smoke(); print("smoke ok")' > $O/smoke.log 2>&1 ;;
+    lregtests)
+      cd $R && step lregtests 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+        -p no:cacheprovider -k "sgd or lreg or golden or dot_reduce" > $O/lregtests.log 2>&1 ;;
+    lregbench)
+      cd $R && step lregbench 600 python3 bench.py --dot 0 --workloads lreg --cpu-baseline 0 > $O/lregbench.json 2> $O/lregbench.err ;;
     kmtests)
       cd $R && step kmtests 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
         -p no:cacheprovider -k "kmeans" > $O/kmtests.log 2>&1 ;;
