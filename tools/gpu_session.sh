@@ -74,6 +74,9 @@ for s in $STEPS; do
     trace2)
       cd /tmp && step trace2 300 rocprofv3 --kernel-trace --stats -d $O/trace2 -o p --output-format csv \
         -- python3 $R/bench.py --dot 0 --workloads 0 --cpu-baseline 0 --steps 20 --warmup 5 > $O/trace2.log 2>&1 ;;
+    traceall)
+      cd /tmp && step traceall 600 rocprofv3 --kernel-trace --stats -d $O/traceall -o p --output-format csv \
+        -- python3 $R/bench.py --cpu-baseline 0 --steps 5 --warmup 1 > $O/traceall.log 2>&1 ;;
     trace5)
       cd /tmp && step trace5 300 rocprofv3 --kernel-trace --stats -d $O/trace5 -o p --output-format csv \
         -- python3 $R/bench.py --dot 0 --workloads lreg --cpu-baseline 0 --steps 2 --warmup 1 > $O/trace5.log 2>&1 ;;
