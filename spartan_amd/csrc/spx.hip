@@ -2526,13 +2526,27 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
     };
     if (R.w1) rmw();
     if (R.w2) rmw();
-    bool more = R.more;
-    while (__ballot(more)) {
-      tput(more ? tb + R.d : tdum, lane);
-      if (more && tget(tb + R.d) == lane) {
-        rmw();
-        more = false;
+    // The rest (a centre's fourth and later rows: rare once the centres have
+    // moved, a few per unit in a first iteration from data-point centres,
+    // whose labels are skewed): each row's rank among its centre's remaining
+    // rows, from ballots over the distinct labels (scalar loop, no LDS), then
+    // one read-add-write round per rank.  A wave's LDS operations run in
+    // issue order, so round k + 1 reads what round k wrote.
+    const unsigned long long mm = __ballot(R.more);
+    if (mm) {
+      int rk = 0, kmax = 0;
+      unsigned long long left = mm;
+      while (left) {
+        const int L = __builtin_amdgcn_readlane(R.d, __builtin_ctzll(left));
+        const bool in = R.more && R.d == L;
+        const unsigned long long g = __ballot(in);
+        left &= ~g;
+        if (in) rk = __builtin_amdgcn_mbcnt_hi((unsigned)(g >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)g, 0u));
+        const int gk = __popcll(g) - 1;
+        kmax = gk > kmax ? gk : kmax;
       }
+      for (int k = 0; k <= kmax; ++k)
+        if (R.more && rk == k) rmw();
     }
   };
 

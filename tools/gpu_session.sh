@@ -50,6 +50,10 @@ for s in $STEPS; do
       # kernel trace of the fused step alone (tools/km_step_once.py at cfg3, second-iteration centres)
       cd /tmp && step kstrace 300 rocprofv3 --kernel-trace --stats -d $O/kstrace -o p --output-format csv \
         -- python3 $R/tools/km_step_once.py 100000000 5 > $O/kstrace.log 2>&1 ;;
+    kftrace)
+      # the same on first-iteration centres (the first K points: skewed labels, more add rounds)
+      cd /tmp && step kftrace 300 rocprofv3 --kernel-trace --stats -d $O/kftrace -o p --output-format csv \
+        -- python3 $R/tools/km_step_once.py 100000000 5 first > $O/kftrace.log 2>&1 ;;
     kundtrace)
       cd /tmp && step kundtrace 300 rocprofv3 --kernel-trace --stats -d $O/kundtrace -o p --output-format csv \
         -- python3 $R/tools/km_und.py 100000000 > $O/kundtrace.log 2>&1 ;;

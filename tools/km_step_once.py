@@ -1,7 +1,8 @@
 """Dev tool (GPU box): spx_kmeans_step REPS times at the cfg3 shape (second-
 iteration centres) for rocprofv3 kernel traces / counter passes.
-  python tools/km_step_once.py [N] [REPS] [assign|step] [libspx variant .so]
-('assign': kmeans_assign + kmeans_accumulate instead of the fused step)"""
+  python tools/km_step_once.py [N] [REPS] [assign|step|first] [libspx variant .so]
+('assign': kmeans_assign + kmeans_accumulate instead of the fused step;
+'first': the fused step on first-iteration centres, the first K points)"""
 import os
 import sys
 
@@ -14,7 +15,8 @@ from spartan_amd import backend  # noqa: E402
 def main():
   N = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000_000
   reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-  two = len(sys.argv) > 3 and sys.argv[3] == 'assign'
+  mode = sys.argv[3] if len(sys.argv) > 3 else 'step'
+  two = mode == 'assign'
   if len(sys.argv) > 4:  # a variant build of the library (tools/build_variant.sh)
     backend.load_library(sys.argv[4])
   be = backend.get()
@@ -28,9 +30,10 @@ def main():
   cen = pts[:K].to(torch.float64).contiguous()
   # second-iteration centres from the two-pass path, so that variant builds of
   # the fused step are timed on the same centres whatever their sums
-  be.kmeans_assign(pts, cen, lab)
-  be.kmeans_accumulate(pts, lab, sums, cnt)
-  cen = (sums / cnt.clamp(min=1).to(torch.float64).reshape(K, 1)).contiguous()
+  if mode != 'first':
+    be.kmeans_assign(pts, cen, lab)
+    be.kmeans_accumulate(pts, lab, sums, cnt)
+    cen = (sums / cnt.clamp(min=1).to(torch.float64).reshape(K, 1)).contiguous()
   be.kmeans_step(pts, cen, lab, sums, cnt)
   torch.cuda.synchronize()
   ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -43,7 +46,7 @@ def main():
       be.kmeans_step(pts, cen, lab, sums, cnt)
   ev[1].record()
   torch.cuda.synchronize()
-  print('%s: %.3f ms per iteration' % ('assign+accumulate' if two else 'step', ev[0].elapsed_time(ev[1]) / reps),
+  print('%s: %.3f ms per iteration' % ('assign+accumulate' if two else mode, ev[0].elapsed_time(ev[1]) / reps),
         flush=True)
 
 
