@@ -3013,6 +3013,7 @@ __global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(4 * 
   const int cb = blockIdx.y / ndb, db = blockIdx.y % ndb;
   const i64 c0 = (i64)cb * KA_CB, d0 = (i64)db * KA_DB;
   const i64 nch = (N + CH - 1) / CH;
+  const i64 G = gridDim.x;
   // this lane's slice of a chunk: point lp, columns d0 + lc .. + VE
   const int lp = t / LPR, lc = (t % LPR) * VE;
   // 16-byte loads need the slice inside the row and aligned; else per element
@@ -3031,13 +3032,20 @@ __global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(4 * 
   // Prefetch ring: loads use clamped (always valid) addresses and nothing
   // consumes them until the stage comes round again -- a use right after the
   // issue would make the compiler wait for the whole ring (vmcnt(0)).
+  // A row list's indices are loaded one round ahead of the rows themselves
+  // (ridx / lidx: chunk ch + ST G's), so a round waits for one load latency,
+  // not for the index load and then the dependent row load.
   V pf[ST];
-  i64 plab[ST];
+  i64 plab[ST], ridx[ST], lidx[ST];
+  auto load_idx = [&](int s, i64 ch) {
+    const i64 p0 = (ch < nch ? ch : nch - 1) * CH;
+    ridx[s] = rows[p0 + lp < N ? p0 + lp : N - 1];
+    if (t < CH) lidx[s] = rows[p0 + t < N ? p0 + t : N - 1];
+  };
   auto load = [&](int s, i64 ch) {
     if (N == 0) return;  // an empty row list: nothing to load
     const i64 p0 = (ch < nch ? ch : nch - 1) * CH;
-    i64 pr = p0 + lp < N ? p0 + lp : N - 1;
-    if (rows) pr = rows[pr];
+    const i64 pr = rows ? ridx[s] : (p0 + lp < N ? p0 + lp : N - 1);
     if (vec) {
       pf[s] = ld_stream((const V*)(P + pr * ldp + d0 + lc));  // read once: nt
     } else {
@@ -3047,12 +3055,14 @@ __global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(4 * 
         pf[s][j] = P[pr * ldp + d];
       }
     }
-    if (t < CH) {
-      const i64 pl = p0 + t < N ? p0 + t : N - 1;
-      plab[s] = labels[rows ? rows[pl] : pl];
-    }
+    if (t < CH) plab[s] = labels[rows ? lidx[s] : (p0 + t < N ? p0 + t : N - 1)];
+    if (rows) load_idx(s, ch + ST * G);
   };
-  const i64 G = gridDim.x;
+#pragma unroll
+  for (int s = 0; s < ST; ++s) {
+    ridx[s] = lidx[s] = 0;
+    if (rows && N > 0) load_idx(s, blockIdx.x + s * G);
+  }
 #pragma unroll
   for (int s = 0; s < ST; ++s) load(s, blockIdx.x + s * G);
   int buf = 0;
