@@ -1,7 +1,8 @@
 """Dev tool (GPU box): per-wave cycles of each loop segment of k_kmeans_fs2
 (a -DKF2_PROF=1 build: tools/build_variant.sh prof -DKF2_PROF=1) at cfg3
-with second-iteration centres, averaged over the waves, per 64-row unit.
-  python tools/kf2_prof.py tools/bin/libspx_prof.so [N]"""
+with second-iteration centres ('first': the first K points), averaged over
+the waves, per 64-row unit.
+  python tools/kf2_prof.py tools/bin/libspx_prof.so [N] [first]"""
 import ctypes
 import os
 import sys
@@ -30,9 +31,11 @@ def main():
   sums = torch.empty((K, D), dtype=torch.float64, device=dev)
   cnt = torch.empty((K,), dtype=torch.int64, device=dev)
   cen = pts[:K].to(torch.float64).contiguous()
-  be.kmeans_assign(pts, cen, lab)
-  be.kmeans_accumulate(pts, lab, sums, cnt)
-  cen = (sums / cnt.clamp(min=1).to(torch.float64).reshape(K, 1)).contiguous()
+  first = len(sys.argv) > 3 and sys.argv[3] == 'first'
+  if not first:
+    be.kmeans_assign(pts, cen, lab)
+    be.kmeans_accumulate(pts, lab, sums, cnt)
+    cen = (sums / cnt.clamp(min=1).to(torch.float64).reshape(K, 1)).contiguous()
   be.kmeans_step(pts, cen, lab, sums, cnt)
   torch.cuda.synchronize()
   buf = (ctypes.c_ulonglong * (256 * 8 * 9))()
