@@ -2,16 +2,17 @@
 
 Data plane, by ``ctx.dist_backend``:
 
-* ``'nccl'`` (the GPU default at N > 1): torch.distributed's own RCCL
-  process group (PyTorch's librccl); also the fallback when the libspx
-  communicator fails its start-up self-test (``selftest``).
-* ``'rccl'`` (opt-in, ``SPARTAN_DIST_BACKEND=rccl``, until a multi-GPU run
-  has validated it): every collective is a libspx.so
+* ``'rccl'`` (the GPU default at N > 1): every collective is a libspx.so
   C-ABI call (``spx_allreduce`` / ``spx_reduce_scatter`` / ``spx_allgather``
   / ``spx_broadcast`` / ``spx_reduce`` / ``spx_sendrecv``, include/spx.h) on
   the RCCL communicator the runtime created, enqueued on the current HIP
   stream.  torch.distributed (gloo) is the host control plane only: the
-  unique-id hand-off, ``barrier`` and ``max_over_ranks`` of host floats.
+  unique-id hand-off, ``barrier``, the SPMD guard and ``max_over_ranks`` of
+  host floats.
+* ``'nccl'``: torch.distributed's own RCCL process group (PyTorch's
+  librccl): ``SPARTAN_DIST_BACKEND=nccl``, or the fallback when the libspx
+  communicator cannot be created or fails its start-up self-test
+  (``selftest``).  The control plane then runs on a gloo group of its own.
 * ``'gloo'``: CPU tests, and the one-GPU multi-rank rehearsal
   (``SPARTAN_DIST_BACKEND=gloo``), where device tensors are staged through
   host memory.
@@ -40,6 +41,17 @@ def _grp():
   """The torch process group of the data plane: torch's own RCCL group when
   the runtime fell back to it, else the default group."""
   return getattr(runtime.get(), 'pg', None)
+
+
+def _ctl(ctx):
+  """(group, device) of the host control plane: the runtime's gloo group
+  when the default group is nccl, else the default (gloo) group."""
+  import torch
+  if getattr(ctx, 'ctl', None) is not None:
+    return ctx.ctl, torch.device('cpu')
+  if _dist().get_backend() == 'nccl':  # a caller-made nccl default group and no gloo group
+    return None, ctx.device
+  return None, torch.device('cpu')
 
 
 def _staged(ctx, t):
@@ -148,9 +160,9 @@ def spmd_check(where='check'):
   if not ctx.distributed:
     return
   h = _GUARD['h']
-  dev = ctx.device if _dist().get_backend() == 'nccl' else torch.device('cpu')
+  grp, dev = _ctl(ctx)
   t = torch.tensor([h, -h], dtype=torch.int64, device=dev)
-  _dist().all_reduce(t, op=_dist().ReduceOp.MAX)
+  _dist().all_reduce(t, op=_dist().ReduceOp.MAX, group=grp)
   hi, lo = int(t[0].item()), -int(t[1].item())
   if hi != h or lo != h:
     raise RuntimeError('SPMD divergence at %s: rank %d issued a different sequence of collectives than '
@@ -354,52 +366,89 @@ def exchange(sends, recvs):
     t.copy_(h)
 
 
-def selftest():
+def _wait_device(dev, timeout):
+  """Wait for the work queued on ``dev``'s current stream, at most ``timeout``
+  s (an event polled from the host: a collective whose peer never arrives
+  would block torch.cuda.synchronize for ever).  True when it finished."""
+  import time
+  import torch
+  if dev.type != 'cuda':
+    return True
+  ev = torch.cuda.Event()
+  ev.record(torch.cuda.current_stream(dev))
+  end = time.monotonic() + timeout
+  while not ev.query():
+    if time.monotonic() > end:
+      return False
+    time.sleep(0.001)
+  return True
+
+
+def selftest(timeout=None):
   """Exercise every collective of the data plane once on small tensors and
   check the results on the host; returns None, or a description of the first
   wrong result / error.  All ranks call it (collective) and all get the same
   verdict (a max over ranks on the control plane).  runtime.initialize runs
   it on the libspx RCCL communicator before any tile data moves, and falls
-  back to torch.distributed's own RCCL group if it fails."""
+  back to torch.distributed's own RCCL group if it fails.
+
+  Every rank issues every collective even after one of its own calls raised
+  (each call in its own try), so the ranks stay in step; the device wait is
+  bounded (``SPARTAN_SELFTEST_TIMEOUT`` s, default 60); the SPMD guard's
+  running hash is restored afterwards, so a rank that failed part-way does
+  not leave the ranks' hashes different."""
   import torch
   ctx = runtime.get()
   if not ctx.distributed:
     return None
+  if timeout is None:
+    timeout = float(os.environ.get('SPARTAN_SELFTEST_TIMEOUT', '60'))
   W, r = ctx.world_size, ctx.rank
   dev = ctx.device
-  err = None
-  try:
-    base = torch.arange(4 * W, dtype=torch.float32, device=dev)
-    t = base + float(r)
-    all_reduce(t, 'sum')
-    want = (W * torch.arange(4 * W, dtype=torch.float64) + W * (W - 1) / 2.0)
-    if not torch.equal(t.double().cpu(), want):
-      err = 'all_reduce(sum) wrong'
-    full = base.double() * (r + 1)
-    out = torch.empty((4,), dtype=torch.float64, device=dev)
-    reduce_scatter_rows(out, full, 'sum')
-    want = torch.arange(4 * W, dtype=torch.float64)[4 * r:4 * r + 4] * (W * (W + 1) / 2.0)
-    if err is None and not torch.equal(out.cpu(), want):
-      err = 'reduce_scatter(sum) wrong'
-    mx = torch.full((3,), float(r), dtype=torch.float64, device=dev)
-    all_reduce(mx, 'max')
-    if err is None and not bool((mx.cpu() == W - 1).all()):
-      err = 'all_reduce(max) wrong'
-    g = all_gather_stack(torch.full((3,), r, dtype=torch.int64, device=dev))
-    if err is None and not torch.equal(g.cpu(), torch.arange(W, dtype=torch.int64).repeat_interleave(3).view(W, 3)):
-      err = 'all_gather wrong'
-    b = torch.full((5,), 7 * r + 1, dtype=torch.int64, device=dev)
-    broadcast(b, W - 1)
-    if err is None and not bool((b.cpu() == 7 * (W - 1) + 1).all()):
-      err = 'broadcast wrong'
-    src = torch.full((6,), 10 * r + 3, dtype=torch.int32, device=dev)
-    dst = torch.empty((6,), dtype=torch.int32, device=dev)
-    exchange([(src, (r + 1) % W)], [(dst, (r - 1) % W)])
-    if err is None and not bool((dst.cpu() == 10 * ((r - 1) % W) + 3).all()):
-      err = 'send/recv wrong'
-    torch.cuda.synchronize(dev) if dev.type == 'cuda' else None
-  except Exception as e:  # noqa: BLE001  (reported to the caller, which decides)
-    err = '%s: %s' % (type(e).__name__, e)
+  saved = dict(_GUARD)
+  errs = []
+  checks = []
+
+  def call(name, fn):
+    try:
+      fn()
+    except Exception as e:  # noqa: BLE001  (reported to the caller, which decides)
+      errs.append('%s: %s: %s' % (name, type(e).__name__, e))
+
+  base = torch.arange(4 * W, dtype=torch.float32, device=dev)
+  t = base + float(r)
+  call('all_reduce(sum)', lambda: all_reduce(t, 'sum'))
+  checks.append(('all_reduce(sum)', t, W * torch.arange(4 * W, dtype=torch.float64) + W * (W - 1) / 2.0))
+  full = base.double() * (r + 1)
+  out = torch.zeros((4,), dtype=torch.float64, device=dev)
+  call('reduce_scatter(sum)', lambda: reduce_scatter_rows(out, full, 'sum'))
+  checks.append(('reduce_scatter(sum)', out,
+                 torch.arange(4 * W, dtype=torch.float64)[4 * r:4 * r + 4] * (W * (W + 1) / 2.0)))
+  mx = torch.full((3,), float(r), dtype=torch.float64, device=dev)
+  call('all_reduce(max)', lambda: all_reduce(mx, 'max'))
+  checks.append(('all_reduce(max)', mx, torch.full((3,), float(W - 1), dtype=torch.float64)))
+  g = [torch.zeros((W, 3), dtype=torch.int64, device=dev)]
+
+  def gather():
+    g[0] = all_gather_stack(torch.full((3,), r, dtype=torch.int64, device=dev))
+  call('all_gather', gather)
+  b = torch.full((5,), 7 * r + 1, dtype=torch.int64, device=dev)
+  call('broadcast', lambda: broadcast(b, W - 1))
+  checks.append(('broadcast', b, torch.full((5,), 7 * (W - 1) + 1, dtype=torch.int64)))
+  src = torch.full((6,), 10 * r + 3, dtype=torch.int32, device=dev)
+  dst = torch.zeros((6,), dtype=torch.int32, device=dev)
+  call('send/recv', lambda: exchange([(src, (r + 1) % W)], [(dst, (r - 1) % W)]))
+  checks.append(('send/recv', dst, torch.full((6,), 10 * ((r - 1) % W) + 3, dtype=torch.int32)))
+  err = errs[0] if errs else None
+  if not _wait_device(dev, timeout):
+    err = err or 'the collectives did not complete within %g s' % timeout
+  else:
+    checks.insert(3, ('all_gather', g[0], torch.arange(W, dtype=torch.int64).repeat_interleave(3).view(W, 3)))
+    for name, got, want in checks:
+      if err is None and not torch.equal(got.cpu().to(want.dtype), want):
+        err = '%s wrong' % name
+  _GUARD.clear()
+  _GUARD.update(saved)
   bad = max_over_ranks(1.0 if err else 0.0)
   if bad and err is None:
     err = 'another rank failed'
@@ -422,9 +471,7 @@ def max_over_ranks(x):
   ctx = runtime.get()
   if not ctx.distributed:
     return x
-  # the default (control-plane) group: gloo -> a host tensor; nccl only when
-  # the whole job runs on torch's RCCL group (SPARTAN_COMM=torch)
-  dev = ctx.device if _dist().get_backend() == 'nccl' else torch.device('cpu')
+  grp, dev = _ctl(ctx)
   t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
-  _dist().all_reduce(t, op=_dist().ReduceOp.MAX)
+  _dist().all_reduce(t, op=_dist().ReduceOp.MAX, group=grp)
   return float(t.item())

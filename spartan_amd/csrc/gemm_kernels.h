@@ -20,10 +20,6 @@
 
 #include <cstdint>
 
-#ifndef SPX_GEMM_AK
-#define SPX_GEMM_AK 1  // fp32: A k-contiguous in LDS, K split between lane halves (see gemm)
-#endif
-
 namespace spx_mfma {
 
 typedef int64_t i64;
@@ -98,9 +94,12 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
   constexpr int VE = 16 / sizeof(T);  // elements per 16-byte load
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / F::TILE, TN = WTN / F::TILE;
-  constexpr int LA = BM * BK / VE / NT, LB = BK * BN / VE / NT;
+  // 16-byte loads per thread and K-tile (a block of more threads than a
+  // tile has 16-byte pieces leaves the upper threads idle for that operand)
+  constexpr int NA = BM * BK / VE, NB = BK * BN / VE;
+  constexpr int LA = (NA + NT - 1) / NT, LB = (NB + NT - 1) / NT;
   constexpr int PADA = 16 / sizeof(T) / 2 > 0 ? 16 / sizeof(T) / 2 : 1;
-  static_assert(LA >= 1 && LB >= 1 && LA * NT * VE == BM * BK && LB * NT * VE == BK * BN, "bad tiling");
+  static_assert((NA % NT == 0 || NA < NT) && (NB % NT == 0 || NB < NT), "bad tiling");
   static_assert(TM >= 1 && TN >= 1 && BK % F::KS == 0, "bad wave tiling");
   // AK (fp32): A kept k-contiguous in LDS ([m][k], rows padded to BK + 4)
   // and the tile's K split between the two lane halves: MFMA step kk takes
@@ -108,7 +107,7 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
   // same way), so a lane's BK/2 A values are two ds_read_b128 per K-tile
   // and the staging store is one ds_write_b128 -- instead of BK/2 ds_read_b32
   // and a 4-way transposing scalar store.
-  constexpr bool AK = SPX_GEMM_AK && sizeof(T) == 4 && F::KS == 2 && BK % 8 == 0;
+  constexpr bool AK = sizeof(T) == 4 && F::KS == 2 && BK % 8 == 0;
   __shared__ __attribute__((aligned(16))) T As[AK ? 1 : 2][AK ? 1 : BK][AK ? 1 : BM + PADA];
   __shared__ __attribute__((aligned(16))) T Ak[AK ? 2 : 1][AK ? BM : 1][AK ? BK + 4 : 1];
   __shared__ __attribute__((aligned(16))) T Bs[2][BK][BN];
@@ -133,6 +132,7 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int idx = t + i * NT;
+      if (NA < NT && idx >= NA) break;
       const int r = idx / (BK / VE), kq = idx % (BK / VE);
       const i64 gr = row0 + r, gk = k0 + kq * VE;
       if (ALIGNED) {
@@ -145,6 +145,7 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int idx = t + i * NT;
+      if (NB < NT && idx >= NB) break;
       const int kr = idx / (BN / VE), cq = idx % (BN / VE);
       const i64 bk = k0 + kr, bc = col0 + cq * VE;
       if (ALIGNED) {
@@ -159,6 +160,7 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int idx = t + i * NT;
+      if (NA < NT && idx >= NA) break;
       const int r = idx / (BK / VE), kq = idx % (BK / VE);
       if constexpr (AK) {
         *(V*)(&Ak[buf][r][kq * VE]) = ra[i];
@@ -170,6 +172,7 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int idx = t + i * NT;
+      if (NB < NT && idx >= NB) break;
       const int kr = idx / (BN / VE), cq = idx % (BN / VE);
       *(V*)(&Bs[buf][kr][cq * VE]) = rb[i];
     }

@@ -1013,10 +1013,7 @@ struct KfConf {
         N, D, K, Kp, (const TP*)P, ldp, CT, cn, cmax, labels, counters, full_list, cand_list);
   }
 };
-#ifndef KF_PROD
-#define KF_PROD KfConf<64, 2, 0, 3>
-#endif
-typedef KF_PROD KfProd;
+typedef KfConf<64, 2, 0, 3> KfProd;
 
 // ---------------------------------------------------------------------------
 // bf16x3 certified filter (fp32 points, K <= 256, D % 64 == 0, D <= 128).
@@ -1055,9 +1052,6 @@ typedef KF_PROD KfProd;
 constexpr int KB_WAVES = 4;
 constexpr int KB_DMAX = 128;
 constexpr int KB_GRP = 4;  // k-steps per MFMA group (divides 4)
-#ifndef KB_FRESH
-#define KB_FRESH 1  // 1: every group into a fresh accumulator (tighter bound), 0: one chain per tile
-#endif
 typedef __bf16 kb_bf8 __attribute__((ext_vector_type(8)));
 typedef float kb_acc __attribute__((ext_vector_type(16)));
 typedef float kb_f4 __attribute__((ext_vector_type(4)));
@@ -1291,9 +1285,9 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
   const double mcoef = cmax_p[1], mun = cmax_p[2];
   const double u32 = 5.9604644775390625e-08;
   const int KS = (int)D / 16;
-  // chain length of one accumulator: 48 KB_GRP products then KS / KB_GRP
-  // adds (fresh accumulators), or all 48 KS products in one MFMA chain
-  const double chain = KB_FRESH ? 48.0 * KB_GRP + (double)(KS / KB_GRP) : 48.0 * (double)KS;
+  // chain length of one accumulator: 48 KB_GRP products into a fresh
+  // accumulator, then KS / KB_GRP adds
+  const double chain = 48.0 * KB_GRP + (double)(KS / KB_GRP);
   const double eS = (u32 + 3.1 * 3.814697265625e-06 + 2.0 * (chain + 3.0) * u32) * 1.01 * cmax;
   const i64 nslots = rows_in ? (i64)*nrows_in : N;
   if (nslots == 0) return;
@@ -1367,35 +1361,18 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
           // fresh accumulator that is then added to the running sum: the
           // rounding bound is that chain + D / (16 KB_GRP) adds instead of
           // one 3D-long chain
-#if KB_FRESH
           kb_acc tk = (kb_acc){};
-#else
-          kb_acc& tk = acc[ct];
-#endif
 #pragma unroll
           for (int g = 0; g < KB_GRP; ++g) {
             tk = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[g], bh[ct & 1][g], tk, 0, 0, 0);
             tk = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[g], bl[ct & 1][g], tk, 0, 0, 0);
             tk = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[g], bh[ct & 1][g], tk, 0, 0, 0);
           }
-#if KB_FRESH
           acc[ct] += tk;
-#endif
         }
       }
     }
     p2 += __shfl_xor(p2, 32, 64);  // row r's |p|^2 in lanes r and r + 32
-#ifdef KB_DEV_NO_EPILOGUE  // tools/kb_split.hip timing split only; never set in the product build
-    {
-      float z = p2;
-#pragma unroll
-      for (int ct = 0; ct < NCT; ++ct)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) z += acc[ct][q];
-      if (z == 1.2345f) labels[0] = -7;
-      continue;
-    }
-#endif
     // ---- epilogue.  Register reg of tile ct holds S(row rt(reg, h), centre
     // 32 ct + r), rt = (reg&3) + 8(reg>>2) + 4h.
     // (A) per register: a' = fl(|c|^2 - 2S) with the tile index ct written
@@ -1535,29 +1512,12 @@ static void kb_launch(hipStream_t s, i64 N, i64 D, const float* P, i64 ldp, cons
 // k_kmeans_filter_b3 gives them candidate masks (k_kmeans_cand then
 // recomputes the candidates in scipy's exact order); non-finite rows go to
 // the all-centre exact kernel as before.
-#ifndef KS_WAVES_CFG
-#define KS_WAVES_CFG 8  // waves per block (one block per CU): 8 = two per SIMD (<= 256 registers), 4 = one (<= 512)
-#endif
-constexpr int KS_WAVES = KS_WAVES_CFG;
-#ifndef KS_WAVES1_CFG
-#define KS_WAVES1_CFG 8  // the same for the fp16 screen (MODE 1): 12 = three per SIMD (<= 168 registers)
-#endif
-#ifndef KS_PAIRF1
-#define KS_PAIRF1 1  // 1: the screen folds two centre tiles at a time (max3 / med3 / max)
-#endif
-#ifndef KS_PIN1
-#define KS_PIN1 0  // 1: the screen's |x'|^2 fmas pinned right after the split (frees the raw tile's registers)
-#endif
-__host__ __device__ constexpr int ks_waves(int mode) { return mode == 1 ? KS_WAVES1_CFG : KS_WAVES; }
-#ifndef KS_PREFETCH
-#define KS_PREFETCH 0  // 1: next tile's loads in flight during the sweep (+64 registers: spills at 2 waves/SIMD)
-#endif
-#ifndef KS_PREFETCH1
-#define KS_PREFETCH1 0  // the same for the fp16 screen (MODE 1)
-#endif
-#ifndef KS_PIPE
-#define KS_PIPE 1  // 1: tile ct's top-2 fold interleaved with tile ct+1's MFMAs (two accumulator sets)
-#endif
+// Waves per block (one block per CU): 8 = two per SIMD (<= 256 registers),
+// for both the bf16x3 filter and the fp16 screen (MODE 1).  Measured and not
+// kept: one or three waves per SIMD, a next-tile prefetch, the
+// |x'|^2 fmas pinned after the split, an unpipelined sweep.
+constexpr int KS_WAVES = 8;
+__host__ __device__ constexpr int ks_waves(int) { return KS_WAVES; }
 
 // LDS row of centre c: [hi: D bf16][lo: D bf16][-cc/2 as 3 bf16 + 5 zeros]
 // [8 zero bf16][16-byte pad]; the row stride is 4 D + 48 bytes = 12 (mod 64)
@@ -1786,11 +1746,8 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
       ra[ks][1] = *(const kb_f4*)(p + ks * 16 + 8);  // dims 8+4h..8+4h+3
     }
   };
-  constexpr bool PF = MODE == 1 ? KS_PREFETCH1 : KS_PREFETCH;
-  if constexpr (PF)
-    if (tile < ntiles) load(tile);
   for (; tile < ntiles; tile += stride) {
-    if constexpr (!PF) load(tile);  // the partner wave's sweep covers the latency
+    load(tile);  // the partner wave's sweep covers the latency
     using AT = std::conditional_t<MODE == 0, kb_bf8, kh_f8>;
     AT ah[KS];
     kb_bf8 al[MODE == 0 ? KS : 1];
@@ -1820,18 +1777,9 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
       }
     }
     float p2 = (p2q[0] + p2q[1]) + (p2q[2] + p2q[3]);
-    if constexpr (MODE == 1 && KS_PIN1) __builtin_amdgcn_sched_barrier(0);
     // (the compiler sinks the 64 |p|^2 fmas to the decision, keeping the raw
     // tile live through the sweep; pinning them here frees 47 registers but
-    // measured 2 % slower, and the freed registers buy a next-tile prefetch
-    // that only wins that back: 20.3 / 20.7 / 20.5 ms, gpurun_out ksv4)
-    if constexpr (PF) {
-      // the split above must finish reading ra before the next tile's loads
-      // land in it: without this fence the scheduler hoists the loads above
-      // the split (three tiles' worth of registers live at once -> spills)
-      __builtin_amdgcn_sched_barrier(0);
-      if (tile + stride < ntiles) load(tile + stride);  // lands during the sweep below
-    }
+    // measured 2 % slower, gpurun_out ksv4)
     // running top-2 of acc = S - cc/2 = -a'/2 (the best centre has the
     // LARGEST acc); lo / sec keep their names from the a' form
     float lo[16], sec[16];
@@ -1880,7 +1828,6 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
 #pragma unroll
       for (int q = 0; q < 16; ++q) fold1(q, ct, c0[q]);
     };
-#if KS_PIPE
     // software pipeline: tile ct's fold (VALU) is independent of tile ct+1's
     // MFMAs, so each wave fills its own MFMA gaps with it: the fold of the
     // previous tile is written into the k-loop of the next tile's chain (16 / KS
@@ -1897,12 +1844,12 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
       }
       c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, *(const kb_bf8*)(rp + CCOFF), c0, 0, 0, 0);
     };
-    // pairwise fold (KS_PAIRF1, screen only): two tiles' values a, b of one
+    // pairwise fold (screen only): two tiles' values a, b of one
     // row fold as sec = max(sec, med3(lo, a, b)), lo = max3(lo, a, b) -- the
     // top two of {lo, sec, a, b} with lo >= sec -- 5 VALU per 2 values
     // instead of 6; needs both tiles' accumulators live (a third and fourth
     // set: the screen has the registers, MODE 0 does not)
-    constexpr bool PAIRF = MODE == 1 && KS_PAIRF1 && NCT >= 2;
+    constexpr bool PAIRF = MODE == 1 && NCT >= 2;
     auto fold2 = [&](int q, int ct, float a, float b) {
       const float ta = ks_tag(a, (unsigned int)ct), tb = ks_tag(b, (unsigned int)(ct + 1));
       sec[q] = ks_max(sec[q], ks_med3(lo[q], ta, tb));
@@ -1963,14 +1910,6 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
         fold(NCT - 1, b0);
       }
     }
-#else
-#pragma unroll 1
-    for (int ct = 0; ct < NCT; ++ct) {  // rolled: bounds the scheduler's window (and the LDS reads it hoists)
-      kb_acc c0;
-      chain(ct, c0);
-      fold(ct, c0);
-    }
-#endif
     float lo0[16];  // this lane's best per register (its centre r over all tiles)
 #pragma unroll
     for (int q = 0; q < 16; ++q) lo0[q] = lo[q];
@@ -2979,19 +2918,13 @@ __global__ __launch_bounds__(256) void k_kmeans_prep(i64 D, i64 K, i64 Kp, const
 //   k_kmeans_reduce   out[i] (+)= sum over g of part[g][i]: four fixed g
 //                     slices per output, combined in a fixed order.
 constexpr int KA_THREADS = 1024;
-#ifndef KA_CPL
-#define KA_CPL 2                           // columns per lane: 2 -> every point is visited once per wave at D = 128
-#endif
+constexpr int KA_CPL = 2;                  // columns per lane: 2 -> every point is visited once per wave at D = 128
 constexpr int KA_DB = 64 * KA_CPL;         // columns per tile
 constexpr int KA_WAVES = KA_THREADS / 64;  // centre owners per tile
 constexpr int KA_CPW = 16;                 // centres per wave (register sums)
 constexpr int KA_CB = KA_WAVES * KA_CPW;   // centres per tile
-#ifndef KA_STAGES
-#define KA_STAGES 3                        // register prefetch ring depth (chunks per barrier): 3 -> 10.1 ms, 2 -> 10.2, 4 -> 10.7, 1 -> 11.8 at cfg3 (profiles/r01_ka_variants.txt)
-#endif
-#ifndef KA_BPC
-#define KA_BPC 1                          // resident blocks per CU (LDS: 2 KA_STAGES x 16 KiB per block)
-#endif
+constexpr int KA_STAGES = 3;               // register prefetch ring depth (chunks per barrier): 3 -> 10.1 ms, 2 -> 10.2, 4 -> 10.7, 1 -> 11.8 at cfg3 (profiles/r01_ka_variants.txt)
+constexpr int KA_BPC = 1;                  // resident blocks per CU (LDS: 2 KA_STAGES x 16 KiB per block)
 
 // rows / nrows (optional): accumulate only the rows rows[0 .. *nrows) (a
 // row list in row order, gathered row by row; the count is read on the device).

@@ -172,8 +172,14 @@ def run_dot(a, b, tile_hint=None):
   # block runs with beta = 0, and only column blocks this rank computes
   # nothing for are zeroed (a rank without local B blocks)
   col_blocks = sorted({(bex.ul[1], bex.lr[1]) for bex in btiles})
-  C = torch.empty((M, N), dtype=backend.torch_dtype(dtype), device=ctx.device)
-  started = set()
+  if _blocks_disjoint(col_blocks):
+    C = torch.empty((M, N), dtype=backend.torch_dtype(dtype), device=ctx.device)
+    started = set()
+  else:
+    # B's column splits differ between K bands: a later block's beta = 0
+    # would overwrite an overlapping earlier one -- accumulate into zeros
+    C = torch.zeros((M, N), dtype=backend.torch_dtype(dtype), device=ctx.device)
+    started = _ALWAYS_STARTED
   requests, plan = [], []
   for bex, w in btiles.items():
     dst = ctx.owner(w) if w != -1 else None
@@ -210,6 +216,25 @@ def run_dot(a, b, tile_hint=None):
 OVERLAPPED_CALLS = 0  # how often the overlapped path ran (tests check it is taken)
 
 
+class _AlwaysStarted(set):
+  """'Every column block already started': beta = 1 for every GEMM (C zeroed)."""
+
+  def __contains__(self, key):
+    return True
+
+  def add(self, key):
+    pass
+
+
+_ALWAYS_STARTED = _AlwaysStarted()
+
+
+def _blocks_disjoint(col_blocks):
+  """True when the distinct (c0, c1) column ranges do not overlap (sorted input):
+  then the first GEMM into each range may run with beta = 0."""
+  return all(col_blocks[i][1] <= col_blocks[i + 1][0] for i in range(len(col_blocks) - 1))
+
+
 def _owner_slabs(output, ctx, M):
   from .engine import _rank_slabs
   return _rank_slabs(output, ctx) and M % ctx.world_size == 0
@@ -240,9 +265,10 @@ def _dot_overlapped(output, got, plan, b, B, K, M, N, dtype, C, col_blocks):
       bt = b.fetch(B.to_base(bex)).reshape(bex.shape)
     local.append((bex, at, _as_dtype(bt, dtype)))
   handles = []
+  disjoint = _blocks_disjoint(col_blocks)  # (else the caller made C zeros)
   for j in range(ctx.world_size):
     r0, r1 = j * slab, (j + 1) * slab
-    started = set()
+    started = set() if disjoint else _ALWAYS_STARTED
     for bex, at, bt in local:
       key = (bex.ul[1], bex.lr[1])
       be.gemm(at[r0:r1], bt, C[r0:r1, key[0]:key[1]], 1.0, 0.0 if key not in started else 1.0)

@@ -171,7 +171,12 @@ def materialise_pres(pres, children, child_to_var, ex, inputs):
 # ----------------------------------------------------------------- map
 def run_location_map(children, child_to_var, op):
   """A map whose tree holds a map_with_location call: lowered once per tile
-  with that tile's extent (map_with_location.py:22-60), one kernel per tile."""
+  with that tile's extent (map_with_location.py:22-60), one kernel per tile.
+
+  Tracing is per tile, so only ranks holding a tile that fails to trace would
+  see UntraceableMapper, and only ranks holding tiles can see two result
+  dtypes: both are decided over all ranks (control plane) before any rank
+  branches, so every rank takes the same path and raises the same error."""
   import torch
   ctx = runtime.get()
   be = backend.get()
@@ -179,12 +184,33 @@ def run_location_map(children, child_to_var, op):
   tiles = driving_tiles(largest)
   arrays = {i: i for i, c in enumerate(children) if _scalar_value(c) is None}
   per_ex = fetch_inputs(children, arrays, tiles)
-  out_local, dtype = {}, None
-  for ex, fetched in per_ex.items():
-    root, slots, pres = bind(children, child_to_var, op, extent=ex)
-    if dtype is not None and np.dtype(root.dtype) != dtype:
-      raise CodegenError('location map yields %s on one tile and %s on another' % (dtype, root.dtype))
+  bound, untraceable, dtypes = {}, None, set()
+  for ex in per_ex:
+    try:
+      bound[ex] = bind(children, child_to_var, op, extent=ex)
+    except UntraceableMapper as e:
+      untraceable = e
+      break
+    dtypes.add(np.dtype(bound[ex][0].dtype))
+  if ctx.distributed:
+    if comm.max_over_ranks(1.0 if untraceable is not None else 0.0) and untraceable is None:
+      untraceable = UntraceableMapper('map_with_location mapper could not be traced on another rank')
+  if untraceable is not None:
+    return run_host_map(children, child_to_var, op, untraceable)
+  if len(dtypes) > 1:
+    mine = None  # _agree_dtype raises on every rank
+  else:
+    mine = next(iter(dtypes)) if dtypes else None
+  if ctx.distributed or len(dtypes) > 1:
+    dtype = _agree_dtype(mine, conflict=len(dtypes) > 1, what='location map')
+  elif mine is None:  # no local tile: the dtype of the first tile's trace
+    root, _, _ = bind(children, child_to_var, op, extent=next(iter(tiles)))
     dtype = np.dtype(root.dtype)
+  else:
+    dtype = mine
+  out_local = {}
+  for ex, fetched in per_ex.items():
+    root, slots, pres = bound[ex]
     inputs = {slot: fetched[ci] for slot, ci in slots.items()}
     materialise_pres(pres, children, child_to_var, ex, inputs)
     out = torch.empty(ex.shape if ex.ndim else (), dtype=backend.torch_dtype(root.dtype), device=ctx.device)
@@ -195,9 +221,6 @@ def run_location_map(children, child_to_var, op):
     else:
       be.map(root, inputs, out)
     out_local[ex] = out
-  if dtype is None:  # no local tile: every rank must agree on the dtype
-    root, _, _ = bind(children, child_to_var, op, extent=next(iter(tiles)))
-    dtype = np.dtype(root.dtype)
   if all(w == -1 for w in tiles.values()):
     (ex, out), = out_local.items()
     return ReplicatedArray(out)
@@ -209,19 +232,23 @@ HOST_MAPPER_CALLS = [0]   # tiles evaluated on the host (tests assert on it)
 _HOST_WARNED = set()
 
 
-def _agree_dtype(dt):
+def _agree_dtype(dt, conflict=False, what='mapper'):
   """The result dtype every rank uses: ranks without a local tile learn it
-  from the others (control plane); ranks that disagree raise."""
+  from the others (control plane).  If any rank saw two dtypes among its own
+  tiles (``conflict``) or the ranks' dtypes differ, EVERY rank raises (one
+  agreed verdict, so no rank goes on to a collective the others skip)."""
   codes = [np.dtype(t) for t in (np.bool_, np.int32, np.int64, np.float32, np.float64)]
-  if dt is not None and np.dtype(dt) not in codes:
-    raise TypeError('mapper result dtype %s is not supported by the MI355X backend' % dt)
-  mine = -1 if dt is None else codes.index(np.dtype(dt))
+  bad_type = dt is not None and np.dtype(dt) not in codes
+  mine = -1 if dt is None or bad_type else codes.index(np.dtype(dt))
   hi = int(comm.max_over_ranks(float(mine)))
   lo = -int(comm.max_over_ranks(float(-mine if mine >= 0 else -99)))
+  flags = int(comm.max_over_ranks(float(2 * bool(bad_type) + bool(conflict))))
+  if flags & 2:
+    raise TypeError('%s result dtype %s is not supported by the MI355X backend' % (what, dt))
+  if flags & 1 or (hi >= 0 and lo != hi):
+    raise CodegenError('%s yields different dtypes on different tiles or ranks' % what)
   if hi < 0:
     raise ValueError('map over an array without tiles')
-  if mine >= 0 and (lo != hi or mine != hi):
-    raise CodegenError('mapper yields different dtypes on different ranks')
   return codes[hi]
 
 
@@ -244,7 +271,7 @@ def run_host_map(children, child_to_var, op, err):
   tiles = driving_tiles(largest)
   arrays = {i: i for i, c in enumerate(children) if _scalar_value(c) is None}
   per_ex = fetch_inputs(children, arrays, tiles)
-  out_local, dtype = {}, None
+  out_local, dtype, conflict = {}, None, False
   for ex, fetched in per_ex.items():
     env = {'extent': ex}
     for i, (c, var) in enumerate(zip(children, child_to_var)):
@@ -254,12 +281,11 @@ def run_host_map(children, child_to_var, op, err):
     shape = ex.shape if ex.ndim else ()
     if tuple(res.shape) != tuple(shape):  # tile_mapper's Assert.eq (map.py:80-82)
       raise AssertionError('Bad shape -- tile %s, mapper result %s' % (shape, res.shape))
-    if dtype is not None and res.dtype != dtype:
-      raise CodegenError('mapper yields %s on one tile and %s on another' % (dtype, res.dtype))
+    conflict = conflict or (dtype is not None and res.dtype != dtype)
     dtype = res.dtype
     out_local[ex] = res
     HOST_MAPPER_CALLS[0] += 1
-  dtype = _agree_dtype(dtype)
+  dtype = _agree_dtype(None if conflict else dtype, conflict=conflict)
   out_local = {ex: transfer.upload(np.ascontiguousarray(res, dtype=dtype), ctx.device)
                for ex, res in out_local.items()}
   if all(w == -1 for w in tiles.values()):

@@ -6,9 +6,13 @@ execution model: ONE process per GPU, launched by torchrun, all processes
 running the same (SPMD) program.  A tile *worker* index (the reference's
 ``TileId.worker``, spartan/core.pyx:16-41) is owned by rank ``worker % world``.
 Every rank computes the same tile plan, runs the kernels for the tiles it owns
-on its own GPU, and exchanges data only through RCCL collectives over xGMI
-issued through libspx.so's C ABI (comm.py); torch.distributed (gloo) is the
-host control plane, and gloo alone carries the CPU-only tests.
+on its own GPU, and exchanges data through RCCL collectives over xGMI.  By
+default (world > 1 on GPUs) they are issued through libspx.so's C ABI
+(``spx_allreduce`` & co., comm.py) on a communicator this module creates, with
+torch.distributed (gloo) as the host control plane; a start-up self-test falls
+back to torch.distributed's own RCCL process group if that communicator
+cannot be created or computes a wrong result.  gloo alone carries the
+CPU-only tests.
 """
 import os
 
@@ -28,6 +32,7 @@ class Context:
     self._comm_stream = None
     self.pg = None          # torch process group of the data plane when dist_backend == 'nccl' (None: default)
     self.selftest = None    # data-plane self-test verdict at start-up (multi-rank RCCL only)
+    self.ctl = None         # gloo group of the control plane when the default group is nccl (None: default)
     self.num_workers = int(FLAGS.num_workers or world_size)
     if self.num_workers < 1:
       raise ValueError('num_workers must be >= 1')
@@ -58,22 +63,52 @@ class Context:
                                                             self.num_workers)
 
 
+def _rccl_init_bounded(comm, rank, world, uid, device, timeout):
+  """spx_comm_init on a helper thread, waited for at most ``timeout`` s.
+
+  ncclCommInitRank blocks until every rank has joined; a rank that never
+  arrives (or a transport that never connects) would block this process for
+  ever.  The call releases the GIL (ctypes), so the main thread can give up
+  and report instead; the helper thread is left behind (a daemon) -- the
+  communicator it may still produce is never used.  Returns (handle, error)."""
+  import threading
+  box = {}
+
+  def run():
+    try:
+      import torch
+      if device.type == 'cuda':
+        torch.cuda.set_device(device)  # RCCL binds the calling thread's current device
+      box['comm'] = comm.rccl_init(rank, world, uid)
+    except Exception as e:  # noqa: BLE001  (reported to the caller)
+      box['err'] = '%s: %s' % (type(e).__name__, e)
+
+  th = threading.Thread(target=run, name='spx_comm_init', daemon=True)
+  th.start()
+  th.join(timeout)
+  if th.is_alive():
+    return None, 'spx_comm_init did not return within %g s' % timeout
+  return box.get('comm'), box.get('err')
+
+
 def initialize(argv=None, device=None):
   """Bring up this rank (reference spartan.initialize, spartan/__init__.py:42-56).
 
   Reads RANK / WORLD_SIZE / LOCAL_RANK from the torchrun environment and
   selects cuda:LOCAL_RANK.  With more than one rank on GPUs the data plane
-  is, by default, torch.distributed's own RCCL process group ('nccl' -- the
-  same librccl, the collective path PyTorch validates on every multi-GPU
-  job).  ``SPARTAN_DIST_BACKEND=rccl`` opts in to the libspx.so C-ABI
-  communicator instead (spx_comm_init; every device collective a C-ABI call,
-  comm.py; torch.distributed then runs gloo as the host control plane: the
-  unique-id hand-off, barriers, host maxima), checked by a start-up
-  self-test that falls back to the torch group.  It stays opt-in until a
-  multi-GPU run has validated it (so far it has run at world 1 only).
-  ``SPARTAN_DIST_BACKEND=gloo`` rehearses N ranks on fewer GPUs (device
-  tensors staged through the host).  ``device`` overrides the device (tests
-  run the host logic on 'cpu' with a test backend and gloo)."""
+  is, by default, libspx.so's C-ABI RCCL communicator (``'rccl'``:
+  spx_comm_init, every device collective an ``spx_*`` call, comm.py), with
+  torch.distributed running gloo as the host control plane (the unique-id
+  hand-off, barriers, host maxima, the SPMD guard).  The communicator's
+  creation is bounded (``SPARTAN_RCCL_INIT_TIMEOUT`` s, default 120) and a
+  start-up self-test checks every collective on every rank; if either fails
+  on any rank, all ranks switch the device collectives to torch.distributed's
+  own RCCL process group (loudly) and re-run the test.
+  ``SPARTAN_DIST_BACKEND=nccl`` selects torch's RCCL group directly (the
+  control plane then gets its own gloo group), ``SPARTAN_DIST_BACKEND=gloo``
+  rehearses N ranks on fewer GPUs (device tensors staged through the host).
+  ``device`` overrides the device (tests run the host logic on 'cpu' with a
+  test backend and gloo)."""
   global _ctx
   import torch
   if argv is not None:
@@ -89,13 +124,15 @@ def initialize(argv=None, device=None):
   device = torch.device(device)
   backend = None
   rccl = None
+  init_err = None
+  ctl = None
   if world > 1:
     import torch.distributed as dist
-    backend = os.environ.get('SPARTAN_DIST_BACKEND', 'nccl' if device.type == 'cuda' else 'gloo')
+    backend = os.environ.get('SPARTAN_DIST_BACKEND', 'rccl' if device.type == 'cuda' else 'gloo')
     if backend not in ('nccl', 'rccl', 'gloo'):
       raise ValueError('SPARTAN_DIST_BACKEND must be nccl, rccl or gloo, not %r' % backend)
-    if backend == 'rccl' and os.environ.get('SPARTAN_COMM') == 'torch':
-      backend = 'nccl'
+    if backend == 'rccl' and (os.environ.get('SPARTAN_COMM') == 'torch' or device.type != 'cuda'):
+      backend = 'nccl' if device.type == 'cuda' else 'gloo'
     pg = 'nccl' if backend == 'nccl' else 'gloo'   # torch.distributed: control plane (or the torch RCCL path)
     if not dist.is_initialized():
       os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
@@ -103,31 +140,55 @@ def initialize(argv=None, device=None):
       if device.type == 'cuda' and pg == 'nccl':
         kw['device_id'] = device
       dist.init_process_group(backend=pg, rank=rank, world_size=world, **kw)
+    if dist.get_backend() == 'nccl':
+      # the SPMD guard and host maxima never share the data plane's communicator
+      ctl = dist.new_group(backend='gloo')
     if backend == 'rccl':
       from . import comm
-      obj = [comm.rccl_unique_id() if rank == 0 else None]
+      obj = [None]
+      if rank == 0:
+        try:
+          obj = [comm.rccl_unique_id()]
+        except Exception as e:  # noqa: BLE001
+          obj = ['error: %s' % e]
       dist.broadcast_object_list(obj, src=0)
-      rccl = comm.rccl_init(rank, world, obj[0])
+      if isinstance(obj[0], bytes):
+        rccl, init_err = _rccl_init_bounded(comm, rank, world, obj[0], device,
+                                            float(os.environ.get('SPARTAN_RCCL_INIT_TIMEOUT', '120')))
+      else:
+        init_err = 'rank 0 could not make an RCCL unique id (%s)' % obj[0]
   _ctx = Context(rank, world, local_rank, device, backend, rccl)
-  if backend == 'rccl' and os.environ.get('SPARTAN_RCCL_SELFTEST', '1') != '0':
-    # every collective of the libspx data plane, once, on small tensors,
-    # checked on the host before any tile moves; a wrong result or an error
-    # moves the data plane to torch.distributed's own RCCL group (loudly)
+  _ctx.ctl = ctl
+  if backend == 'rccl':
     from . import comm
-    err = comm.selftest()
+    # every rank learns whether any rank's communicator failed to come up
+    bad = comm.max_over_ranks(1.0 if init_err or rccl is None else 0.0)
+    err = init_err or ('another rank could not create its RCCL communicator' if bad else None)
+    if err is None and os.environ.get('SPARTAN_RCCL_SELFTEST', '1') != '0':
+      # every collective of the libspx data plane, once, on small tensors,
+      # checked on the host before any tile moves
+      err = comm.selftest()
     _ctx.selftest = err or 'ok'
     if err:
-      import warnings
-      warnings.warn('spartan_amd: the libspx RCCL data plane failed its self-test (%s); '
-                    'using torch.distributed\'s RCCL process group instead' % err)
-      import torch.distributed as dist
-      _ctx.pg = dist.new_group(backend='nccl')
-      _ctx.dist_backend = 'nccl'
-      _ctx.rccl = None  # not destroyed: a communicator in an unknown state may block in ncclCommDestroy
-      bad = comm.selftest()
-      if bad:
-        raise RuntimeError('spartan_amd: no working GPU data plane (libspx RCCL: %s; torch RCCL: %s)' % (err, bad))
+      _fall_back_to_torch_rccl(err)
   return _ctx
+
+
+def _fall_back_to_torch_rccl(err):
+  """Move the device collectives to torch.distributed's own RCCL group after
+  the libspx communicator failed (``err``); raise if that group fails too."""
+  import warnings
+  import torch.distributed as dist
+  from . import comm
+  warnings.warn('spartan_amd: the libspx RCCL data plane failed (%s); using torch.distributed\'s RCCL '
+                'process group instead' % err)
+  _ctx.pg = dist.new_group(backend='nccl')
+  _ctx.dist_backend = 'nccl'
+  _ctx.rccl = None  # not destroyed: a communicator in an unknown state may block in ncclCommDestroy
+  bad = comm.selftest()
+  _ctx.selftest = 'fallback (%s)' % err
+  if bad:
+    raise RuntimeError('spartan_amd: no working GPU data plane (libspx RCCL: %s; torch RCCL: %s)' % (err, bad))
 
 
 def shutdown():

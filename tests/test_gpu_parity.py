@@ -1364,3 +1364,69 @@ def test_kmeans_step_windows(ex):
   torch.testing.assert_close(sums, ws, rtol=1e-5, atol=0)  # the fp32 rule (points >= 0: sum |x| = sum x)
   # the window slots were used: a block's units span several flushes
   assert (N + 63) // 64 // 256 > 2 * 256
+
+
+def _step_check_all(be, P, Cd, rtol=1e-5):
+  """spx_kmeans_step on (P, Cd): labels equal the all-exact kernel's, counts
+  equal the bincount of them, sums within rtol of the fp64 index-add (points
+  >= 0, so sum |x| = sum x)."""
+  import torch
+  N, D = P.shape
+  K = Cd.shape[0]
+  lab = torch.empty((N,), dtype=torch.int64, device='cuda')
+  sums = torch.empty((K, D), dtype=torch.float64, device='cuda')
+  cnt = torch.empty((K,), dtype=torch.int64, device='cuda')
+  be.kmeans_step(P, Cd, lab, sums, cnt)
+  exact = torch.empty_like(lab)
+  be.kmeans_assign(P, Cd, exact, exact_only=True)
+  assert torch.equal(lab, exact)
+  assert torch.equal(cnt, torch.bincount(lab, minlength=K))
+  ws = torch.zeros((K, D), dtype=torch.float64, device='cuda')
+  ws.index_add_(0, lab, P.to(torch.float64))
+  torch.testing.assert_close(sums, ws, rtol=rtol, atol=0)
+  return lab, cnt
+
+
+@pytest.mark.parametrize('K', [2, 256])
+def test_kmeans_step_long_chains(ex, K):
+  """The advisory case: every window of a block puts (nearly) all of its rows
+  into one or two centres, so a centre's fp32 window chain is up to 64 x 256
+  rows long -- K = 2 over 12M rows, and K = 256 with 95 % of the rows next
+  to centre 0 (skewed, as a first iteration from data-point centres is).
+  Counts exact, labels exact, sums within 1e-5 of the fp64 sums."""
+  import torch
+  from spartan_amd import backend
+  be = backend.get()
+  N, D = 12_000_000, 64
+  P = torch.empty((N, D), dtype=torch.float32, device='cuda')
+  be.fill(P, backend.FILL_UNIFORM, 0.0, 1.0, 91, (0, 0), (N, D))
+  if K == 2:
+    Cd = torch.stack([torch.full((D,), 0.3), torch.full((D,), 0.7)]).to(torch.float64).cuda()
+  else:
+    P[: N * 95 // 100].mul_(0.01)  # 95 % of the rows in [0, 0.01): all nearest to centre 0
+    g = np.random.default_rng(5)
+    C = g.random((K, D)) * 0.5 + 0.5
+    C[0] = 0.005
+    Cd = torch.as_tensor(C).cuda()
+  lab, cnt = _step_check_all(be, P, Cd)
+  assert int(cnt.max()) > N // 2   # the chains really are long
+
+
+@pytest.mark.parametrize('N', [1, 31, 63, 64, 65, 4097, 64 * 256 * 3 + 17])
+def test_kmeans_step_same_row_units(ex, N):
+  """Every row of every 64-row unit carries the same label (identical rows):
+  the adds' table rounds take three rows of a centre and the other 61 go
+  through the ranked tail loop (spx.hip k_kmeans_fs2 add_end) -- the
+  data-dependent part of the unit loop -- with ragged tails (N not a
+  multiple of 64, fewer units than blocks, a single row).  Labels, counts
+  and sums as the two-pass path."""
+  import torch
+  from spartan_amd import backend
+  be = backend.get()
+  D, K = 128, 256
+  g = np.random.default_rng(N)
+  C = g.random((K, D))
+  row = (C[17] + 1e-3).astype(np.float32)
+  P = torch.as_tensor(np.tile(row, (N, 1))).cuda()
+  lab, cnt = _step_check_all(be, P, torch.as_tensor(C).cuda())
+  assert int(cnt[17]) == N

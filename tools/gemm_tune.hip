@@ -97,6 +97,14 @@ int main(int argc, char** argv) {
   i64 S = argc > 1 ? atoll(argv[1]) : 8192;
   int rounds = argc > 2 ? atoi(argv[2]) : 2;
   std::string which = argc > 3 ? argv[3] : "both";
+  if (which == "seg2") {  // two-level accumulation at <= 128 registers (32 x 64 / 64 x 32 wave tiles)
+    run<float>(S, rounds,
+               {V(float, 256, 128, 16, 4, 2, 8), VS(float, 256, 128, 16, 4, 2, 8, 16), VS(float, 128, 128, 16, 4, 2, 8, 16),
+                VS(float, 128, 128, 16, 2, 4, 8, 16), VS(float, 256, 128, 16, 8, 2, 8, 16), VS(float, 256, 128, 32, 8, 2, 8, 8),
+                VS(float, 128, 256, 16, 4, 4, 8, 16), VS(float, 256, 128, 16, 4, 4, 8, 16), VS(float, 128, 128, 32, 4, 2, 8, 8)},
+               157.3);
+    return 0;
+  }
   if (which == "seg") {  // two-level accumulation (SEG K-tiles per fresh accumulator) against one chain
     run<float>(S, rounds,
                {V(float, 256, 128, 16, 4, 2, 8), VS(float, 256, 128, 16, 4, 2, 8, 16), VS(float, 256, 128, 16, 4, 2, 8, 32),

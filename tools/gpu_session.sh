@@ -71,6 +71,8 @@ for s in $STEPS; do
         -d $O/kfs_lds -o p --output-format csv -- python3 $R/tools/km_step_once.py 100000000 2 > $O/kfs_lds.log 2>&1 ;;
     lregtune)
       cd $R && step lregtune 300 ./tools/bin/lreg_tune 100000000 3 > $O/lregtune.txt 2>&1 ;;
+    gemmseg2)
+      cd $R && step gemmseg2 600 ./tools/bin/gemm_tune 32768 2 seg2 > $O/gemmseg2.txt 2>&1 ;;
     gemmseg)
       cd $R && step gemmseg 600 ./tools/bin/gemm_tune 32768 2 seg > $O/gemmseg.txt 2>&1 ;;
     bench)
