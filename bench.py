@@ -218,11 +218,23 @@ def main():
     out = {k: cb[k] for k in ('value', 'unit', 'cores', 'kind', 'sample', 'single_process', 'host')}
     out['value'] = round(cb['value'], 3)
     legs = {}
-    for name, fn, kw in (('dot', CB.dot_cpu_baseline, {'S': 4096}),
-                         ('lreg', CB.lreg_cpu_baseline, {'N': 20_000_000}),
-                         ('kmeans', CB.kmeans_cpu_baseline, {'N': 1_000_000})):
+    # the side legs run on samples; each states its scale factor to the
+    # BASELINE.json size and the time projected there at the sample's rate
+    # (linear in N for lreg / k-means, the GFLOP/s held for the S^3 dot)
+    sized = (('dot', CB.dot_cpu_baseline, {'S': 4096}, '32768 x 32768 fp32 (configs[3])', (32768 / 4096) ** 3),
+             ('lreg', CB.lreg_cpu_baseline, {'N': 20_000_000}, '1e8 x 64 fp32 (configs[4])', 1e8 / 20_000_000),
+             ('kmeans', CB.kmeans_cpu_baseline, {'N': 1_000_000}, '1e8 x 128 fp32, k=256 (configs[2])',
+              1e8 / 1_000_000))
+    for name, fn, kw, full, factor in sized:
       try:
         legs[name] = fn(**kw)
+        lg = legs[name]
+        lg['baseline_size'] = full
+        lg['scale_to_baseline'] = factor
+        if name == 'dot':
+          lg['projected_seconds_at_baseline'] = round(2.0 * 32768 ** 3 / (lg['value'] * 1e9), 1)
+        else:
+          lg['projected_ms_per_iter_at_baseline'] = round(lg['ms_per_iter'] * factor, 1)
       except Exception as e:  # noqa: BLE001  (a failing side leg is reported, not fatal)
         legs[name] = {'error': '%s: %s' % (type(e).__name__, str(e)[:200])}
     out['legs'] = legs
@@ -358,11 +370,44 @@ def check_kmeans(X, labels, centers, comm, n_check=1 << 20, dist_dtype=np.float6
   return bool(comm.max_over_ranks(0.0 if ok else 1.0) == 0.0)
 
 
+def check_kmeans_sums(X, labels, sums, counts, comm, chunk=1 << 20):
+  """The last iteration's all-reduced counts against the bincount of its
+  labels (exact), and its centre sums against an fp64 index-add of the same
+  rows (torch fp64 on the device, a checker only), all-reduced over ranks:
+  every element within 1e-5 of the sum of |x| of its centre's rows."""
+  import torch
+  from spartan_amd import runtime
+  ctx = runtime.get()
+  K, D = sums.shape
+  ws = torch.zeros((K, D), dtype=torch.float64, device=ctx.device)
+  wa = torch.zeros((K, D), dtype=torch.float64, device=ctx.device)
+  wc = torch.zeros((K,), dtype=torch.int64, device=ctx.device)
+  for ex, tile in X.local.items():
+    lab = labels.local[[e for e in labels.local if e.ul[0] == ex.ul[0]][0]].data
+    for r0 in range(0, ex.shape[0], chunk):
+      # one-hot fp64 GEMMs, not index_add_ (its fp64 atomics serialise when
+      # most rows share a label, as a first iteration's may)
+      lb = lab[r0:r0 + chunk]
+      oh = torch.nn.functional.one_hot(lb, K).to(torch.float64).t()
+      xb = tile.data[r0:r0 + chunk].to(torch.float64)
+      ws += oh @ xb
+      wa += oh @ xb.abs()
+      wc += torch.bincount(lb, minlength=K)
+  comm.all_reduce(ws, 'sum')
+  comm.all_reduce(wa, 'sum')
+  comm.all_reduce(wc, 'sum')
+  ok = bool(np.array_equal(wc.cpu().numpy(), np.asarray(counts)))
+  ok &= bool(np.all(np.abs(np.asarray(sums) - ws.cpu().numpy()) <= 1e-5 * wa.cpu().numpy() + 1e-300))
+  return ok
+
+
 def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
   """configs[2]: one k-means iteration (spx_kmeans_step: the certified
   fp16 screen fused with the centroid accumulation, bf16x3 / exact-order
-  passes over its undecided rows = scipy-exact labels, fp64 centroid sums,
-  all-reduce) over npts x 128 fp32 points, k=256."""
+  passes over its undecided rows = scipy-exact labels, fp32 window sums
+  combined in fp64, all-reduce) over npts x 128 fp32 points, k=256.
+  Checked after the timed region: labels (a 1 M-row prefix, bit for bit),
+  counts (exact) and sums (1e-5 of sum |x|) of the last iteration."""
   import torch
   from spartan_amd import workloads
   X = expr.rand(npts * ctx.world_size, D, dtype=np.float32, seed=21).force()
@@ -376,6 +421,7 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
   comm.barrier()
   el = comm.max_over_ranks(time.perf_counter() - t0) / iters
   checked = check_kmeans(X, labels, info['assign_centers'], comm)
+  checked_sums = check_kmeans_sums(X, labels, info['sums'], info['counts'], comm)
   n = npts * ctx.world_size
   out = {'ms_per_iter': round(el * 1e3, 3), 'points_per_s': round(n / el, 1),
          'gemm_form_tflops': round(2.0 * n * K * D / el / 1e12, 2),
@@ -386,11 +432,12 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
          # 1.16 x that, profiles/r03_kmeans_step_pmc.json)
          'f16_mfma_frac_per_gpu': round(2.0 * n * K * D / el / 1e12 / (2500.0 * ctx.world_size), 4),
          'hbm_GBps_one_pass': round(4.0 * n * D / el / 1e9, 1),
-         'checked': checked,
+         'checked': checked and checked_sums, 'checked_labels': checked, 'checked_sums_counts': checked_sums,
          'config': 'cfg3: %d x %d fp32 points (U[0,1), seed 21) per GPU, k=%d, centres = first %d points; '
                    'spx_kmeans_step: certified fp16-MFMA screen + per-centre sums of the rows it decides in one '
                    'pass over X, bf16x3-MFMA pass + exact-order fp64 recompute of its undecided rows (bit-exact '
-                   'labels) + their gathered sums, fp64 centroid sums' % (npts, D, K, K)}
+                   'labels) + their gathered sums; centre sums in fp32 per block and window of 16128 rows, '
+                   'the windows combined in fp64' % (npts, D, K, K)}
   del X, labels
   torch.cuda.empty_cache()
   return out

@@ -1977,7 +1977,7 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
 // KC_TPT tiles per thread: 16 for the sparse full-row pass (~5 % of rows at
 // cfg3), 1 for the dense list pass (~20 % of its slots): a thread's rows are
 // written one after another, so a dense mask wants few tiles per thread.
-// LAYOUT 2 (k_kmeans_fs2): bit l < 32 <-> row 32 tile + l.  base_in (the
+// LAYOUT 2 (k_kmeans_pp): bit l < 32 <-> row 32 tile + l.  base_in (the
 // deterministic form, k_ks_count + k_exscan_u32): the block's first list slot
 // instead of an atomic on cnt -- the list is then in row order.
 template <int KC_TPT, int LAYOUT = 0>
@@ -2024,7 +2024,7 @@ __global__ __launch_bounds__(256) void k_ks_compact(i64 N, const unsigned long l
       if (LAYOUT == 0) {  // 32x32 output layout (k_kmeans_filter_as)
         const int q = (l & 31) >> 1, h = l >> 5;
         slot = tl * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-      } else {  // point order (k_kmeans_fs2)
+      } else {  // point order (k_kmeans_pp)
         slot = tl * 32 + l;
       }
       out[pos++] = rows_in ? rows_in[slot] : slot;
@@ -2075,125 +2075,113 @@ static void ks_launch_n(int nct, hipStream_t s, i64 N, i64 D, const float* P, i6
 }
 
 // ---------------------------------------------------------------------------
-// Shared by the fused k-means step (k_kmeans_fs2 below): 8 waves per block,
-// 64-row units (two 32-row MFMA tiles), the per-screening-wave exchange rows
-// of the decision, the fp16 row stride and the DPP helpers.
-typedef float kfs_f2 __attribute__((ext_vector_type(2)));
-constexpr int KFS_WAVES = 8;
-constexpr int KFS_U = 64;  // rows per unit (two 32-row MFMA tiles)
-// exchange strides per screening wave: +32 B / +32 B so the 8 lanes of a
-// decide row group (one per screening wave) read 8 different bank groups
-// (ds_read_b64: bank (a / 4) mod 64, ds_read_b32: mod 32)
-constexpr int KFS_EXV_S = 2 * KFS_U + 8, KFS_EXI_S = KFS_U + 8;
-constexpr int KFS_PU = KFS_U + 4;  // |x'|^2 partial rows per wave: +16 B, the same for the decision's p2 reads
-__host__ __device__ constexpr int kfs_rs(int D) { return 2 * D + 16; }  // fp16 row stride: +16 B keeps ds_read_b128 conflict-free
-
-template <int CTL>
-__device__ __forceinline__ float kfs_dppf(float x) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTL, 0xF, 0xF, false));
-}
-template <int CTL>
-__device__ __forceinline__ int kfs_dppi(int x) {
-  return __builtin_amdgcn_update_dpp(0, x, CTL, 0xF, 0xF, false);
-}
-
-// ---------------------------------------------------------------------------
-// Fused k-means step (k_kmeans_fs2): the fp16 screen AND the centroid
+// Fused k-means step (k_kmeans_pp): the fp16 screen AND the centroid
 // accumulation in ONE pass over the points (spx_kmeans_step;
 // kmeans_dist_mapper + argmin + kmeans_count_mapper + kmeans_center_mapper,
-// k_means_.py:52-89, 126-136).  One block per CU, 8 waves, one loop
-// iteration per 64-row unit, two barriers:
-//   phase 1   screen: wave w < NCT keeps ITS 32 centres in registers (the
-//             MFMA A operand, fp16(c') as k_kmeans_filter_as MODE 1 stages
-//             them, plus the -cc/2 pieces); two chains of 8 fp16 MFMAs + 1
-//             bf16 MFMA (-cc/2) over the unit's fp16 x' in LDS give S - cc/2
-//             = -a''/2 for 32 centres x 64 points; a per-lane top-2 over the
-//             lane's 16 centres (4-bit register tags, priced in the bound),
-//             a v_permlane32_swap half-swap, (b1, b2, index) per point to
-//             LDS.  Woven between the MFMAs: the table rounds of the previous
-//             unit's adds (below) and its label / undecided-bit stores;
-//   phase 2   decide: wave w takes rows 8w .. 8w + 7, one lane per (row,
-//             screening wave): top-2 over the NCT candidates by three DPP
-//             exchanges, then the certified rule b1 - b2 > e(|x'|) (the same
-//             bound, kq and finiteness checks as MODE 1); add the previous
-//             unit's decided rows into the LDS sums; stage the next unit
-//             (x' = fl(x - mu), fp16(x') to LDS, |x'|^2 partials).
+// k_means_.py:52-89, 126-136).
+//
+// Ping-pong over 32-row units.  One block per CU, 8 waves in two groups:
+// waves 0-3 (group 0) and 4-7 (group 1), wave s of each group on SIMD s
+// (a workgroup's waves w and w + 4 share a SIMD).  Unit u belongs to group
+// u & 1.  Slot t (one barrier each): group t & 1 plays the MATRIX role, the
+// other group the VECTOR role, so on every SIMD one wave keeps the matrix
+// pipe busy while its partner does vector / LDS work (MI355X_MICROARCH.md
+// "Two waves per SIMD"):
+//   matrix role (group t & 1): the screen of unit t -- wave s holds centre
+//     tiles 2s, 2s + 1 (64 centres) as the fp16 MFMA A operand plus their
+//     -cc/2 pieces; two chains of 8 v_mfma_f32_32x32x16_f16 + 1 bf16 MFMA
+//     (-cc/2) over unit t's fp16 x' (LDS) give S - cc/2 = -a''/2 for 64
+//     centres x 32 rows.  Woven between those MFMAs: the decision of unit
+//     t - 2 (this group's previous unit; its candidates were folded in slot
+//     t - 1), the table rounds of its adds; after them the read-add-writes
+//     of unit t - 2's decided rows into the LDS sums, its labels and
+//     undecided bits, and the loads of unit t + 4;
+//   vector role (the other group): fold unit t - 1's accumulators (its
+//     matrix role of slot t - 1) to per-row top-2 candidates, and stage unit
+//     t + 1 (x' = fl(x - mu), fp16(x') to LDS, |x'|^2 column partials).
+// Every cross-wave hand-off crosses at least one barrier: x' is staged one
+// slot before its MFMAs (xh by unit parity), candidates are folded one slot
+// before their decision (exv by unit parity), |x'|^2 partials three slots
+// before (p2p by unit mod 4); the sums are written by the matrix group only.
+// The certified decision is k_kmeans_filter_as MODE 1's (same MFMA chains,
+// bound, kq and finiteness checks; 4-bit register tags per centre tile).
 // Accumulation: the block's per-centre sums live in LDS as fp32 [256][D]
-// (128 KiB at D = 128; columns XOR-swizzled by the centre to spread the
-// banks).  The unit is loaded column-split -- wave w holds columns w D/8 ..
-// + D/8 of ALL 64 rows (lane = row) -- so a wave adds its rows straight from
-// the registers their loads landed in, and waves never share an address.
-// Two rows of one centre in one unit would race in a plain read-add-write
-// (LDS float atomics measured ~3.5x slower for the whole step), so the adds
-// go in rounds: a row joins round k when its lane wins its centre's slot in
-// the wave's byte table at the k-th write / read-back (one winner per centre
-// and round, the LDS unit's fixed choice); rounds 0 and 1 cover all but the
-// rare third row of a centre, which loops.  The order of every add is fixed:
-// the sums are deterministic.  |x'|^2 comes as 8 column partials per row,
-// summed in a fixed DPP tree (all 8 lanes of a row get the same bits).
-// Labels (a coalesced 64 B store per wave) and the undecided-row mask go
-// out one unit behind the decision; every global store is issued
-// unconditionally (ghost / tail rows write to a dummy word), so the
-// compiler's count of the loads in flight stays static.  Every KF2_FW units
-// the fp32 sums go by plain stores to the block's partial slot for that
-// window and are cleared (an fp32 chain covers ~KF2_FW / 4 rows of one
-// centre, ~64 here); the slots are summed in fp64 in a fixed order after the
-// kernel.  Ring: unit u lives in register slot u % KF2_NS from its load (two
-// units ahead) through its staging until its add one iteration after its
-// decision.
-constexpr int KF2_NS = 4;
-constexpr int KF2_FW = 256;
-static_assert(KF2_FW % KF2_NS == 0, "the flush points must fall on the unrolled body's first copy");
-static size_t kf2_lds_bytes(int D) {
-  return (size_t)256 * D * 4 + 256 * 4 + (size_t)KFS_U * kfs_rs(D) + (size_t)2 * KFS_WAVES * KFS_PU * 4 +
-         (size_t)KFS_WAVES * (KFS_EXV_S + KFS_EXI_S) * 4 + KFS_U * 4 + KFS_WAVES * 256 + 64;
+// (columns XOR-swizzled by the centre).  Lane (j, h) of wave s holds columns
+// D/4 s + D/8 h .. + D/8 of row j, so a wave adds its rows from the registers
+// the loads landed in and waves never share an address.  Two rows of one
+// centre in one unit would race in a plain read-add-write, so the adds go in
+// rounds decided by a per-wave byte table (a row joins round k when it wins
+// its centre's slot at the k-th write / read-back, the LDS unit's fixed
+// choice); a centre's fourth and later rows are ranked by ballots over the
+// distinct labels (a loop of at most 32 steps: each removes one label; a
+// device trap guards the bound).  The order of every add is fixed: the sums
+// are deterministic.  Every KP_FW units the fp32 sums go by plain stores to
+// the block's partial slot for that window and are cleared; the slots are
+// summed in fp64 in a fixed order after the kernel.  Global stores are
+// issued unconditionally (ghost rows write a dummy word), so the count of
+// loads in flight that the compiler tracks is the same in every slot.
+typedef float kfs_f2 __attribute__((ext_vector_type(2)));
+typedef int kfs_i2 __attribute__((ext_vector_type(2)));
+__host__ __device__ constexpr int kfs_rs(int D) { return 2 * D + 16; }  // fp16 row stride: +16 B keeps ds_read_b128 conflict-free
+constexpr int KP_WAVES = 8;
+constexpr int KP_U = 32;     // rows per unit (one 32-row MFMA tile)
+constexpr int KP_NR = 3;     // units per group in the register ring (load -> stage -> MFMA -> add)
+constexpr int KP_AHEAD = 4;  // unit t + 4 is loaded in slot t (its stage is in slot t + 3)
+constexpr int KP_UNR = 6;    // slots per unrolled loop body: ring entries (unit >> 1) % 3 are compile-time
+constexpr int KP_FW = 504;   // units per flush window (16128 rows)
+constexpr int KP_XS = 48;    // exv / p2p row stride (bytes): 12 dwords, spreads a lane group's rows over the banks
+static_assert(KP_FW % KP_UNR == 0 && KP_UNR == 2 * KP_NR && KP_AHEAD == 2 * (KP_NR - 1),
+              "flush points fall on the unrolled body's first slot; the ring cycles once per body");
+static size_t kp_lds_bytes(int D) {
+  return (size_t)256 * D * 4 + 256 * 4 + (size_t)2 * KP_U * kfs_rs(D) + (size_t)2 * KP_U * KP_XS +
+         (size_t)4 * KP_U * KP_XS + 4 * 256 + 64;
 }
 
-#ifndef KF2_PROF
-#define KF2_PROF 0  // dev builds: per-wave cycles per loop segment (s_memtime) -> spx_dev_kf2_prof
-#endif
-#if KF2_PROF
-__device__ unsigned long long g_kf2_prof[256 * 8 * 9];
-extern "C" int spx_dev_kf2_prof(unsigned long long* host_out) {
-  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_kf2_prof), sizeof(g_kf2_prof)) == hipSuccess ? 0 : 1;
-}
-#endif
 template <int KS, int NCT>
-__global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
+struct KpStep {
+  static constexpr int D = 16 * KS, CPW = D / 4, CPL = D / 8, NQ = CPL / 4, RS = kfs_rs(D), U = KP_U,
+                       NR = KP_NR;
+  static_assert(CPL % 8 == 0, "D = 64 or 128");
+};
+
+template <int KS, int NCT>
+__global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     i64 N, i64 K, const float* __restrict__ P, i64 ldp, const __bf16* __restrict__ CBh,
     const __bf16* __restrict__ CBl, const float* __restrict__ cnf2, const double* cmax_p,
     const float* __restrict__ muf, i64* __restrict__ labels, unsigned long long* __restrict__ und_mask,
     float* __restrict__ part, int nwin, unsigned long long* __restrict__ pcnt, unsigned long long* __restrict__ dummy) {
-  constexpr int D = 16 * KS, CPW = D / 8, RS = kfs_rs(D), W = KFS_WAVES, U = KFS_U, NS = KF2_NS;
-  static_assert(CPW % 8 == 0, "D = 64 or 128");
-  extern __shared__ __attribute__((aligned(16))) unsigned char kf2_lds[];
-  float* sums = (float*)kf2_lds;                         // [256][D] fp32, column c of centre d at c ^ (d & (D - 4))
+  typedef KpStep<KS, NCT> C;
+  constexpr int D = C::D, CPW = C::CPW, CPL = C::CPL, NQ = C::NQ, RS = C::RS, U = C::U, NR = C::NR;
+  extern __shared__ __attribute__((aligned(16))) unsigned char kp_lds[];
+  float* sums = (float*)kp_lds;                          // [256][D] fp32, column c of centre d at c ^ (d & (D - 4))
   unsigned int* cnts = (unsigned int*)(sums + 256 * D);  // [256] decided rows per centre
-  unsigned char* xh = (unsigned char*)(cnts + 256);      // [U][RS] fp16 x'
-  float* p2p = (float*)(xh + (size_t)U * RS);            // [2][W][KFS_PU] |x'|^2 over wave w's columns
-  float* exv = p2p + 2 * W * KFS_PU;                     // [W][KFS_EXV_S] (b1, b2) per row
-  int* exi = (int*)(exv + W * KFS_EXV_S);                // [W][KFS_EXI_S] best centre
-  short* dl = (short*)(exi + W * KFS_EXI_S);             // [2][U] label of a decided row, -1 otherwise (by unit parity)
-  unsigned char* tbl = (unsigned char*)(dl + 2 * U);       // [W][256] per-wave winner table of the add rounds
-  unsigned char* ldum = tbl + W * 256;                   // [64] per-lane dummy byte of the straight-line table rounds
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, j = lane & 31, h = lane >> 5;
-  const int col0 = w * CPW;
-  for (int i = t; i < 256 * D + 256; i += W * 64) sums[i] = 0.f;  // (cnts: the same bits)
-  if (t < 2 * U) dl[t] = -1;
-  float mu[CPW];
+  unsigned char* xh = (unsigned char*)(cnts + 256);      // [2][U][RS] fp16 x' (by unit parity)
+  unsigned char* exv = xh + (size_t)2 * U * RS;          // [2][U][KP_XS]: (b1, b2) of waves 0-3, then their 4 indices
+  unsigned char* p2p = exv + (size_t)2 * U * KP_XS;      // [4][U][KP_XS]: 8 |x'|^2 column partials (by unit mod 4)
+  unsigned char* tbl = p2p + (size_t)4 * U * KP_XS;      // [4][256] per-wave winner table of the add rounds
+  unsigned char* ldum = tbl + 4 * 256;                   // [64] per-lane dummy byte of the table rounds
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, grp = w >> 2, s = w & 3, j = lane & 31, h = lane >> 5;
+  const int col0 = CPW * s + CPL * h;
+  for (int i = t; i < 256 * D + 256; i += KP_WAVES * 64) sums[i] = 0.f;  // (cnts: the same bits)
+  float mu[CPL];
 #pragma unroll
-  for (int e = 0; e < CPW; ++e) mu[e] = muf[col0 + e];
+  for (int e = 0; e < CPL; ++e) mu[e] = muf[col0 + e];
 
-  kh_f8 ca[KS];
-  kb_bf8 ccp;
-  {
-    const i64 c = 32 * (i64)(w < NCT ? w : 0) + j;
+  // A operands: wave s screens centre tiles 2s and 2s + 1 (lane (j, h):
+  // centre 32 ct + j, dims 16 ks + 8 h .. + 8 of k-step ks)
+  const bool scr0 = 2 * s < NCT, scr1 = 2 * s + 1 < NCT;
+  kh_f8 ca[2][KS];
+  kb_bf8 ccp[2];
+#pragma unroll
+  for (int tl = 0; tl < 2; ++tl) {
+    const int ct = 2 * s + tl;
+    const i64 c = 32 * (i64)(ct < NCT ? ct : 0) + j;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const i64 d = 16 * ks + 8 * h + e;
-        ca[ks][e] = (_Float16)((float)CBh[c * D + d] + (float)CBl[c * D + d]);
+        ca[tl][ks][e] = (_Float16)((float)CBh[c * D + d] + (float)CBl[c * D + d]);
       }
     const float v = -0.5f * cnf2[c];
     const __bf16 b1 = (__bf16)v;
@@ -2201,7 +2189,7 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
     const __bf16 b2 = (__bf16)v1;
     const __bf16 b3 = (__bf16)(v1 - (float)b2);
     const __bf16 z = (__bf16)0.f;
-    ccp = h == 0 ? (kb_bf8){b1, b2, b3, z, z, z, z, z} : (kb_bf8){z, z, z, z, z, z, z, z};
+    ccp[tl] = h == 0 ? (kb_bf8){b1, b2, b3, z, z, z, z, z} : (kb_bf8){z, z, z, z, z, z, z, z};
   }
   const __bf16 one = (__bf16)1.f;
   const kb_bf8 ones = (kb_bf8){one, one, one, one, one, one, one, one};
@@ -2222,22 +2210,26 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
   const float pn_lim = (float)(cmax > 0.0 ? 1e36 / cmax : 1e36);
 
   const int G = gridDim.x, bk = blockIdx.x;
-  const i64 nunits = (N + U - 1) / U, ntiles = (N + 31) / 32;
+  const i64 nunits = (N + U - 1) / U;
   const int nit = bk < nunits ? (int)((nunits - 1 - bk) / G + 1) : 0;
-  kb_f4 ring[NS][CPW / 4];
-  auto load = [&](kb_f4 (&r)[CPW / 4], int it) __attribute__((always_inline)) {  // clamped: always a valid address
-    const i64 un = bk + (i64)(it < nit ? it : nit - 1) * G;
-    i64 row = un * U + lane;
+  // slots 0 .. nit + 1 (unit nit - 1 is added in slot nit + 1), whole bodies
+  const int nrun = nit > 0 ? (nit + 2 + KP_UNR - 1) / KP_UNR * KP_UNR : 0;
+
+  kb_f4 ring[NR][NQ];
+  kb_acc acc0 = (kb_acc){}, acc1 = (kb_acc){};
+  auto load = [&](kb_f4 (&r)[NQ], int u) __attribute__((always_inline)) {  // clamped: always a valid address
+    const i64 un = bk + (i64)(u < nit ? u : nit - 1) * G;
+    i64 row = un * U + j;
     row = row < N ? row : N - 1;
     const float* p = P + row * ldp + col0;
 #pragma unroll
-    for (int q = 0; q < CPW / 4; ++q) r[q] = *(const kb_f4*)(p + 4 * q);
+    for (int q = 0; q < NQ; ++q) r[q] = *(const kb_f4*)(p + 4 * q);
   };
-  auto stage = [&](const kb_f4 (&r)[CPW / 4], int b) __attribute__((always_inline)) {  // slot -> xh, p2p[b]
-    _Float16 hv[CPW];
+  auto stage = [&](const kb_f4 (&r)[NQ], int u) __attribute__((always_inline)) {  // unit u -> xh[u & 1], p2p[u & 3]
+    _Float16 hv[CPL];
     kfs_f2 p2v = (kfs_f2){0.f, 0.f};
 #pragma unroll
-    for (int q = 0; q < CPW / 4; ++q)
+    for (int q = 0; q < NQ; ++q)
 #pragma unroll
       for (int e = 0; e < 4; e += 2) {
         const kfs_f2 x = (kfs_f2){r[q][e], r[q][e + 1]} - (kfs_f2){mu[4 * q + e], mu[4 * q + e + 1]};
@@ -2245,15 +2237,21 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
         hv[4 * q + e] = (_Float16)x[0];
         hv[4 * q + e + 1] = (_Float16)x[1];
       }
-    unsigned char* hrow = xh + (size_t)lane * RS + 2 * col0;
+    unsigned char* hrow = xh + ((size_t)(u & 1) * U + j) * RS + 2 * col0;
 #pragma unroll
-    for (int g = 0; g < CPW / 8; ++g)
-      *(kh_f8*)(hrow + 16 * g) = (kh_f8){hv[8 * g], hv[8 * g + 1], hv[8 * g + 2], hv[8 * g + 3],
-                                         hv[8 * g + 4], hv[8 * g + 5], hv[8 * g + 6], hv[8 * g + 7]};
-    p2p[(b * W + w) * KFS_PU + lane] = p2v[0] + p2v[1];
+    for (int gq = 0; gq < CPL / 8; ++gq)
+      *(kh_f8*)(hrow + 16 * gq) = (kh_f8){hv[8 * gq], hv[8 * gq + 1], hv[8 * gq + 2], hv[8 * gq + 3],
+                                          hv[8 * gq + 4], hv[8 * gq + 5], hv[8 * gq + 6], hv[8 * gq + 7]};
+    *(float*)(p2p + ((size_t)(u & 3) * U + j) * KP_XS + 4 * (2 * s + h)) = p2v[0] + p2v[1];
   };
-
-  auto fold16 = [&](const kb_acc& acc, float& lo, float& sec, int& il) __attribute__((always_inline)) {
+  // lane j and lane j + 32 exchange x: both get (x of lane j, x of lane j + 32)
+  auto sw32 = [](float x, float& lo, float& hi) __attribute__((always_inline)) {
+    const unsigned int b = __builtin_bit_cast(unsigned int, x);
+    const auto r = __builtin_amdgcn_permlane32_swap(b, b, false, false);
+    lo = __builtin_bit_cast(float, (unsigned int)r[0]);
+    hi = __builtin_bit_cast(float, (unsigned int)r[1]);
+  };
+  auto fold16 = [&](const kb_acc& acc, int ct, float& lo, float& sec, int& il) __attribute__((always_inline)) {
     float tv[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -2268,83 +2266,32 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
       lo = ks_max3(lo, tv[q], tv[q + 1]);
     }
     const unsigned int qb = __builtin_bit_cast(unsigned int, lo) & 15u;
-    il = 32 * w + (int)((qb & 3) + 8 * (qb >> 2)) + 4 * h;
+    il = 32 * ct + (int)((qb & 3) + 8 * (qb >> 2)) + 4 * h;
   };
-  auto screen_fold = [&](const kb_acc& a0, const kb_acc& a1) __attribute__((always_inline)) {
-    float loa, seca, lob, secb;
-    int ila, ilb;
-    fold16(a0, loa, seca, ila);
-    fold16(a1, lob, secb, ilb);
-    // half-swap by v_permlane32_swap (VALU, no LDS round trip): lanes 0-31
-    // end with tile 0's candidates of point j from both halves, lanes 32-63
-    // with tile 1's; the top-2 merge is symmetric in the two, and on equal
-    // values the row stays undecided, so the index tie-break does not matter
-    auto sw32 = [](float x, float y, float& r0, float& r1) __attribute__((always_inline)) {
-      const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned int, x),
-                                                      __builtin_bit_cast(unsigned int, y), false, false);
-      r0 = __builtin_bit_cast(float, (unsigned int)r[0]);
-      r1 = __builtin_bit_cast(float, (unsigned int)r[1]);
-    };
-    float l0, l1, s0, s1, f0, f1;
-    sw32(loa, lob, l0, l1);
-    sw32(seca, secb, s0, s1);
-    sw32(__builtin_bit_cast(float, ila), __builtin_bit_cast(float, ilb), f0, f1);
-    const float b1 = ks_max(l0, l1);
-    const float b2 = ks_med3(l0, l1, ks_max(s0, s1));
-    const int ib = l0 >= l1 ? __builtin_bit_cast(int, f0) : __builtin_bit_cast(int, f1);
-    // lane (j, h) holds unit row 32 h + j = lane
-    *(kfs_f2*)(exv + w * KFS_EXV_S + 2 * lane) = (kfs_f2){b1, b2};
-    exi[w * KFS_EXI_S + lane] = ib;
+  // vector role, part 1: unit u's accumulators -> the wave's top-2 over its
+  // 64 centres per row -> exv[u & 1] (lane j: (b1, b2), lane j + 32: index)
+  auto fold = [&](int u) __attribute__((always_inline)) {
+    float lo0 = -INFINITY, sec0 = -INFINITY, lo1 = -INFINITY, sec1 = -INFINITY;
+    int il0 = 0, il1 = 0;
+    if (scr0) fold16(acc0, 2 * s, lo0, sec0, il0);
+    if (scr1) fold16(acc1, 2 * s + 1, lo1, sec1, il1);
+    const float b1 = ks_max(lo0, lo1), b2 = ks_med3(lo0, lo1, ks_max(sec0, sec1));
+    const int ib = lo0 >= lo1 ? il0 : il1;
+    // the other 32 centres of row j sit in lane j + 32 (and vice versa): a
+    // half swap; the merge is symmetric, so both lanes end with the same bits
+    float b1l, b1h, b2l, b2h, fl, fh;
+    sw32(b1, b1l, b1h);
+    sw32(b2, b2l, b2h);
+    sw32(__builtin_bit_cast(float, ib), fl, fh);
+    const float B1 = ks_max(b1l, b1h), B2 = ks_med3(b1l, b1h, ks_max(b2l, b2h));
+    const int IB = b1l >= b1h ? __builtin_bit_cast(int, fl) : __builtin_bit_cast(int, fh);
+    unsigned char* er = exv + ((size_t)(u & 1) * U + j) * KP_XS;
+    if (h == 0)
+      *(kfs_f2*)(er + 8 * s) = (kfs_f2){B1, B2};
+    else
+      *(int*)(er + 32 + 4 * s) = IB;
   };
 
-  // decision of unit it (its |x'|^2 partials in p2p[b]); wave w: rows 8 w .. + 7
-  // (pre: issued after the decision's own LDS loads -- round 0's reads of
-  // the adds, whose latency the DPP chain then covers; issued before them,
-  // they would delay the decision's loads, which return in order behind them)
-  auto decide = [&](int it, int b, auto&& pre) __attribute__((always_inline)) {
-    const int r = lane >> 3, v = lane & 7, row = 8 * w + r;
-    float b1 = -INFINITY, b2 = -INFINITY;
-    int ib = 0;
-    if (NCT == 8 || v < NCT) {
-      const kfs_f2 e2 = *(const kfs_f2*)(exv + v * KFS_EXV_S + 2 * row);
-      b1 = e2[0];
-      b2 = e2[1];
-      ib = exi[v * KFS_EXI_S + row];
-    }
-    float p2f = p2p[(b * W + v) * KFS_PU + row];
-    pre();
-    auto merge = [&](auto ctl) __attribute__((always_inline)) {
-      constexpr int C = decltype(ctl)::value;
-      const float pb1 = kfs_dppf<C>(b1), pb2 = kfs_dppf<C>(b2);
-      const int pib = kfs_dppi<C>(ib);
-      b2 = ks_med3(b1, pb1, ks_max(b2, pb2));
-      ib = pb1 > b1 ? pib : ib;
-      b1 = ks_max(b1, pb1);
-      p2f += kfs_dppf<C>(p2f);  // a fixed tree: the row's 8 lanes end with the same bits
-    };
-    merge(std::integral_constant<int, 0xB1>{});
-    merge(std::integral_constant<int, 0x4E>{});
-    merge(std::integral_constant<int, 0x141>{});
-    const float pn = __builtin_amdgcn_sqrtf(__builtin_fmaf(p2f, 1.001f, 1e-37f)) * 1.0001f;
-    const float e = __builtin_fmaf(__builtin_fmaf(kq[2], pn, kq[1]), pn, kq[0]) * 1.0001f;
-    const bool fin = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim && isfinite(b1) && isfinite(b2);
-    const i64 grow = (bk + (i64)it * G) * U + row;
-    const bool live = it < nit && grow < N;
-    const bool dec = fin && b1 - b2 > 1.0001f * e;
-    if (v == 0) dl[b * U + row] = (short)(live && dec ? ib : -1);
-  };
-
-  // Unit it - 1's decided rows go into the LDS sums by plain read-add-writes.
-  // Rows of one centre in one unit would race there, so the adds go in
-  // rounds: a row joins round k when its lane wins its centre's slot in this
-  // wave's table at the k-th write / read-back (one winner per centre and
-  // round; which lane wins is the LDS unit's fixed choice).  The table
-  // rounds (three dependent LDS round trips) are woven between unit it's
-  // MFMAs in phase 1, where the wave's issue would otherwise wait on the
-  // matrix pipe; the read-add-writes of rounds 0 and 1 run in phase 2 beside
-  // the decision (straight-line code: lanes outside a round read and write
-  // their own dummy slot), then the rare rows of a centre's third and later
-  // add in a loop.
   typedef __attribute__((address_space(3))) unsigned char lds_u8;
   // (relaxed atomics on the table: not folded into the lane's own store like
   // plain accesses, and not waited for at once like volatile ones)
@@ -2354,67 +2301,89 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
   auto tget = [](lds_u8* p) __attribute__((always_inline)) {
     return (int)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
-  unsigned char* const dum = ldum + lane;
-  lds_u8* const tb = (lds_u8*)(tbl + w * 256);
-  lds_u8* const tdum = (lds_u8*)dum;
-  struct Rounds {
-    int d;          // the row's label (< 0: not decided)
-    int dlr;        // label of row 8 w + lane / 8 (out_labels' store)
-    bool w0, w1, w2;  // the row adds in round 0 / 1 / 2
-    bool more;        // the row adds after round 2 (a centre's fourth row in a unit: rare)
-  };
-  auto screen_tbl = [&](kb_acc& a0, kb_acc& a1, int bp) __attribute__((always_inline)) {
-    const bool scr = NCT == 8 || w < NCT;
-    const unsigned char* bpa = xh + (size_t)j * RS + 16 * h;
-    const unsigned char* bpb = bpa + (size_t)32 * RS;
-    a0 = (kb_acc){};
-    a1 = (kb_acc){};
-    Rounds R{0, 0, false, false, false, false};
-    bool act = false, rem = false;
-    int tv = 0;  // the table byte read back (compared one step later)
+  lds_u8* const tb = (lds_u8*)(tbl + s * 256);
+  lds_u8* const tdum = (lds_u8*)(ldum + lane);
+
+  // matrix role of slot t: MFMAs of unit t (if t < nit) with the decision
+  // and table rounds of unit t - 2 woven between them; then unit t - 2's
+  // read-add-writes, labels and undecided bits; then the loads of unit t + 4
+  // into the ring entry unit t - 2 leaves.
+  auto matrix_role = [&](int tt, kb_f4 (&r)[NQ]) __attribute__((always_inline)) {
+    const bool mf = tt < nit;
+    const int u2 = tt - 2;
+    const bool dv = u2 >= 0 && u2 < nit;
+    const i64 un2 = bk + (i64)(dv ? u2 : 0) * G;
+    const i64 grow = un2 * U + j;
+    const bool rlive = dv && grow < N;
+    const unsigned char* bp = xh + ((size_t)(tt & 1) * U + j) * RS + 16 * h;
+    const unsigned char* er = exv + ((size_t)(u2 & 1) * U + j) * KP_XS;
+    const unsigned char* pr = p2p + ((size_t)(u2 & 3) * U + j) * KP_XS;
+    if (mf) {
+      acc0 = (kb_acc){};
+      acc1 = (kb_acc){};
+    }
+    int d = -1, tv = 0;
+    bool act = false, rem = false, w0 = false, w1 = false, w2 = false, more = false;
+    kb_f4 e4, p4;
+    kfs_i2 i2;
+    float b1 = 0.f, b2 = 0.f, pp = 0.f;
+    int ib = 0;
     auto step = [&](auto kc) __attribute__((always_inline)) {
       constexpr int k = decltype(kc)::value;
       if constexpr (k == 0) {
-        R.d = dl[bp * U + lane];
-        R.dlr = dl[bp * U + 8 * w + (lane >> 3)];
+        e4 = *(const kb_f4*)(er + 16 * h);
+        i2 = *(const kfs_i2*)(er + 32 + 8 * h);
+        p4 = *(const kb_f4*)(pr + 16 * h);
       } else if constexpr (k == 1) {
-        act = R.d >= 0;
-        tput(act ? tb + R.d : tdum, lane);
+        b1 = ks_max(e4[0], e4[2]);
+        b2 = ks_med3(e4[0], e4[2], ks_max(e4[1], e4[3]));
+        ib = e4[0] >= e4[2] ? i2[0] : i2[1];
+        pp = (p4[0] + p4[1]) + (p4[2] + p4[3]);
       } else if constexpr (k == 2) {
-        tv = tget(act ? tb + R.d : tdum);
-      } else if constexpr (k == 3) {  // (no short-circuit: a branch would split the straight-line block)
-        R.w0 = act & (tv == lane);
-        rem = act & !R.w0;
-        tput(rem ? tb + R.d : tdum, lane);
+        float b1l, b1h, b2l, b2h, fl, fh, pl, ph;
+        sw32(b1, b1l, b1h);
+        sw32(b2, b2l, b2h);
+        sw32(__builtin_bit_cast(float, ib), fl, fh);
+        sw32(pp, pl, ph);
+        const float B1 = ks_max(b1l, b1h), B2 = ks_med3(b1l, b1h, ks_max(b2l, b2h));
+        const int IB = b1l >= b1h ? __builtin_bit_cast(int, fl) : __builtin_bit_cast(int, fh);
+        const float p2f = pl + ph;  // the same order in both lanes of the row
+        const float pn = __builtin_amdgcn_sqrtf(__builtin_fmaf(p2f, 1.001f, 1e-37f)) * 1.0001f;
+        const float e = __builtin_fmaf(__builtin_fmaf(kq[2], pn, kq[1]), pn, kq[0]) * 1.0001f;
+        const bool fin = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim && isfinite(B1) && isfinite(B2);
+        const bool dec = fin && B1 - B2 > 1.0001f * e;
+        d = rlive && dec ? IB : -1;
+      } else if constexpr (k == 3) {
+        act = d >= 0;
+        tput(act ? tb + d : tdum, j);
       } else if constexpr (k == 4) {
-        tv = tget(rem ? tb + R.d : tdum);
-      } else if constexpr (k == 5) {
-        R.w1 = rem & (tv == lane);
-        rem = rem & !R.w1;
-        tput(rem ? tb + R.d : tdum, lane);
+        tv = tget(act ? tb + d : tdum);
+      } else if constexpr (k == 5) {  // (no short-circuit: a branch would split the straight-line block)
+        w0 = act & (tv == j);
+        rem = act & !w0;
+        tput(rem ? tb + d : tdum, j);
       } else if constexpr (k == 6) {
-        tv = tget(rem ? tb + R.d : tdum);
+        tv = tget(rem ? tb + d : tdum);
       } else if constexpr (k == 7) {
-        R.w2 = rem & (tv == lane);
-        R.more = rem & !R.w2;
+        w1 = rem & (tv == j);
+        rem = rem & !w1;
+        tput(rem ? tb + d : tdum, j);
+      } else if constexpr (k == 8) {
+        tv = tget(rem ? tb + d : tdum);
+      } else if constexpr (k == 9) {
+        w2 = rem & (tv == j);
+        more = rem & !w2;
       }
     };
-    // B fragments one k-step ahead: an MFMA's wait for its operands then
-    // covers only LDS operations issued a step earlier
-    kh_f8 va = *(const kh_f8*)bpa, vb = *(const kh_f8*)bpb;
-    auto mf = [&](auto kc) __attribute__((always_inline)) {
+    // B fragments one k-step ahead
+    kh_f8 b = *(const kh_f8*)bp;
+    auto mk = [&](auto kc) __attribute__((always_inline)) {
       constexpr int ks = decltype(kc)::value;
-      kh_f8 na = va, nb = vb;
-      if constexpr (ks + 1 < KS) {
-        na = *(const kh_f8*)(bpa + 32 * (ks + 1));
-        nb = *(const kh_f8*)(bpb + 32 * (ks + 1));
-      }
-      if (scr) {
-        a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[ks], va, a0, 0, 0, 0);
-        a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[ks], vb, a1, 0, 0, 0);
-      }
-      va = na;
-      vb = nb;
+      kh_f8 nb = b;
+      if constexpr (ks + 1 < KS) nb = *(const kh_f8*)(bp + 32 * (ks + 1));
+      if (mf && scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[0][ks], b, acc0, 0, 0, 0);
+      if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[1][ks], b, acc1, 0, 0, 0);
+      b = nb;
       if constexpr (KS == 8) {
         step(std::integral_constant<int, ks>{});
       } else {
@@ -2423,204 +2392,163 @@ __global__ __launch_bounds__(KFS_WAVES * 64, 1) void k_kmeans_fs2(
       }
       __builtin_amdgcn_sched_barrier(0);
     };
-    ks_unroll(mf, std::make_integer_sequence<int, KS>{});
-    if (scr) {
-      a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ccp, ones, a0, 0, 0, 0);
-      a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ccp, ones, a1, 0, 0, 0);
-    }
-    return R;
-  };
-
-  // the read-add-writes of unit it - 1 (raw columns in r), in rounds; each
-  // round exec-masked to its rows (LDS time goes by the active lanes).
-  // Round 0's reads are issued before the decision of unit it (add_begin),
-  // whose DPP chain then covers their latency.
-  kb_f4 v0[CPW / 4];
-  unsigned int c0 = 0;
-  auto add_begin = [&](const Rounds& R) __attribute__((always_inline)) {
-    if (R.w0) {
-      float* const srow = sums + R.d * D;
-      const int sw = R.d & (D - 4);  // XOR by a multiple of 4: the lane's 4-column groups stay whole
-#pragma unroll
-      for (int q = 0; q < CPW / 4; ++q) v0[q] = *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw));
-      if (w == 0) c0 = cnts[R.d];
-    }
-  };
-  auto add_end = [&](const Rounds& R, const kb_f4 (&r)[CPW / 4]) __attribute__((always_inline)) {
-    float* const srow = sums + R.d * D;
-    const int sw = R.d & (D - 4);
-    if (R.w0) {
-#pragma unroll
-      for (int q = 0; q < CPW / 4; ++q) *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw)) = v0[q] + r[q];
-      if (w == 0) cnts[R.d] = c0 + 1u;
-    }
+    ks_unroll(mk, std::make_integer_sequence<int, KS>{});
+    if (mf && scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ccp[0], ones, acc0, 0, 0, 0);
+    if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ccp[1], ones, acc1, 0, 0, 0);
+    step(std::integral_constant<int, 8>{});
+    step(std::integral_constant<int, 9>{});
+    // the read-add-writes of unit t - 2 (raw columns in r), round by round
+    // (a wave's LDS operations run in issue order: round k + 1 reads what
+    // round k wrote)
+    float* const srow = sums + (d >= 0 ? d : 0) * D;
+    const int sw = (d >= 0 ? d : 0) & (D - 4);  // XOR by a multiple of 4: the lane's 4-column groups stay whole
     auto rmw = [&]() __attribute__((always_inline)) {
-      kb_f4 v[CPW / 4];
+      kb_f4 v[NQ];
 #pragma unroll
-      for (int q = 0; q < CPW / 4; ++q) v[q] = *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw));
-      const unsigned int cv = w == 0 ? cnts[R.d] : 0u;
+      for (int q = 0; q < NQ; ++q) v[q] = *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw));
+      const unsigned int cv = s == 0 && h == 0 ? cnts[d] : 0u;
 #pragma unroll
-      for (int q = 0; q < CPW / 4; ++q) *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw)) = v[q] + r[q];
-      if (w == 0) cnts[R.d] = cv + 1u;
+      for (int q = 0; q < NQ; ++q) *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw)) = v[q] + r[q];
+      if (s == 0 && h == 0) cnts[d] = cv + 1u;
     };
-    if (R.w1) rmw();
-    if (R.w2) rmw();
-    // The rest (a centre's fourth and later rows: rare once the centres have
-    // moved, a few per unit in a first iteration from data-point centres,
-    // whose labels are skewed): each row's rank among its centre's remaining
-    // rows, from ballots over the distinct labels (scalar loop, no LDS), then
-    // one read-add-write round per rank.  A wave's LDS operations run in
-    // issue order, so round k + 1 reads what round k wrote.
-    const unsigned long long mm = __ballot(R.more);
+    if (w0) rmw();
+    if (w1) rmw();
+    if (w2) rmw();
+    // a centre's fourth and later rows of the unit (rare on settled centres,
+    // a few per unit from data-point centres): each row's rank among its
+    // centre's remaining rows from ballots over the distinct labels (scalar
+    // loop: every step removes at least the label it reads, so it ends after
+    // at most 32 steps; a device trap makes that bound an invariant), then one
+    // read-add-write round per rank
+    const unsigned long long mm = __ballot(more) & 0xffffffffull;  // rows (lanes j; lane j + 32 is the same row)
     if (mm) {
-      int rk = 0, kmax = 0;
+      int rk = 0, kmax = 0, guard = 0;
       unsigned long long left = mm;
       while (left) {
-        const int L = __builtin_amdgcn_readlane(R.d, __builtin_ctzll(left));
-        const bool in = R.more && R.d == L;
-        const unsigned long long g = __ballot(in);
-        left &= ~g;
-        if (in) rk = __builtin_amdgcn_mbcnt_hi((unsigned)(g >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)g, 0u));
-        const int gk = __popcll(g) - 1;
+        if (++guard > 32) {  // unreachable: a trap (inline, so the loop's control flow stays as it is)
+          asm volatile("s_trap 2");
+          break;
+        }
+        const int L = __builtin_amdgcn_readlane(d, __builtin_ctzll(left));
+        const bool in = more && d == L;
+        const unsigned long long gl = __ballot(in) & 0xffffffffull;
+        left &= ~gl;
+        if (in) rk = __popcll(gl & ((1ull << j) - 1ull));
+        const int gk = __popcll(gl) - 1;
         kmax = gk > kmax ? gk : kmax;
       }
       for (int k = 0; k <= kmax; ++k)
-        if (R.more && rk == k) rmw();
+        if (more && rk == k) rmw();
     }
+    // labels (-1 for an undecided row: the list passes write it) and the
+    // unit's undecided-row mask; every store issued
+    i64* la = h == 0 && rlive ? labels + grow : (i64*)dummy;
+    *la = (i64)d;
+    const unsigned long long m = __ballot(d < 0 && rlive) & 0xffffffffull;
+    unsigned long long* ma = lane == 0 && dv ? und_mask + un2 : dummy + 1;
+    *ma = m;
+    load(r, tt + KP_AHEAD);
   };
 
-  // labels and undecided bits of unit it - 1 (d: its label array entry of this lane's row)
-  auto out_labels = [&](int d, int dlr, int it) __attribute__((always_inline)) {
-    const int up = it - 1;
-    const i64 unp = bk + (i64)up * G;
-    const bool ulive = up >= 0 && up < nit;
-    const int lr = 8 * w + (lane >> 3);
-    const i64 glr = unp * U + lr;
-    i64* la = ulive && glr < N ? labels + glr : (i64*)dummy;
-    *la = (i64)dlr;  // -1 for an undecided row: the list passes write it
-    const unsigned long long m = __ballot(d < 0 && ulive && unp * U + lane < N);
-    const i64 tile = 2 * unp + (lane & 1);
-    unsigned long long* ma = ulive && tile < ntiles ? und_mask + tile : dummy;
-    *ma = (lane & 1) ? (m >> 32) : (m & 0xffffffffull);
-  };
-
-  // window win of the block's fp32 sums into its own partial slot (plain
-  // 16-byte stores, every slot written once: no atomics, no ordering), then
-  // cleared (all waves, between barriers); the slots are summed in a fixed
-  // order in fp64 after the kernel
-  auto flush = [&](int win) __attribute__((always_inline)) {
-    float* pb = part + ((i64)bk * nwin + win) * K * D;
-    for (int i = 4 * t; i < K * D; i += 4 * W * 64) {
-      const int d = i / D, c = i % D;
-      kb_f4* src = (kb_f4*)(sums + d * D + (c ^ (d & (D - 4))));
-      *(kb_f4*)(pb + i) = *src;
-      *src = (kb_f4){0.f, 0.f, 0.f, 0.f};
-    }
-  };
-
-#if KF2_PROF
-  unsigned long long pacc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, plast = __builtin_amdgcn_s_memtime();
-#define KF2_T(k)                                                   \
-  {                                                                \
-    const unsigned long long now = __builtin_amdgcn_s_memtime();  \
-    pacc[k] += now - plast;                                        \
-    plast = now;                                                   \
-  }
-#else
-#define KF2_T(k)
-#endif
-  const int nrun = nit > 0 ? (nit + NS) / NS * NS : 0;  // >= nit + 1: unit nit - 1 is added at iteration nit
-  __syncthreads();  // sums, dl
-  if (nit > 0) {
-    // the loads in the order the loop keeps them in flight (two stores after
-    // each unit, as an iteration issues them), so the compiler's count of the
-    // loads outstanding at the loop head is the same on entry and on the back edge
-#pragma unroll
-    for (int r = 0; r < NS - 1; ++r) {
-      load(ring[r], r);
-      dummy[lane & 1] = 0ull;
-      dummy[lane & 1] = 0ull;
-    }
-    stage(ring[0], 0);
-  }
-  for (int it0 = 0; it0 < nrun; it0 += NS) {
-    ks_unroll([&](auto sc) __attribute__((always_inline)) {
-      constexpr int s = decltype(sc)::value;
-      constexpr int sp = (s + NS - 1) % NS, sn = (s + 1) % NS;  // slots of units it - 1 and it + 1
-      const int it = it0 + s;
-      KF2_T(0);
-      __syncthreads();
-      KF2_T(1);
-      if constexpr (s == 0)
-        if (it >= KF2_FW && it % KF2_FW == 0) {
-          flush(it / KF2_FW - 1);
-          __syncthreads();
-          __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  // one slot of the unrolled body (compile-time copy c of KP_UNR, group GR)
+  auto slot = [&](auto gc, auto cc, int tt) __attribute__((always_inline)) {
+    constexpr int GR = decltype(gc)::value, c = decltype(cc)::value;
+    __syncthreads();
+    if constexpr (c == 0)
+      if (tt > 0 && tt % KP_FW == 0) {
+        // window tt / KP_FW - 1 of the block's fp32 sums into its partial
+        // slot (plain 16-byte stores), then cleared; summed in fp64 later
+        float* pb = part + ((i64)bk * nwin + tt / KP_FW - 1) * K * D;
+        for (int i = 4 * t; i < K * D; i += 4 * KP_WAVES * 64) {
+          const int dd = i / D, cl = i % D;
+          kb_f4* src = (kb_f4*)(sums + dd * D + (cl ^ (dd & (D - 4))));
+          *(kb_f4*)(pb + i) = *src;
+          *src = (kb_f4){0.f, 0.f, 0.f, 0.f};
         }
-      // (add_out outside the screen's branch: its stores on one path only,
-      // so the compiler keeps an exact count of the loads in flight)
-      kb_acc a0, a1;
-      const Rounds R = screen_tbl(a0, a1, (s + 1) % 2);
-      KF2_T(2);
-      out_labels(R.d, R.dlr, it);
-      KF2_T(3);
-      if (w < NCT) screen_fold(a0, a1);
-      KF2_T(4);
-      __syncthreads();
-      KF2_T(5);
-      decide(it, s % 2, [&]() __attribute__((always_inline)) { add_begin(R); });
-      KF2_T(6);
-      add_end(R, ring[sp]);
-      KF2_T(7);
-      stage(ring[sn], (s + 1) % 2);
-      KF2_T(8);
-      load(ring[sp], it + NS - 1);  // unit it + 3 into the slot unit it - 1 left
-    }, std::make_integer_sequence<int, NS>{});
-  }
-#if KF2_PROF
-  if (lane == 0)
-    for (int k = 0; k < 9; ++k) g_kf2_prof[(blockIdx.x * W + w) * 9 + k] = pacc[k];
-#endif
+        __syncthreads();
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      }
+    if constexpr ((c & 1) == GR) {
+      matrix_role(tt, ring[((c + KP_UNR - 2) >> 1) % NR]);
+    } else {
+      const int uf = tt - 1, us = tt + 1;
+      if (uf >= 0 && uf < nit) fold(uf);
+      if (us < nit) stage(ring[((c + 1) >> 1) % NR], us);
+    }
+  };
+
+  auto body = [&](auto gc) __attribute__((always_inline)) {
+    constexpr int GR = decltype(gc)::value;
+    if (nit > 0) {
+      // the loads in the order the loop keeps them in flight (two stores
+      // before each unit's loads, as a matrix slot issues them), so the
+      // compiler's count of outstanding operations is the same at the loop
+      // head on entry and on the back edge
+#pragma unroll
+      for (int k = 0; k < NR - 1; ++k) {
+        __builtin_nontemporal_store(0ull, dummy + (lane & 1) + 4 * k);
+        __builtin_nontemporal_store(0ull, dummy + 2 + (lane & 1) + 4 * k);
+        load(ring[k], GR + 2 * k);
+      }
+      if constexpr (GR == 0) stage(ring[0], 0);
+    }
+    for (int t0 = 0; t0 < nrun; t0 += KP_UNR) {
+      ks_unroll([&](auto cc) __attribute__((always_inline)) {
+        slot(gc, cc, t0 + decltype(cc)::value);
+      }, std::make_integer_sequence<int, KP_UNR>{});
+    }
+  };
+  // the set-up loads (centres, mu, bound inputs) complete here, so the loop's
+  // waits count only the ring's loads and the slots' stores
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  if (grp == 0)
+    body(std::integral_constant<int, 0>{});
+  else
+    body(std::integral_constant<int, 1>{});
+
   __syncthreads();
   {
-    // the last window (nrun - 1 >= nit: at least one loop iteration ran if
-    // nit > 0), then zero slots for windows this block does not have
-    const int wdone = nrun > 0 ? (nrun - 1) / KF2_FW : 0;
-    flush(wdone);
+    // the last window, then zero slots for windows this block does not have
+    const int wdone = nrun > 0 ? (nrun - 1) / KP_FW : 0;
+    float* pb = part + ((i64)bk * nwin + wdone) * K * D;
+    for (int i = 4 * t; i < K * D; i += 4 * KP_WAVES * 64) {
+      const int dd = i / D, cl = i % D;
+      *(kb_f4*)(pb + i) = *(kb_f4*)(sums + dd * D + (cl ^ (dd & (D - 4))));
+    }
     for (int win = wdone + 1; win < nwin; ++win)
-      for (int i = 4 * t; i < K * D; i += 4 * W * 64)
+      for (int i = 4 * t; i < K * D; i += 4 * KP_WAVES * 64)
         *(kb_f4*)(part + ((i64)bk * nwin + win) * K * D + i) = (kb_f4){0.f, 0.f, 0.f, 0.f};
   }
   if (t < K) pcnt[(i64)bk * K + t] = cnts[t];
 }
 
 template <int KS, int NCT>
-static void kf2_launch(hipStream_t s, int grid, i64 N, i64 K, const float* P, i64 ldp, const __bf16* CBh,
-                       const __bf16* CBl, const float* cnf2, const double* cmax, const float* muf, i64* labels,
-                       unsigned long long* und_mask, float* part, int nwin, unsigned long long* pcnt,
-                       unsigned long long* dummy) {
+static void kp_launch(hipStream_t s, int grid, i64 N, i64 K, const float* P, i64 ldp, const __bf16* CBh,
+                      const __bf16* CBl, const float* cnf2, const double* cmax, const float* muf, i64* labels,
+                      unsigned long long* und_mask, float* part, int nwin, unsigned long long* pcnt,
+                      unsigned long long* dummy) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_kmeans_fs2<KS, NCT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kf2_lds_bytes(16 * KS));
+    (void)hipFuncSetAttribute((const void*)k_kmeans_pp<KS, NCT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kp_lds_bytes(16 * KS));
     attr = true;
   }
-  k_kmeans_fs2<KS, NCT><<<grid, KFS_WAVES * 64, kf2_lds_bytes(16 * KS), s>>>(
+  k_kmeans_pp<KS, NCT><<<grid, KP_WAVES * 64, kp_lds_bytes(16 * KS), s>>>(
       N, K, P, ldp, CBh, CBl, cnf2, cmax, muf, labels, und_mask, part, nwin, pcnt, dummy);
 }
 
-static void kf2_launch_n(int nct, int KS, hipStream_t s, int grid, i64 N, i64 K, const float* P, i64 ldp,
-                         const __bf16* CBh, const __bf16* CBl, const float* cnf2, const double* cmax, const float* muf,
-                         i64* labels, unsigned long long* und_mask, float* part, int nwin, unsigned long long* pcnt,
-                         unsigned long long* dummy) {
-#define KF2_CASE(KSV, NC)                                                                                         \
-  if (KS == KSV && nct == NC) {                                                                                   \
-    kf2_launch<KSV, NC>(s, grid, N, K, P, ldp, CBh, CBl, cnf2, cmax, muf, labels, und_mask, part, nwin, pcnt, dummy); \
-    return;                                                                                                       \
+static void kp_launch_n(int nct, int KS, hipStream_t s, int grid, i64 N, i64 K, const float* P, i64 ldp,
+                        const __bf16* CBh, const __bf16* CBl, const float* cnf2, const double* cmax, const float* muf,
+                        i64* labels, unsigned long long* und_mask, float* part, int nwin, unsigned long long* pcnt,
+                        unsigned long long* dummy) {
+#define KP_CASE(KSV, NC)                                                                                         \
+  if (KS == KSV && nct == NC) {                                                                                  \
+    kp_launch<KSV, NC>(s, grid, N, K, P, ldp, CBh, CBl, cnf2, cmax, muf, labels, und_mask, part, nwin, pcnt, dummy); \
+    return;                                                                                                      \
   }
-  KF2_CASE(8, 8) KF2_CASE(8, 4) KF2_CASE(8, 2) KF2_CASE(8, 1)
-  KF2_CASE(4, 8) KF2_CASE(4, 4) KF2_CASE(4, 2) KF2_CASE(4, 1)
-#undef KF2_CASE
+  KP_CASE(8, 8) KP_CASE(8, 4) KP_CASE(8, 2) KP_CASE(8, 1)
+  KP_CASE(4, 8) KP_CASE(4, 4) KP_CASE(4, 2) KP_CASE(4, 1)
+#undef KP_CASE
 }
 
 // Deterministic compaction of lane masks (LAYOUT 2: bit j <-> row 32 tile + j)
@@ -3084,7 +3012,7 @@ __global__ __launch_bounds__(256) void k_kmeans_reduce(i64 n, i64 G, const P* __
   }
 }
 
-// Many fp32 partial slots (k_kmeans_fs2's windows: G x nwin = 6144 at cfg3,
+// Many fp32 partial slots (k_kmeans_pp's windows: G x nwin = 6144 at cfg3,
 // 805 MB) -> KR_S fp64 slice sums: slice s adds slots s, s + KR_S, ... in
 // order, 4 consecutive elements per thread (16-byte loads, a wave reads 1 KiB
 // of one slot), so ~1 K blocks keep the stream busy where one thread per
@@ -3378,29 +3306,29 @@ extern "C" int spx_kmeans_accumulate(int dtype, int64_t N, int64_t D, int64_t K,
 // spx_kmeans_step = spx_kmeans_assign + spx_kmeans_accumulate with the same
 // results (labels bit for bit; counts exact; sums deterministic, within the
 // fp32-chain bound below of the fp64 sums) and, in the certified screen's
-// domain, ONE pass over the points for the decided rows: k_kmeans_fs2
+// domain, ONE pass over the points for the decided rows: k_kmeans_pp
 // labels and accumulates them; the rows it leaves undecided (a few %) are
 // listed in row order, resolved by km_resolve and accumulated by
 // k_kmeans_accum over that list.  Partials are combined in a fixed order.
 // Workspace: spx_kmeans_assign's | spx_kmeans_accumulate's | fused partial
 // sums (G x K x D f64) | fused partial counts (G x K u64) | compaction block
 // counts.
-static i64 kfs_grid(i64 N) {  // one block per CU, at most one per 64-row unit
-  const i64 nunits = (N + 63) / 64, ncu = num_cus();
+static i64 kfs_grid(i64 N) {  // one block per CU, at most one per 32-row unit
+  const i64 nunits = (N + KP_U - 1) / KP_U, ncu = num_cus();
   return nunits < ncu ? (nunits < 1 ? 1 : nunits) : ncu;
 }
 
 static i64 kfs_nblk(i64 N) { return ((N + 31) / 32 + 256 * 16 - 1) / (256 * 16); }
 
-// windows of k_kmeans_fs2's fp32 partials per block (the block with the most units)
-static i64 kf2_nwin(i64 N) {
-  const i64 nunits = (N + 63) / 64, G = kfs_grid(N);
-  const i64 nit = (nunits + G - 1) / G, nrun = (nit + KF2_NS) / KF2_NS * KF2_NS;
-  return (nrun - 1) / KF2_FW + 1;
+// windows of k_kmeans_pp's fp32 partials per block (the block with the most units)
+static i64 kp_nwin(i64 N) {
+  const i64 nunits = (N + KP_U - 1) / KP_U, G = kfs_grid(N);
+  const i64 nit = (nunits + G - 1) / G, nrun = (nit + 2 + KP_UNR - 1) / KP_UNR * KP_UNR;
+  return (nrun - 1) / KP_FW + 1;
 }
 
-// bytes of the fused step's block partials (k_kmeans_fs2's fp32 windows)
-static i64 kfs_part_bytes(i64 N, i64 D, i64 K) { return kfs_grid(N) * kf2_nwin(N) * K * D * 4; }
+// bytes of the fused step's block partials (k_kmeans_pp's fp32 windows)
+static i64 kfs_part_bytes(i64 N, i64 D, i64 K) { return kfs_grid(N) * kp_nwin(N) * K * D * 4; }
 
 extern "C" int64_t spx_kmeans_step_workspace(int dtype, int64_t N, int64_t D, int64_t K) {
   const int64_t a = spx_kmeans_assign_workspace(dtype, N, D, K);
@@ -3450,8 +3378,8 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
   k_kmeans_prep_b3<<<1, 1024, 0, S(stream)>>>(D, K, 32 * nct, centers, CBh, CBl, cnf, w.cmax, mcoef, cnf2, w.muf);
   LAUNCH_CHECK("spx_kmeans_step(prep)");
   unsigned long long* dummy = (unsigned long long*)(((uintptr_t)(bcnt + nb + 1) + 63) & ~(uintptr_t)63);
-  const i64 nwin = kf2_nwin(N);
-  kf2_launch_n(nct, (int)(D / 16), S(stream), (int)G, N, K, Pf, ldp, CBh, CBl, cnf2, w.cmax, w.muf, labels,
+  const i64 nwin = kp_nwin(N);
+  kp_launch_n(nct, (int)(D / 16), S(stream), (int)G, N, K, Pf, ldp, CBh, CBl, cnf2, w.cmax, w.muf, labels,
                w.und_mask, partF, (int)nwin, pcntF, dummy);
   LAUNCH_CHECK("spx_kmeans_step(fused screen + accumulate)");
   // the screen's undecided rows, in row order (the gathered accumulation's order)
@@ -3463,7 +3391,7 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
   int rc = km_resolve(S(stream), N, D, K, Pf, ldp, centers, labels, w, nct, r32);
   if (rc) return rc;
   // the undecided rows' sums and counts, gathered through the row list
-  // (an LDS-sum form of this pass, k_kmeans_fs2's adds over gathered 64-row
+  // (an LDS-sum form of this pass, the fused kernel's adds over gathered 64-row
   // units, measured 1.18-2.27 ms against this kernel's 1.1 ms: not kept)
   i64 G2, ndb, ncb;
   ka_grid(dtype, N, D, K, &G2, &ndb, &ncb);

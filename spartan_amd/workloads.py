@@ -73,7 +73,8 @@ def kmeans_fit(X, n_clusters, n_iter, centers=None, seed=0, info=None):
   or None (first K rows of X).  Returns (centers (K, D) fp64 host array,
   labels DistArray (N,) int64 tiled like X's rows).  ``info`` (a dict, optional)
   receives 'assign_centers': the (K, D) centres the returned labels were
-  assigned against (bench.py's post-timing check)."""
+  assigned against, and 'sums' / 'counts': that iteration's all-reduced
+  per-centre sums and counts (bench.py's post-timing checks)."""
   import torch
   from . import backend, comm, runtime
   from .array import distarray, extent as ext
@@ -113,6 +114,8 @@ def kmeans_fit(X, n_clusters, n_iter, centers=None, seed=0, info=None):
     host = buf.cpu().numpy()
     c_host = host[K * D:].view(np.int64)
     s_host = host[:K * D].reshape(K, D)
+    if info is not None:
+      info['sums'], info['counts'] = s_host.copy(), c_host.copy()
     empty = c_host == 0
     if np.any(empty):
       c_host = c_host.copy()

@@ -1341,9 +1341,9 @@ def test_kmeans_step_matches_two_passes(ex, kind, ddt):
 
 
 def test_kmeans_step_windows(ex):
-  """Enough rows that every block passes several 256-unit windows (the fp32
+  """Enough rows that every block passes several 504-unit windows (the fp32
   sums written to the block's window slots and cleared inside the unit
-  loop): 12M x 64 = 732 units per block on 256 CUs."""
+  loop): 12M x 64 = 1465 32-row units per block on 256 CUs."""
   import torch
   from spartan_amd import backend
   be = backend.get()
@@ -1358,12 +1358,23 @@ def test_kmeans_step_windows(ex):
   exact = torch.empty_like(lab)
   be.kmeans_assign(P, Cd, exact, exact_only=True)
   assert torch.equal(lab, exact)
-  ws = torch.zeros((K, D), dtype=torch.float64, device='cuda')
-  ws.index_add_(0, lab, P.to(torch.float64))
   assert torch.equal(cnt, torch.bincount(lab, minlength=K))
-  torch.testing.assert_close(sums, ws, rtol=1e-5, atol=0)  # the fp32 rule (points >= 0: sum |x| = sum x)
-  # the window slots were used: a block's units span several flushes
-  assert (N + 63) // 64 // 256 > 2 * 256
+  torch.testing.assert_close(sums, _centre_sums64(lab, P, K), rtol=1e-5, atol=0)  # the fp32 rule (points >= 0)
+  # the window slots were used: a block's 32-row units span several flushes
+  assert (N + 31) // 32 // 256 > 2 * 504
+
+
+def _centre_sums64(lab, X, K, chunk=1 << 20):
+  """Checker: per-centre fp64 sums of the rows of X by label, as a one-hot
+  fp64 GEMM per chunk of rows (torch, test-only).  index_add_ would be the
+  obvious form, but its fp64 atomics serialise when most rows share a label
+  (the skewed cases below: minutes for 12M rows)."""
+  import torch
+  out = torch.zeros((K, X.shape[1]), dtype=torch.float64, device=X.device)
+  for r0 in range(0, X.shape[0], chunk):
+    oh = torch.nn.functional.one_hot(lab[r0:r0 + chunk], K).to(torch.float64)
+    out += oh.t() @ X[r0:r0 + chunk].to(torch.float64)
+  return out
 
 
 def _step_check_all(be, P, Cd, rtol=1e-5):
@@ -1381,9 +1392,7 @@ def _step_check_all(be, P, Cd, rtol=1e-5):
   be.kmeans_assign(P, Cd, exact, exact_only=True)
   assert torch.equal(lab, exact)
   assert torch.equal(cnt, torch.bincount(lab, minlength=K))
-  ws = torch.zeros((K, D), dtype=torch.float64, device='cuda')
-  ws.index_add_(0, lab, P.to(torch.float64))
-  torch.testing.assert_close(sums, ws, rtol=rtol, atol=0)
+  torch.testing.assert_close(sums, _centre_sums64(lab, P, K), rtol=rtol, atol=0)
   return lab, cnt
 
 

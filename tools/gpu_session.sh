@@ -37,6 +37,12 @@ for s in $STEPS; do
         -p no:cacheprovider -k "sgd or lreg or golden or dot_reduce" > $O/lregtests.log 2>&1 ;;
     lregbench)
       cd $R && step lregbench 600 python3 bench.py --dot 0 --workloads lreg --cpu-baseline 0 > $O/lregbench.json 2> $O/lregbench.err ;;
+    kmquick)
+      # small fused-step cases first (ragged units, same-label units, all K / D shapes)
+      cd $R && step kmquick 240 python -u -m pytest tests/test_gpu_parity.py -v --timeout 60 --timeout-method thread \
+        -p no:cacheprovider -k "kmeans_step_same_row or kmeans_step_matches" > $O/kmquick.log 2>&1 ;;
+    kmdiag)
+      cd $R && step kmdiag 150 python3 -u tools/km_diag.py 1200000 > $O/kmdiag.log 2>&1 ;;
     kmtests)
       cd $R && step kmtests 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
         -p no:cacheprovider -k "kmeans" > $O/kmtests.log 2>&1 ;;
