@@ -492,8 +492,11 @@ class HipBackend:
       # exactly two resident blocks per CU (cfg2 axis 0: 512 blocks 1.80 ms,
       # 1024 1.87, 2048 1.87, 4096 1.90); one narrow column tile (cfg5's 64
       # columns) with eight (2048: 4.06 ms per lreg iteration, 512: 4.15)
-      # -- profiles/r02_cfg2_grid.txt
-      tb = (2 if CT > 1 else 8) * _num_cus()
+      # -- profiles/r02_cfg2_grid.txt; a fused row dot (cfg5's gradient, one
+      # 64-column tile) with sixteen and rows unrolled 8 deep (3.866 ms per
+      # lreg iteration against 3.959 at eight and 4; profiles/r04_lreg_sweep.txt)
+      rowdot = bool(codegen.rowdots(root))
+      tb = (2 if CT > 1 else 16 if rowdot else 8) * _num_cus()
       if base < tb:
         P = max(1, min(-(-tb // base), -(-R // (rows_per_step * 4))))
       chunk = -(-R // P)
@@ -527,6 +530,8 @@ class HipBackend:
     U, rowinv = None, ()
     if kind == 'cols':
       U = codegen.cols_unroll(ins, classes, V, [vstr[k][1] for k in range(len(slots))])
+      if codegen.rowdots(root) and U == 4:
+        U = 8
       rowinv = tuple(s for k, s in enumerate(slots) if vstr[k][1] == 0)
     sig = ('reduce', root.sig(), tuple(ins), tuple(classes), kind, op, V, U, rowinv)
     fn = self._sig_fns.get(sig)

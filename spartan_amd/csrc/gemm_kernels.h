@@ -84,7 +84,14 @@ __device__ __forceinline__ void tile_of(int bid, int ntiles, int tiles_n, int GM
 // the relative error's spread drops from ~4e-6 to ~6e-7, well inside the fp32
 // tolerance of 1e-5 at every element, where one long chain exceeded it in a
 // few elements per row).
-template <typename T, int BM, int BN, int BK, int WM, int WN, int GM, bool ALIGNED, int SEG = 0>
+//
+// GFL > 0: the same bound without the register cost -- every GFL K-tiles the
+// wave adds its accumulators into C in global memory (the first flush
+// applies beta) and restarts them from zero, so an element is a chain of
+// GFL * BK / 2 MFMA steps plus K / (GFL * BK) fp32 additions in memory; the
+// kernel keeps one accumulator set (and the occupancy of the one-chain
+// form), at the cost of K / (GFL BK) read-modify-writes of C.
+template <typename T, int BM, int BN, int BK, int WM, int WN, int GM, bool ALIGNED, int SEG = 0, int GFL = 0>
 __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T* __restrict__ A, i64 lda,
                                                      const T* __restrict__ B, i64 ldb, T* __restrict__ C,
                                                      i64 ldc, T alpha, T beta, int tiles_n, int ntiles) {
@@ -177,6 +184,43 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
       *(V*)(&Bs[buf][kr][cq * VE]) = rb[i];
     }
   };
+  // acc (times alpha) into C.  With GFL > 0 the kernel runs with beta 0 or 1
+  // (spx_gemm scales C first for other betas): the first write of an element
+  // is a plain store when beta is 0, every other one a no-return fp32 atomic
+  // add -- C is never read back into registers (64 loads in flight would
+  // double the kernel's registers), and one wave owns each element, so its
+  // adds land in program order: deterministic.  Without GFL: the one
+  // epilogue, alpha * acc + beta * C.
+  const bool use_beta = beta != (T)0;
+  auto flush_c = [&](bool again) {
+    int fl = lane;
+    asm volatile("" : "+v"(fl));  // C's addresses are loop-invariant: do not hoist them out of the K loop
+    // this lane's element (i, j, r) sits at cb + (i TILE + crow(0, r)) ldc + j TILE
+    T* const cb = C + (row0 + wm * WTM + F::crow(fl, 0)) * ldc + col0 + wn * WTN + F::ccol(fl);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < F::NREG; ++r) {
+          const i64 gr = row0 + wm * WTM + i * F::TILE + F::crow(fl, r);
+          const i64 gc = col0 + wn * WTN + j * F::TILE + F::ccol(fl);
+          if (ALIGNED || (gr < M && gc < N)) {
+            T v = alpha * acc[i][j][r];
+            if constexpr (GFL > 0) {
+              T* const pc = cb + (i64)(i * F::TILE + F::crow(0, r) - F::crow(0, 0)) * ldc + j * F::TILE;
+              if (again || use_beta)
+                unsafeAtomicAdd(pc, v);
+              else
+                *pc = v;
+            } else {
+              if (use_beta) v += beta * C[gr * ldc + gc];
+              C[gr * ldc + gc] = v;
+            }
+          }
+        }
+  };
+  bool flushed = false;
   const int nk = (int)((K + BK - 1) / BK);
   load(0);
   store(0);
@@ -223,6 +267,16 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
           for (int j = 0; j < TN; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
       }
     }
+    if constexpr (GFL > 0) {
+      if ((kt + 1) % GFL == 0 && kt + 1 < nk) {  // block-uniform: flush into C
+        flush_c(flushed);
+        flushed = true;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = F::zero();
+      }
+    }
     if constexpr (SEG > 0) {
       if ((kt + 1) % SEG == 0) {  // block-uniform
 #pragma unroll
@@ -243,24 +297,10 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] += run[i][j];
   }
-  const bool use_beta = beta != (T)0;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < F::NREG; ++r) {
-        const i64 gr = row0 + wm * WTM + i * F::TILE + F::crow(lane, r);
-        const i64 gc = col0 + wn * WTN + j * F::TILE + F::ccol(lane);
-        if (ALIGNED || (gr < M && gc < N)) {
-          T v = alpha * acc[i][j][r];
-          if (use_beta) v += beta * C[gr * ldc + gc];
-          C[gr * ldc + gc] = v;
-        }
-      }
+  flush_c(flushed);
 }
 
-template <typename T, int BM, int BN, int BK, int WM, int WN, int GM, int SEG = 0>
+template <typename T, int BM, int BN, int BK, int WM, int WN, int GM, int SEG = 0, int GFL = 0>
 struct Config {
   static constexpr int bm = BM, bn = BN, bk = BK, threads = 64 * WM * WN;
   static hipError_t launch(i64 M, i64 N, i64 K, const T* A, i64 lda, const T* B, i64 ldb, T* C, i64 ldc,
@@ -268,11 +308,11 @@ struct Config {
     i64 tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
     int nt = (int)(tm * tn);
     if (aligned)
-      gemm<T, BM, BN, BK, WM, WN, GM, true, SEG><<<nt, threads, 0, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta,
-                                                                   (int)tn, nt);
+      gemm<T, BM, BN, BK, WM, WN, GM, true, SEG, GFL><<<nt, threads, 0, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha,
+                                                                        beta, (int)tn, nt);
     else
-      gemm<T, BM, BN, BK, WM, WN, GM, false, SEG><<<nt, threads, 0, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha,
-                                                                    beta, (int)tn, nt);
+      gemm<T, BM, BN, BK, WM, WN, GM, false, SEG, GFL><<<nt, threads, 0, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha,
+                                                                         beta, (int)tn, nt);
     return hipGetLastError();
   }
   static bool is_aligned(i64 M, i64 N, i64 K, const void* A, i64 lda, const void* B, i64 ldb) {

@@ -7,6 +7,7 @@
 // entry point in include/spx.h.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdint>
@@ -616,8 +617,20 @@ extern "C" int spx_argreduce_combine(int op, int dtype, const void* vals, const 
 // fp32: 256x128x16, 8 waves (with the k-contiguous A staging: 141.4 TF = 89.9 %
 // of 157.3 at 32768^3 against 135.6 TF for the 256x256x16 16-wave tile,
 // profiles/r02_gemm_tune_ak.txt)
-typedef spx_mfma::Config<float, 256, 128, 16, 4, 2, 8, 16> GemmF32Big;
-typedef spx_mfma::Config<float, 128, 128, 16, 2, 2, 8, 16> GemmF32Small;
+// fp32: one accumulator set, flushed into C every 256 K-tiles (gemm_kernels.h
+// GFL): chains of 2048 MFMA steps instead of K / 2, at the one-chain form's
+// registers and occupancy (round 3's register two-level form, SEG, cost 6 %)
+constexpr int SPX_GEMM_GFL = 256;
+typedef spx_mfma::Config<float, 256, 128, 16, 4, 2, 8, 0, SPX_GEMM_GFL> GemmF32Big;
+typedef spx_mfma::Config<float, 128, 128, 16, 2, 2, 8, 0, SPX_GEMM_GFL> GemmF32Small;
+
+// C *= beta (the GFL kernels take beta 0 or 1)
+__global__ __launch_bounds__(256) void k_scale_rows(i64 M, i64 N, float* C, i64 ldc, float beta) {
+  for (i64 i = (i64)blockIdx.x * 256 + threadIdx.x; i < M * N; i += (i64)gridDim.x * 256) {
+    const i64 r = i / N, c = i % N;
+    C[r * ldc + c] *= beta;
+  }
+}
 typedef spx_mfma::Config<double, 128, 128, 16, 4, 4, 0> GemmF64;
 
 // integer GEMM (exact, wrap-around like NumPy's int matmul): 16x16 output
@@ -674,6 +687,12 @@ extern "C" int spx_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* 
   hipError_t e;
   if (dtype == SPX_F32) {
     const float *a = (const float*)A, *b = (const float*)B;
+    if (beta != 0.0 && beta != 1.0) {
+      k_scale_rows<<<(unsigned)std::min<i64>((M * N + 255) / 256, 4096), 256, 0, S(stream)>>>(M, N, (float*)C, ldc,
+                                                                                           (float)beta);
+      LAUNCH_CHECK("spx_gemm(scale C)");
+      beta = 1.0;
+    }
     i64 big_tiles = ((M + 255) / 256) * ((N + 255) / 256);
     if (big_tiles >= 512) {
       if (big_tiles > 0x7fffffffLL) return set_err(SPX_EINVAL, "spx_gemm: too many tiles");
@@ -2091,18 +2110,23 @@ static void ks_launch_n(int nct, hipStream_t s, i64 N, i64 D, const float* P, i6
 //     tiles 2s, 2s + 1 (64 centres) as the fp16 MFMA A operand plus their
 //     -cc/2 pieces; two chains of 8 v_mfma_f32_32x32x16_f16 + 1 bf16 MFMA
 //     (-cc/2) over unit t's fp16 x' (LDS) give S - cc/2 = -a''/2 for 64
-//     centres x 32 rows.  Woven between those MFMAs: the decision of unit
-//     t - 2 (this group's previous unit; its candidates were folded in slot
-//     t - 1), the table rounds of its adds; after them the read-add-writes
-//     of unit t - 2's decided rows into the LDS sums, its labels and
-//     undecided bits, and the loads of unit t + 4;
-//   vector role (the other group): fold unit t - 1's accumulators (its
-//     matrix role of slot t - 1) to per-row top-2 candidates, and stage unit
-//     t + 1 (x' = fl(x - mu), fp16(x') to LDS, |x'|^2 column partials).
+//     centres x 32 rows.  Woven between those MFMAs: the read-add-writes of
+//     unit t - 4's decided rows (this group's unit whose decision the other
+//     group made in slot t - 2) into the LDS sums; then that unit's labels
+//     and undecided bits, and the loads of unit t + 4;
+//   vector role (the other group): the decision of unit t - 2 (the matrix
+//     group's unit, folded in slot t - 1) with the add rounds of its rows,
+//     written to LDS for its adds in slot t + 2; the fold of unit t - 1's
+//     accumulators (this group's matrix role of slot t - 1) to per-row top-2
+//     candidates; the staging of unit t + 1 (x' = fl(x - mu), fp16(x') to
+//     LDS, |x'|^2 column partials).  The decision's LDS round trips are
+//     hidden behind the fold's vector work, and none of them sits in front
+//     of an MFMA.
 // Every cross-wave hand-off crosses at least one barrier: x' is staged one
 // slot before its MFMAs (xh by unit parity), candidates are folded one slot
 // before their decision (exv by unit parity), |x'|^2 partials three slots
-// before (p2p by unit mod 4); the sums are written by the matrix group only.
+// before (p2p by unit mod 4), decisions two slots before the adds (dres by
+// unit mod 4); the sums are written by the matrix group only.
 // The certified decision is k_kmeans_filter_as MODE 1's (same MFMA chains,
 // bound, kq and finiteness checks; 4-bit register tags per centre tile).
 // Accumulation: the block's per-centre sums live in LDS as fp32 [256][D]
@@ -2110,31 +2134,33 @@ static void ks_launch_n(int nct, hipStream_t s, i64 N, i64 D, const float* P, i6
 // D/4 s + D/8 h .. + D/8 of row j, so a wave adds its rows from the registers
 // the loads landed in and waves never share an address.  Two rows of one
 // centre in one unit would race in a plain read-add-write, so the adds go in
-// rounds decided by a per-wave byte table (a row joins round k when it wins
+// rounds: a row's round is its rank among the unit's rows of its centre --
+// rounds 0-2 from a per-wave byte table (a row joins round k when it wins
 // its centre's slot at the k-th write / read-back, the LDS unit's fixed
-// choice); a centre's fourth and later rows are ranked by ballots over the
-// distinct labels (a loop of at most 32 steps: each removes one label; a
-// device trap guards the bound).  The order of every add is fixed: the sums
-// are deterministic.  Every KP_FW units the fp32 sums go by plain stores to
-// the block's partial slot for that window and are cleared; the slots are
-// summed in fp64 in a fixed order after the kernel.  Global stores are
-// issued unconditionally (ghost rows write a dummy word), so the count of
-// loads in flight that the compiler tracks is the same in every slot.
+// choice), later ones from ballots over the distinct labels (a loop of at
+// most 32 steps: each removes one label; a device trap guards the bound).
+// The order of every add is fixed: the sums are deterministic.  Every KP_FW
+// units the fp32 sums go by plain stores to the block's partial slot for
+// that window and are cleared; the slots are summed in fp64 in a fixed order
+// after the kernel.  Global stores are issued unconditionally (ghost rows
+// write a dummy word), so the count of loads in flight that the compiler
+// tracks is the same in every slot.
 typedef float kfs_f2 __attribute__((ext_vector_type(2)));
 typedef int kfs_i2 __attribute__((ext_vector_type(2)));
 __host__ __device__ constexpr int kfs_rs(int D) { return 2 * D + 16; }  // fp16 row stride: +16 B keeps ds_read_b128 conflict-free
 constexpr int KP_WAVES = 8;
 constexpr int KP_U = 32;     // rows per unit (one 32-row MFMA tile)
-constexpr int KP_NR = 3;     // units per group in the register ring (load -> stage -> MFMA -> add)
+constexpr int KP_NR = 4;     // units per group in the register ring (load -> stage -> MFMA -> decide -> add)
 constexpr int KP_AHEAD = 4;  // unit t + 4 is loaded in slot t (its stage is in slot t + 3)
-constexpr int KP_UNR = 6;    // slots per unrolled loop body: ring entries (unit >> 1) % 3 are compile-time
+constexpr int KP_LAG = 4;    // unit t - 4 is added in slot t
+constexpr int KP_UNR = 8;    // slots per unrolled loop body: ring entries (unit >> 1) % 4 are compile-time
 constexpr int KP_FW = 504;   // units per flush window (16128 rows)
 constexpr int KP_XS = 48;    // exv / p2p row stride (bytes): 12 dwords, spreads a lane group's rows over the banks
-static_assert(KP_FW % KP_UNR == 0 && KP_UNR == 2 * KP_NR && KP_AHEAD == 2 * (KP_NR - 1),
+static_assert(KP_FW % KP_UNR == 0 && KP_UNR == 2 * KP_NR && KP_AHEAD + KP_LAG == 2 * KP_NR,
               "flush points fall on the unrolled body's first slot; the ring cycles once per body");
 static size_t kp_lds_bytes(int D) {
   return (size_t)256 * D * 4 + 256 * 4 + (size_t)2 * KP_U * kfs_rs(D) + (size_t)2 * KP_U * KP_XS +
-         (size_t)4 * KP_U * KP_XS + 4 * 256 + 64;
+         (size_t)4 * KP_U * KP_XS + (size_t)4 * KP_U * 4 + 256 * 4 + (size_t)D * 4 + (size_t)8 * 32 * 8;
 }
 
 template <int KS, int NCT>
@@ -2158,20 +2184,20 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
   unsigned char* xh = (unsigned char*)(cnts + 256);      // [2][U][RS] fp16 x' (by unit parity)
   unsigned char* exv = xh + (size_t)2 * U * RS;          // [2][U][KP_XS]: (b1, b2) of waves 0-3, then their 4 indices
   unsigned char* p2p = exv + (size_t)2 * U * KP_XS;      // [4][U][KP_XS]: 8 |x'|^2 column partials (by unit mod 4)
-  unsigned char* tbl = p2p + (size_t)4 * U * KP_XS;      // [4][256] per-wave winner table of the add rounds
-  unsigned char* ldum = tbl + 4 * 256;                   // [64] per-lane dummy byte of the table rounds
+  int* dres = (int*)(p2p + (size_t)4 * U * KP_XS);       // [4][U]: label (low 16 bits, -1: undecided) | add round << 16
+  unsigned int* rcnt = (unsigned int*)(dres + 4 * U);    // [256] rows per centre so far in the unit (rank counters)
+  float* mus = (float*)(rcnt + 256);                     // [D] mu (the stage reads it: no registers held)
+  unsigned long long* ccl = (unsigned long long*)(mus + D);  // [8 tiles][32] -cc/2 as 3 bf16 pieces + a zero
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, grp = w >> 2, s = w & 3, j = lane & 31, h = lane >> 5;
   const int col0 = CPW * s + CPL * h;
   for (int i = t; i < 256 * D + 256; i += KP_WAVES * 64) sums[i] = 0.f;  // (cnts: the same bits)
-  float mu[CPL];
-#pragma unroll
-  for (int e = 0; e < CPL; ++e) mu[e] = muf[col0 + e];
+  for (int i = t; i < 256; i += KP_WAVES * 64) rcnt[i] = 0u;
+  for (int i = t; i < D; i += KP_WAVES * 64) mus[i] = muf[i];
 
   // A operands: wave s screens centre tiles 2s and 2s + 1 (lane (j, h):
   // centre 32 ct + j, dims 16 ks + 8 h .. + 8 of k-step ks)
   const bool scr0 = 2 * s < NCT, scr1 = 2 * s + 1 < NCT;
   kh_f8 ca[2][KS];
-  kb_bf8 ccp[2];
 #pragma unroll
   for (int tl = 0; tl < 2; ++tl) {
     const int ct = 2 * s + tl;
@@ -2189,7 +2215,13 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     const __bf16 b2 = (__bf16)v1;
     const __bf16 b3 = (__bf16)(v1 - (float)b2);
     const __bf16 z = (__bf16)0.f;
-    ccp[tl] = h == 0 ? (kb_bf8){b1, b2, b3, z, z, z, z, z} : (kb_bf8){z, z, z, z, z, z, z, z};
+    // the MFMA operand of the -cc/2 step: lane (j, 0) holds centre j's three
+    // pieces, lane (j, 1) zeros -- kept in LDS (16 B per centre), read at
+    // the step
+    if (h == 0 && ct < NCT) {
+      typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+      ccl[ct * 32 + j] = __builtin_bit_cast(unsigned long long, (bf4){b1, b2, b3, z});
+    }
   }
   const __bf16 one = (__bf16)1.f;
   const kb_bf8 ones = (kb_bf8){one, one, one, one, one, one, one, one};
@@ -2212,8 +2244,8 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
   const int G = gridDim.x, bk = blockIdx.x;
   const i64 nunits = (N + U - 1) / U;
   const int nit = bk < nunits ? (int)((nunits - 1 - bk) / G + 1) : 0;
-  // slots 0 .. nit + 1 (unit nit - 1 is added in slot nit + 1), whole bodies
-  const int nrun = nit > 0 ? (nit + 2 + KP_UNR - 1) / KP_UNR * KP_UNR : 0;
+  // slots 0 .. nit + KP_LAG - 1 (unit nit - 1 is added in slot nit - 1 + KP_LAG), whole bodies
+  const int nrun = nit > 0 ? (nit + KP_LAG + KP_UNR - 1) / KP_UNR * KP_UNR : 0;
 
   kb_f4 ring[NR][NQ];
   kb_acc acc0 = (kb_acc){}, acc1 = (kb_acc){};
@@ -2229,14 +2261,16 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     _Float16 hv[CPL];
     kfs_f2 p2v = (kfs_f2){0.f, 0.f};
 #pragma unroll
-    for (int q = 0; q < NQ; ++q)
+    for (int q = 0; q < NQ; ++q) {
+      const kb_f4 m4 = *(const kb_f4*)(mus + col0 + 4 * q);
 #pragma unroll
       for (int e = 0; e < 4; e += 2) {
-        const kfs_f2 x = (kfs_f2){r[q][e], r[q][e + 1]} - (kfs_f2){mu[4 * q + e], mu[4 * q + e + 1]};
+        const kfs_f2 x = (kfs_f2){r[q][e], r[q][e + 1]} - (kfs_f2){m4[e], m4[e + 1]};
         p2v = __builtin_elementwise_fma(x, x, p2v);
         hv[4 * q + e] = (_Float16)x[0];
         hv[4 * q + e + 1] = (_Float16)x[1];
       }
+    }
     unsigned char* hrow = xh + ((size_t)(u & 1) * U + j) * RS + 2 * col0;
 #pragma unroll
     for (int gq = 0; gq < CPL / 8; ++gq)
@@ -2268,115 +2302,114 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     const unsigned int qb = __builtin_bit_cast(unsigned int, lo) & 15u;
     il = 32 * ct + (int)((qb & 3) + 8 * (qb >> 2)) + 4 * h;
   };
-  // vector role, part 1: unit u's accumulators -> the wave's top-2 over its
-  // 64 centres per row -> exv[u & 1] (lane j: (b1, b2), lane j + 32: index)
-  auto fold = [&](int u) __attribute__((always_inline)) {
-    float lo0 = -INFINITY, sec0 = -INFINITY, lo1 = -INFINITY, sec1 = -INFINITY;
-    int il0 = 0, il1 = 0;
-    if (scr0) fold16(acc0, 2 * s, lo0, sec0, il0);
-    if (scr1) fold16(acc1, 2 * s + 1, lo1, sec1, il1);
-    const float b1 = ks_max(lo0, lo1), b2 = ks_med3(lo0, lo1, ks_max(sec0, sec1));
-    const int ib = lo0 >= lo1 ? il0 : il1;
-    // the other 32 centres of row j sit in lane j + 32 (and vice versa): a
-    // half swap; the merge is symmetric, so both lanes end with the same bits
-    float b1l, b1h, b2l, b2h, fl, fh;
-    sw32(b1, b1l, b1h);
-    sw32(b2, b2l, b2h);
-    sw32(__builtin_bit_cast(float, ib), fl, fh);
-    const float B1 = ks_max(b1l, b1h), B2 = ks_med3(b1l, b1h, ks_max(b2l, b2h));
-    const int IB = b1l >= b1h ? __builtin_bit_cast(int, fl) : __builtin_bit_cast(int, fh);
-    unsigned char* er = exv + ((size_t)(u & 1) * U + j) * KP_XS;
-    if (h == 0)
-      *(kfs_f2*)(er + 8 * s) = (kfs_f2){B1, B2};
-    else
-      *(int*)(er + 32 + 4 * s) = IB;
-  };
 
-  typedef __attribute__((address_space(3))) unsigned char lds_u8;
-  // (relaxed atomics on the table: not folded into the lane's own store like
-  // plain accesses, and not waited for at once like volatile ones)
-  auto tput = [](lds_u8* p, int v) __attribute__((always_inline)) {
-    __hip_atomic_store(p, (unsigned char)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  };
-  auto tget = [](lds_u8* p) __attribute__((always_inline)) {
-    return (int)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  };
-  lds_u8* const tb = (lds_u8*)(tbl + s * 256);
-  lds_u8* const tdum = (lds_u8*)(ldum + lane);
-
-  // matrix role of slot t: MFMAs of unit t (if t < nit) with the decision
-  // and table rounds of unit t - 2 woven between them; then unit t - 2's
-  // read-add-writes, labels and undecided bits; then the loads of unit t + 4
-  // into the ring entry unit t - 2 leaves.
-  auto matrix_role = [&](int tt, kb_f4 (&r)[NQ]) __attribute__((always_inline)) {
-    const bool mf = tt < nit;
-    const int u2 = tt - 2;
-    const bool dv = u2 >= 0 && u2 < nit;
-    const i64 un2 = bk + (i64)(dv ? u2 : 0) * G;
-    const i64 grow = un2 * U + j;
+  // vector role of slot t: the decision of unit t - 2 and its add rounds
+  // (dres[(t - 2) & 3]), the fold of unit t - 1 (exv[(t - 1) & 1]), the
+  // staging of unit t + 1.  Every wave of the group computes the decision
+  // (the same bits; wave 0 writes it): its LDS round trips run in the shadow
+  // of the fold's vector work, interleaved by hand (sched barriers).
+  auto vector_role = [&](int tt, const kb_f4 (&rs)[NQ]) __attribute__((always_inline)) {
+    const int u2 = tt - 2, uf = tt - 1, us = tt + 1;
+    const bool dv = u2 >= 0 && u2 < nit, fv = uf >= 0 && uf < nit;
+    const i64 grow = (bk + (i64)(dv ? u2 : 0) * G) * U + j;
     const bool rlive = dv && grow < N;
-    const unsigned char* bp = xh + ((size_t)(tt & 1) * U + j) * RS + 16 * h;
     const unsigned char* er = exv + ((size_t)(u2 & 1) * U + j) * KP_XS;
     const unsigned char* pr = p2p + ((size_t)(u2 & 3) * U + j) * KP_XS;
+    // (1) the decision's loads
+    const kb_f4 e4 = *(const kb_f4*)(er + 16 * h);
+    const kfs_i2 i2 = *(const kfs_i2*)(er + 32 + 8 * h);
+    const kb_f4 p4 = *(const kb_f4*)(pr + 16 * h);
+    // (2) fold, first tile (its latency cover)
+    float lo0 = -INFINITY, sec0 = -INFINITY, lo1 = -INFINITY, sec1 = -INFINITY;
+    int il0 = 0, il1 = 0;
+    if (fv && scr0) fold16(acc0, 2 * s, lo0, sec0, il0);
+    __builtin_amdgcn_sched_barrier(0);
+    // (3) decide: top-2 over the 4 waves' candidates, the certified rule
+    int d;
+    {
+      const float b1 = ks_max(e4[0], e4[2]), b2 = ks_med3(e4[0], e4[2], ks_max(e4[1], e4[3]));
+      const int ib = e4[0] >= e4[2] ? i2[0] : i2[1];
+      const float pp = (p4[0] + p4[1]) + (p4[2] + p4[3]);
+      float b1l, b1h, b2l, b2h, fl, fh, pl, ph;
+      sw32(b1, b1l, b1h);
+      sw32(b2, b2l, b2h);
+      sw32(__builtin_bit_cast(float, ib), fl, fh);
+      sw32(pp, pl, ph);
+      const float B1 = ks_max(b1l, b1h), B2 = ks_med3(b1l, b1h, ks_max(b2l, b2h));
+      const int IB = b1l >= b1h ? __builtin_bit_cast(int, fl) : __builtin_bit_cast(int, fh);
+      const float p2f = pl + ph;  // the same order in both lanes of the row
+      const float pn = __builtin_amdgcn_sqrtf(__builtin_fmaf(p2f, 1.001f, 1e-37f)) * 1.0001f;
+      const float e = __builtin_fmaf(__builtin_fmaf(kq[2], pn, kq[1]), pn, kq[0]) * 1.0001f;
+      const bool fin = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim && isfinite(B1) && isfinite(B2);
+      const bool dec = fin && B1 - B2 > 1.0001f * e;
+      d = rlive && dec ? IB : -1;
+    }
+    // (4) each decided row's rank among the unit's rows of its centre (its
+    // add round): one LDS atomic increment per row on wave 0's counter table
+    // (lanes j < 32: one per row; the lanes of one instruction that hit one
+    // address are ordered the same way every time, so the add order -- and
+    // the sums -- are deterministic), the counters reset right behind it;
+    // fold of the second tile beside the round trip
+    const bool act = d >= 0;
+    unsigned int rk = 0;
+    if (s == 0 && h == 0 && act)
+      rk = __hip_atomic_fetch_add(rcnt + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (fv && scr1) fold16(acc1, 2 * s + 1, lo1, sec1, il1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (s == 0 && h == 0 && act) __hip_atomic_store(rcnt + d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // (5) merge the fold's tiles and halves, the candidates out
+    const float fb1 = ks_max(lo0, lo1), fb2 = ks_med3(lo0, lo1, ks_max(sec0, sec1));
+    const int fib = lo0 >= lo1 ? il0 : il1;
+    float c1l, c1h, c2l, c2h, cfl, cfh;
+    sw32(fb1, c1l, c1h);
+    sw32(fb2, c2l, c2h);
+    sw32(__builtin_bit_cast(float, fib), cfl, cfh);
+    const float FB1 = ks_max(c1l, c1h), FB2 = ks_med3(c1l, c1h, ks_max(c2l, c2h));
+    const int FIB = c1l >= c1h ? __builtin_bit_cast(int, cfl) : __builtin_bit_cast(int, cfh);
+    if (fv) {
+      unsigned char* ew = exv + ((size_t)(uf & 1) * U + j) * KP_XS;
+      if (h == 0)
+        *(kfs_f2*)(ew + 8 * s) = (kfs_f2){FB1, FB2};
+      else
+        *(int*)(ew + 32 + 4 * s) = FIB;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // (6) stage of unit t + 1
+    if (us < nit) stage(rs, us);
+    const int rnd = act ? (int)rk : 0xffff;  // add round (0xffff: no add)
+    if (s == 0 && h == 0) dres[(u2 & 3) * U + j] = (d & 0xffff) | (rnd << 16);
+  };
+
+  // matrix role of slot t: the MFMAs of unit t (if t < nit), with the add
+  // rounds of unit t - 4 (raw columns in r, label and round from dres)
+  // between them; then that unit's labels and undecided bits; then the loads
+  // of unit t + 4 into the ring entry unit t - 4 leaves.
+  auto matrix_role = [&](int tt, kb_f4 (&r)[NQ]) __attribute__((always_inline)) {
+    const bool mf = tt < nit;
+    const int ua = tt - KP_LAG;
+    const bool av = ua >= 0 && ua < nit;
+    const i64 una = bk + (i64)(av ? ua : 0) * G;
+    const i64 grow = una * U + j;
+    const bool rlive = av && grow < N;
+    const int dr = dres[(ua & 3) * U + j];
+    const unsigned char* bp = xh + ((size_t)(tt & 1) * U + j) * RS + 16 * h;
+    kh_f8 b = *(const kh_f8*)bp;
+    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+    auto ccop = [&](bool on, int ct) __attribute__((always_inline)) {  // (pieces, 0, 0 0 0 0) or zeros
+      const unsigned long long v = on ? ccl[ct * 32 + j] : 0ull;
+      return __builtin_bit_cast(kb_bf8, (u4v){(unsigned int)v, (unsigned int)(v >> 32), 0u, 0u});
+    };
+    const kb_bf8 cc0 = ccop(h == 0 && scr0, 2 * s);
+    const kb_bf8 cc1 = ccop(h == 0 && scr1, 2 * s + 1);
     if (mf) {
       acc0 = (kb_acc){};
       acc1 = (kb_acc){};
     }
-    int d = -1, tv = 0;
-    bool act = false, rem = false, w0 = false, w1 = false, w2 = false, more = false;
-    kb_f4 e4, p4;
-    kfs_i2 i2;
-    float b1 = 0.f, b2 = 0.f, pp = 0.f;
-    int ib = 0;
-    auto step = [&](auto kc) __attribute__((always_inline)) {
-      constexpr int k = decltype(kc)::value;
-      if constexpr (k == 0) {
-        e4 = *(const kb_f4*)(er + 16 * h);
-        i2 = *(const kfs_i2*)(er + 32 + 8 * h);
-        p4 = *(const kb_f4*)(pr + 16 * h);
-      } else if constexpr (k == 1) {
-        b1 = ks_max(e4[0], e4[2]);
-        b2 = ks_med3(e4[0], e4[2], ks_max(e4[1], e4[3]));
-        ib = e4[0] >= e4[2] ? i2[0] : i2[1];
-        pp = (p4[0] + p4[1]) + (p4[2] + p4[3]);
-      } else if constexpr (k == 2) {
-        float b1l, b1h, b2l, b2h, fl, fh, pl, ph;
-        sw32(b1, b1l, b1h);
-        sw32(b2, b2l, b2h);
-        sw32(__builtin_bit_cast(float, ib), fl, fh);
-        sw32(pp, pl, ph);
-        const float B1 = ks_max(b1l, b1h), B2 = ks_med3(b1l, b1h, ks_max(b2l, b2h));
-        const int IB = b1l >= b1h ? __builtin_bit_cast(int, fl) : __builtin_bit_cast(int, fh);
-        const float p2f = pl + ph;  // the same order in both lanes of the row
-        const float pn = __builtin_amdgcn_sqrtf(__builtin_fmaf(p2f, 1.001f, 1e-37f)) * 1.0001f;
-        const float e = __builtin_fmaf(__builtin_fmaf(kq[2], pn, kq[1]), pn, kq[0]) * 1.0001f;
-        const bool fin = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim && isfinite(B1) && isfinite(B2);
-        const bool dec = fin && B1 - B2 > 1.0001f * e;
-        d = rlive && dec ? IB : -1;
-      } else if constexpr (k == 3) {
-        act = d >= 0;
-        tput(act ? tb + d : tdum, j);
-      } else if constexpr (k == 4) {
-        tv = tget(act ? tb + d : tdum);
-      } else if constexpr (k == 5) {  // (no short-circuit: a branch would split the straight-line block)
-        w0 = act & (tv == j);
-        rem = act & !w0;
-        tput(rem ? tb + d : tdum, j);
-      } else if constexpr (k == 6) {
-        tv = tget(rem ? tb + d : tdum);
-      } else if constexpr (k == 7) {
-        w1 = rem & (tv == j);
-        rem = rem & !w1;
-        tput(rem ? tb + d : tdum, j);
-      } else if constexpr (k == 8) {
-        tv = tget(rem ? tb + d : tdum);
-      } else if constexpr (k == 9) {
-        w2 = rem & (tv == j);
-        more = rem & !w2;
-      }
-    };
-    // B fragments one k-step ahead
-    kh_f8 b = *(const kh_f8*)bp;
+    const int d = av ? (int)(short)(dr & 0xffff) : -1;
+    const int rnd = av ? (int)((unsigned int)dr >> 16) : 0xffff;
+    float* const srow = sums + (d >= 0 ? d : 0) * D;
+    const int sw = (d >= 0 ? d : 0) & (D - 4);  // XOR by a multiple of 4: the lane's 4-column groups stay whole
+    kb_f4 v0[NQ];
     auto mk = [&](auto kc) __attribute__((always_inline)) {
       constexpr int ks = decltype(kc)::value;
       kh_f8 nb = b;
@@ -2384,68 +2417,43 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
       if (mf && scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[0][ks], b, acc0, 0, 0, 0);
       if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[1][ks], b, acc1, 0, 0, 0);
       b = nb;
-      if constexpr (KS == 8) {
-        step(std::integral_constant<int, ks>{});
-      } else {
-        step(std::integral_constant<int, 2 * ks>{});
-        step(std::integral_constant<int, 2 * ks + 1>{});
+      // round 0 of the adds: reads after the first MFMA pair, the write-back
+      // three pairs later (the reads' latency under the MFMAs)
+      if constexpr (ks == 0) {
+        if (rnd == 0) {
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) v0[q] = *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw));
+        }
+      } else if constexpr (ks == (KS == 8 ? 3 : 2)) {
+        if (rnd == 0) {
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw)) = v0[q] + r[q];
+          if (s == 0 && h == 0) cnts[d] += 1u;
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
     };
     ks_unroll(mk, std::make_integer_sequence<int, KS>{});
-    if (mf && scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ccp[0], ones, acc0, 0, 0, 0);
-    if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ccp[1], ones, acc1, 0, 0, 0);
-    step(std::integral_constant<int, 8>{});
-    step(std::integral_constant<int, 9>{});
-    // the read-add-writes of unit t - 2 (raw columns in r), round by round
-    // (a wave's LDS operations run in issue order: round k + 1 reads what
-    // round k wrote)
-    float* const srow = sums + (d >= 0 ? d : 0) * D;
-    const int sw = (d >= 0 ? d : 0) & (D - 4);  // XOR by a multiple of 4: the lane's 4-column groups stay whole
-    auto rmw = [&]() __attribute__((always_inline)) {
-      kb_f4 v[NQ];
+    if (mf && scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cc0, ones, acc0, 0, 0, 0);
+    if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cc1, ones, acc1, 0, 0, 0);
+    // the later rounds (a wave's LDS operations run in issue order: round
+    // k + 1 reads what round k wrote); rounds are ranks, so the loop ends
+    // with the unit's largest rank (<= 34)
+    for (int k = 1; __ballot(rnd >= k && rnd != 0xffff) != 0ull; ++k)
+      if (rnd == k) {
+        kb_f4 v[NQ];
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) v[q] = *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw));
-      const unsigned int cv = s == 0 && h == 0 ? cnts[d] : 0u;
+        for (int q = 0; q < NQ; ++q) v[q] = *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw));
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw)) = v[q] + r[q];
-      if (s == 0 && h == 0) cnts[d] = cv + 1u;
-    };
-    if (w0) rmw();
-    if (w1) rmw();
-    if (w2) rmw();
-    // a centre's fourth and later rows of the unit (rare on settled centres,
-    // a few per unit from data-point centres): each row's rank among its
-    // centre's remaining rows from ballots over the distinct labels (scalar
-    // loop: every step removes at least the label it reads, so it ends after
-    // at most 32 steps; a device trap makes that bound an invariant), then one
-    // read-add-write round per rank
-    const unsigned long long mm = __ballot(more) & 0xffffffffull;  // rows (lanes j; lane j + 32 is the same row)
-    if (mm) {
-      int rk = 0, kmax = 0, guard = 0;
-      unsigned long long left = mm;
-      while (left) {
-        if (++guard > 32) {  // unreachable: a trap (inline, so the loop's control flow stays as it is)
-          asm volatile("s_trap 2");
-          break;
-        }
-        const int L = __builtin_amdgcn_readlane(d, __builtin_ctzll(left));
-        const bool in = more && d == L;
-        const unsigned long long gl = __ballot(in) & 0xffffffffull;
-        left &= ~gl;
-        if (in) rk = __popcll(gl & ((1ull << j) - 1ull));
-        const int gk = __popcll(gl) - 1;
-        kmax = gk > kmax ? gk : kmax;
+        for (int q = 0; q < NQ; ++q) *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw)) = v[q] + r[q];
+        if (s == 0 && h == 0) cnts[d] += 1u;
       }
-      for (int k = 0; k <= kmax; ++k)
-        if (more && rk == k) rmw();
-    }
     // labels (-1 for an undecided row: the list passes write it) and the
     // unit's undecided-row mask; every store issued
     i64* la = h == 0 && rlive ? labels + grow : (i64*)dummy;
     *la = (i64)d;
     const unsigned long long m = __ballot(d < 0 && rlive) & 0xffffffffull;
-    unsigned long long* ma = lane == 0 && dv ? und_mask + un2 : dummy + 1;
+    unsigned long long* ma = lane == 0 && av ? und_mask + una : dummy + 1;
     *ma = m;
     load(r, tt + KP_AHEAD);
   };
@@ -2468,13 +2476,10 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
         __syncthreads();
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
       }
-    if constexpr ((c & 1) == GR) {
-      matrix_role(tt, ring[((c + KP_UNR - 2) >> 1) % NR]);
-    } else {
-      const int uf = tt - 1, us = tt + 1;
-      if (uf >= 0 && uf < nit) fold(uf);
-      if (us < nit) stage(ring[((c + 1) >> 1) % NR], us);
-    }
+    if constexpr ((c & 1) == GR)
+      matrix_role(tt, ring[((c + KP_UNR - KP_LAG) >> 1) % NR]);
+    else
+      vector_role(tt, ring[((c + 1) >> 1) % NR]);
   };
 
   auto body = [&](auto gc) __attribute__((always_inline)) {
@@ -2485,7 +2490,7 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
       // compiler's count of outstanding operations is the same at the loop
       // head on entry and on the back edge
 #pragma unroll
-      for (int k = 0; k < NR - 1; ++k) {
+      for (int k = 0; k < KP_AHEAD / 2; ++k) {
         __builtin_nontemporal_store(0ull, dummy + (lane & 1) + 4 * k);
         __builtin_nontemporal_store(0ull, dummy + 2 + (lane & 1) + 4 * k);
         load(ring[k], GR + 2 * k);
@@ -2501,6 +2506,7 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
   // the set-up loads (centres, mu, bound inputs) complete here, so the loop's
   // waits count only the ring's loads and the slots' stores
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __syncthreads();  // sums, mus, ccl
   if (grp == 0)
     body(std::integral_constant<int, 0>{});
   else
@@ -3323,7 +3329,7 @@ static i64 kfs_nblk(i64 N) { return ((N + 31) / 32 + 256 * 16 - 1) / (256 * 16);
 // windows of k_kmeans_pp's fp32 partials per block (the block with the most units)
 static i64 kp_nwin(i64 N) {
   const i64 nunits = (N + KP_U - 1) / KP_U, G = kfs_grid(N);
-  const i64 nit = (nunits + G - 1) / G, nrun = (nit + 2 + KP_UNR - 1) / KP_UNR * KP_UNR;
+  const i64 nit = (nunits + G - 1) / G, nrun = (nit + KP_LAG + KP_UNR - 1) / KP_UNR * KP_UNR;
   return (nrun - 1) / KP_FW + 1;
 }
 

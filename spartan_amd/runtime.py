@@ -63,6 +63,20 @@ class Context:
                                                             self.num_workers)
 
 
+def data_plane(device_type, env=None):
+  """The device-collective backend a multi-rank run starts with: 'rccl' (the
+  libspx C-ABI communicator) on GPUs unless SPARTAN_DIST_BACKEND names
+  another ('nccl': torch's RCCL group; 'gloo': host-staged rehearsal); 'gloo'
+  for CPU devices (tests)."""
+  env = os.environ if env is None else env
+  backend = env.get('SPARTAN_DIST_BACKEND', 'rccl' if device_type == 'cuda' else 'gloo')
+  if backend not in ('nccl', 'rccl', 'gloo'):
+    raise ValueError('SPARTAN_DIST_BACKEND must be nccl, rccl or gloo, not %r' % backend)
+  if backend == 'rccl' and (env.get('SPARTAN_COMM') == 'torch' or device_type != 'cuda'):
+    backend = 'nccl' if device_type == 'cuda' else 'gloo'
+  return backend
+
+
 def _rccl_init_bounded(comm, rank, world, uid, device, timeout):
   """spx_comm_init on a helper thread, waited for at most ``timeout`` s.
 
@@ -128,11 +142,7 @@ def initialize(argv=None, device=None):
   ctl = None
   if world > 1:
     import torch.distributed as dist
-    backend = os.environ.get('SPARTAN_DIST_BACKEND', 'rccl' if device.type == 'cuda' else 'gloo')
-    if backend not in ('nccl', 'rccl', 'gloo'):
-      raise ValueError('SPARTAN_DIST_BACKEND must be nccl, rccl or gloo, not %r' % backend)
-    if backend == 'rccl' and (os.environ.get('SPARTAN_COMM') == 'torch' or device.type != 'cuda'):
-      backend = 'nccl' if device.type == 'cuda' else 'gloo'
+    backend = data_plane(device.type)
     pg = 'nccl' if backend == 'nccl' else 'gloo'   # torch.distributed: control plane (or the torch RCCL path)
     if not dist.is_initialized():
       os.environ.setdefault('MASTER_ADDR', '127.0.0.1')

@@ -238,3 +238,18 @@ def test_world2_gloo(W):
     p.join(timeout=60)
   for r in range(2):
     assert res.get(r) == 'ok', res.get(r)
+
+
+def test_default_data_plane_is_libspx_rccl():
+  """Round 4: at world > 1 on GPUs the device collectives default to the
+  libspx C-ABI RCCL communicator; SPARTAN_DIST_BACKEND overrides; CPU runs
+  use gloo."""
+  import pytest
+  from spartan_amd import runtime
+  assert runtime.data_plane('cuda', {}) == 'rccl'
+  assert runtime.data_plane('cuda', {'SPARTAN_DIST_BACKEND': 'nccl'}) == 'nccl'
+  assert runtime.data_plane('cuda', {'SPARTAN_DIST_BACKEND': 'gloo'}) == 'gloo'
+  assert runtime.data_plane('cuda', {'SPARTAN_COMM': 'torch'}) == 'nccl'
+  assert runtime.data_plane('cpu', {}) == 'gloo'
+  with pytest.raises(ValueError):
+    runtime.data_plane('cuda', {'SPARTAN_DIST_BACKEND': 'mpi'})

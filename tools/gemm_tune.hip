@@ -34,6 +34,8 @@ struct Variant {
 
 #define V(T, BM, BN, BK, WM, WN, GM) \
   Variant<T>{#BM "x" #BN "x" #BK " w" #WM "x" #WN " g" #GM, Config<T, BM, BN, BK, WM, WN, GM>::launch}
+#define VG(T, BM, BN, BK, WM, WN, GM, GFL) \
+  Variant<T>{#BM "x" #BN "x" #BK " w" #WM "x" #WN " g" #GM " gfl" #GFL, Config<T, BM, BN, BK, WM, WN, GM, 0, GFL>::launch}
 #define VS(T, BM, BN, BK, WM, WN, GM, SEG) \
   Variant<T>{#BM "x" #BN "x" #BK " w" #WM "x" #WN " g" #GM " seg" #SEG, Config<T, BM, BN, BK, WM, WN, GM, SEG>::launch}
 
@@ -97,6 +99,14 @@ int main(int argc, char** argv) {
   i64 S = argc > 1 ? atoll(argv[1]) : 8192;
   int rounds = argc > 2 ? atoi(argv[2]) : 2;
   std::string which = argc > 3 ? argv[3] : "both";
+  if (which == "gfl") {  // one accumulator set, flushed into C every GFL K-tiles, against SEG and one chain
+    run<float>(S, rounds,
+               {V(float, 256, 128, 16, 4, 2, 8), VS(float, 256, 128, 16, 4, 2, 8, 16), VG(float, 256, 128, 16, 4, 2, 8, 128),
+                VG(float, 256, 128, 16, 4, 2, 8, 256), VG(float, 256, 128, 16, 4, 2, 8, 512),
+                VS(float, 256, 128, 32, 8, 2, 8, 8)},
+               157.3);
+    return 0;
+  }
   if (which == "seg2") {  // two-level accumulation at <= 128 registers (32 x 64 / 64 x 32 wave tiles)
     run<float>(S, rounds,
                {V(float, 256, 128, 16, 4, 2, 8), VS(float, 256, 128, 16, 4, 2, 8, 16), VS(float, 128, 128, 16, 4, 2, 8, 16),

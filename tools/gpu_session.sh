@@ -41,6 +41,11 @@ for s in $STEPS; do
       # small fused-step cases first (ragged units, same-label units, all K / D shapes)
       cd $R && step kmquick 240 python -u -m pytest tests/test_gpu_parity.py -v --timeout 60 --timeout-method thread \
         -p no:cacheprovider -k "kmeans_step_same_row or kmeans_step_matches" > $O/kmquick.log 2>&1 ;;
+    dottests)
+      cd $R && step dottests 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+        -p no:cacheprovider -k "dot or gemm" > $O/dottests.log 2>&1 ;;
+    gemmgfl)
+      cd $R && step gemmgfl 600 ./tools/bin/gemm_tune 32768 2 gfl > $O/gemmgfl.txt 2>&1 ;;
     kmdiag)
       cd $R && step kmdiag 150 python3 -u tools/km_diag.py 1200000 > $O/kmdiag.log 2>&1 ;;
     kmtests)

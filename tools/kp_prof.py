@@ -13,8 +13,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from spartan_amd import backend  # noqa: E402
 
-SEG = ['barrier wait', 'matrix: MFMA + decide + table', 'matrix: rmw rounds 0-2', 'matrix: tail ranks',
-       'matrix: stores + loads', 'vector: fold', 'vector: stage', 'pre-barrier (flush)']
+SEG = ['barrier wait', 'matrix: MFMAs + add round 0', 'matrix: add rounds 1+', 'matrix: stores + loads',
+       'vector: loads + fold 0 + decide', 'vector: rank + fold 1 + exv', 'vector: stage',
+       'pre-barrier (flush)']
 
 
 def main():
@@ -44,7 +45,7 @@ def main():
   G = min(ncu, (N + 31) // 32)
   a = a[:G]
   nit = ((N + 31) // 32 + G - 1) // G
-  nrun = (nit + 2 + 5) // 6 * 6
+  nrun = (nit + 4 + 7) // 8 * 8
   print('N=%d grid=%d slots per block=%d (%s centres)' % (N, G, nrun, 'first-iteration' if first else 'second-iteration'))
   tot = a.sum(axis=2).mean(axis=0)  # per wave, cycles over the kernel's loop
   print('cycles per slot (32 rows), mean over blocks; waves 0-3 | 4-7:')

@@ -28,12 +28,12 @@ ins('  const int col0 = CPW * s + CPL * h;\n',
 ins('    __syncthreads();\n    if constexpr (c == 0)\n', '    KPT(7)\n', after=False)
 ins('    __syncthreads();\n    if constexpr (c == 0)\n', '') 
 s = s.replace('    KPT(7)\n    __syncthreads();\n    if constexpr (c == 0)\n', '    KPT(7)\n    __syncthreads();\n    KPT(0)\n    if constexpr (c == 0)\n')
-ins('    step(std::integral_constant<int, 9>{});\n', '    KPT(1)\n')
-ins('    if (w2) rmw();\n', '    KPT(2)\n')
-ins('    // labels (-1 for an undecided row', '    KPT(3)\n', after=False)
-ins('    load(r, tt + KP_AHEAD);\n', '    KPT(4)\n')
-ins('      if (uf >= 0 && uf < nit) fold(uf);\n', '      KPT(5)\n')
-ins('      if (us < nit) stage(ring[((c + 1) >> 1) % NR], us);\n', '      KPT(6)\n')
+ins('    if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cc1, ones, acc1, 0, 0, 0);\n', '    KPT(1)\n')
+ins('    // labels (-1 for an undecided row', '    KPT(2)\n', after=False)
+ins('    load(r, tt + KP_AHEAD);\n', '    KPT(3)\n')
+ins('    // (4) each decided row', '    KPT(4)\n', after=False)
+ins('    // (6) stage of unit t + 1\n', '    KPT(5)\n', after=False)
+ins('    if (s == 0 && h == 0) dres[', '    KPT(6)\n', after=False)
 ins('  if (t < K) pcnt[(i64)bk * K + t] = cnts[t];\n}\n',
     '', after=True)
 s = s.replace('  if (t < K) pcnt[(i64)bk * K + t] = cnts[t];\n}\n\ntemplate <int KS, int NCT>\nstatic void kp_launch',
@@ -46,6 +46,7 @@ s = s.replace('#include "gemm_kernels.h"', '#include "%s/spartan_amd/csrc/gemm_k
 open(sys.argv[2], 'w').write(s)
 PY
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared -std=c++17 \
-  -mllvm -amdgpu-promote-alloca-to-vector-limit=1024 -o "$here/tools/bin/libspx_kpprof.so" "$src" \
+  -mllvm -amdgpu-promote-alloca-to-vector-limit=1024 -o "$here/tools/bin/libspx_kpprof.so.tmp" "$src" \
   "$here/spartan_amd/csrc/tiling.cpp" "$here/spartan_amd/csrc/comm.cpp" -ldl
+mv "$here/tools/bin/libspx_kpprof.so.tmp" "$here/tools/bin/libspx_kpprof.so"
 echo "built tools/bin/libspx_kpprof.so"
