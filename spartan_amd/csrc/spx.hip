@@ -2160,7 +2160,7 @@ static_assert(KP_FW % KP_UNR == 0 && KP_UNR == 2 * KP_NR && KP_AHEAD + KP_LAG ==
               "flush points fall on the unrolled body's first slot; the ring cycles once per body");
 static size_t kp_lds_bytes(int D) {
   return (size_t)256 * D * 4 + 256 * 4 + (size_t)2 * KP_U * kfs_rs(D) + (size_t)2 * KP_U * KP_XS +
-         (size_t)4 * KP_U * KP_XS + (size_t)4 * KP_U * 4 + 256 * 4 + (size_t)D * 4 + (size_t)8 * 32 * 8;
+         (size_t)4 * KP_U * KP_XS + (size_t)4 * KP_U * 4 + 256 * 4 + (size_t)8 * 32 * 8;
 }
 
 template <int KS, int NCT>
@@ -2186,13 +2186,14 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
   unsigned char* p2p = exv + (size_t)2 * U * KP_XS;      // [4][U][KP_XS]: 8 |x'|^2 column partials (by unit mod 4)
   int* dres = (int*)(p2p + (size_t)4 * U * KP_XS);       // [4][U]: label (low 16 bits, -1: undecided) | add round << 16
   unsigned int* rcnt = (unsigned int*)(dres + 4 * U);    // [256] rows per centre so far in the unit (rank counters)
-  float* mus = (float*)(rcnt + 256);                     // [D] mu (the stage reads it: no registers held)
-  unsigned long long* ccl = (unsigned long long*)(mus + D);  // [8 tiles][32] -cc/2 as 3 bf16 pieces + a zero
+  unsigned long long* ccl = (unsigned long long*)(rcnt + 256);  // [8 tiles][32] -cc/2 as 3 bf16 pieces + a zero
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, grp = w >> 2, s = w & 3, j = lane & 31, h = lane >> 5;
   const int col0 = CPW * s + CPL * h;
   for (int i = t; i < 256 * D + 256; i += KP_WAVES * 64) sums[i] = 0.f;  // (cnts: the same bits)
   for (int i = t; i < 256; i += KP_WAVES * 64) rcnt[i] = 0u;
-  for (int i = t; i < D; i += KP_WAVES * 64) mus[i] = muf[i];
+  float mu[CPL];
+#pragma unroll
+  for (int e = 0; e < CPL; ++e) mu[e] = muf[col0 + e];
 
   // A operands: wave s screens centre tiles 2s and 2s + 1 (lane (j, h):
   // centre 32 ct + j, dims 16 ks + 8 h .. + 8 of k-step ks)
@@ -2262,10 +2263,9 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     kfs_f2 p2v = (kfs_f2){0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      const kb_f4 m4 = *(const kb_f4*)(mus + col0 + 4 * q);
 #pragma unroll
       for (int e = 0; e < 4; e += 2) {
-        const kfs_f2 x = (kfs_f2){r[q][e], r[q][e + 1]} - (kfs_f2){m4[e], m4[e + 1]};
+        const kfs_f2 x = (kfs_f2){r[q][e], r[q][e + 1]} - (kfs_f2){mu[4 * q + e], mu[4 * q + e + 1]};
         p2v = __builtin_elementwise_fma(x, x, p2v);
         hv[4 * q + e] = (_Float16)x[0];
         hv[4 * q + e + 1] = (_Float16)x[1];
@@ -2393,7 +2393,12 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     const bool rlive = av && grow < N;
     const int dr = dres[(ua & 3) * U + j];
     const unsigned char* bp = xh + ((size_t)(tt & 1) * U + j) * RS + 16 * h;
-    kh_f8 b = *(const kh_f8*)bp;
+    // B fragments three k-steps ahead: under load an LDS read takes longer
+    // than one MFMA pair, and a read issued one step ahead stalled every pair
+    constexpr int PF = KS < 3 ? KS : 3;
+    kh_f8 bq[4];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) bq[p] = *(const kh_f8*)(bp + 32 * p);
     typedef unsigned int u4v __attribute__((ext_vector_type(4)));
     auto ccop = [&](bool on, int ct) __attribute__((always_inline)) {  // (pieces, 0, 0 0 0 0) or zeros
       const unsigned long long v = on ? ccl[ct * 32 + j] : 0ull;
@@ -2409,37 +2414,20 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     const int rnd = av ? (int)((unsigned int)dr >> 16) : 0xffff;
     float* const srow = sums + (d >= 0 ? d : 0) * D;
     const int sw = (d >= 0 ? d : 0) & (D - 4);  // XOR by a multiple of 4: the lane's 4-column groups stay whole
-    kb_f4 v0[NQ];
     auto mk = [&](auto kc) __attribute__((always_inline)) {
       constexpr int ks = decltype(kc)::value;
-      kh_f8 nb = b;
-      if constexpr (ks + 1 < KS) nb = *(const kh_f8*)(bp + 32 * (ks + 1));
-      if (mf && scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[0][ks], b, acc0, 0, 0, 0);
-      if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[1][ks], b, acc1, 0, 0, 0);
-      b = nb;
-      // round 0 of the adds: reads after the first MFMA pair, the write-back
-      // three pairs later (the reads' latency under the MFMAs)
-      if constexpr (ks == 0) {
-        if (rnd == 0) {
-#pragma unroll
-          for (int q = 0; q < NQ; ++q) v0[q] = *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw));
-        }
-      } else if constexpr (ks == (KS == 8 ? 3 : 2)) {
-        if (rnd == 0) {
-#pragma unroll
-          for (int q = 0; q < NQ; ++q) *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw)) = v0[q] + r[q];
-          if (s == 0 && h == 0) cnts[d] += 1u;
-        }
-      }
+      if constexpr (ks + PF < KS) bq[(ks + PF) & 3] = *(const kh_f8*)(bp + 32 * (ks + PF));
+      if (mf && scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[0][ks], bq[ks & 3], acc0, 0, 0, 0);
+      if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[1][ks], bq[ks & 3], acc1, 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     };
     ks_unroll(mk, std::make_integer_sequence<int, KS>{});
     if (mf && scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cc0, ones, acc0, 0, 0, 0);
     if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cc1, ones, acc1, 0, 0, 0);
-    // the later rounds (a wave's LDS operations run in issue order: round
-    // k + 1 reads what round k wrote); rounds are ranks, so the loop ends
-    // with the unit's largest rank (<= 34)
-    for (int k = 1; __ballot(rnd >= k && rnd != 0xffff) != 0ull; ++k)
+    // the add rounds, after the MFMAs are issued (a wave's LDS operations run
+    // in issue order: round k + 1 reads what round k wrote); rounds are
+    // ranks, so the loop ends with the unit's largest rank (< 32)
+    for (int k = 0; __ballot(rnd >= k && rnd != 0xffff) != 0ull; ++k)
       if (rnd == k) {
         kb_f4 v[NQ];
 #pragma unroll
@@ -2506,7 +2494,7 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
   // the set-up loads (centres, mu, bound inputs) complete here, so the loop's
   // waits count only the ring's loads and the slots' stores
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  __syncthreads();  // sums, mus, ccl
+  __syncthreads();  // sums, rcnt, ccl
   if (grp == 0)
     body(std::integral_constant<int, 0>{});
   else
