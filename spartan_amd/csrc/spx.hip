@@ -617,10 +617,11 @@ extern "C" int spx_argreduce_combine(int op, int dtype, const void* vals, const 
 // fp32: 256x128x16, 8 waves (with the k-contiguous A staging: 141.4 TF = 89.9 %
 // of 157.3 at 32768^3 against 135.6 TF for the 256x256x16 16-wave tile,
 // profiles/r02_gemm_tune_ak.txt)
-// fp32: one accumulator set, flushed into C every 256 K-tiles (gemm_kernels.h
-// GFL): chains of 2048 MFMA steps instead of K / 2, at the one-chain form's
-// registers and occupancy (round 3's register two-level form, SEG, cost 6 %)
-constexpr int SPX_GEMM_GFL = 256;
+// fp32: one accumulator set, flushed into C every 512 K-tiles (gemm_kernels.h
+// GFL): chains of 4096 MFMA steps instead of K / 2, at the one-chain form's
+// registers and occupancy (round 3's register two-level form, SEG, cost 6 %;
+// GFL 128 / 256 / 512: 139.1 / 140.1 / 140.8 TF, profiles/r04_gemm_gfl.txt)
+constexpr int SPX_GEMM_GFL = 512;
 typedef spx_mfma::Config<float, 256, 128, 16, 4, 2, 8, 0, SPX_GEMM_GFL> GemmF32Big;
 typedef spx_mfma::Config<float, 128, 128, 16, 2, 2, 8, 0, SPX_GEMM_GFL> GemmF32Small;
 
@@ -2129,16 +2130,16 @@ static void ks_launch_n(int nct, hipStream_t s, i64 N, i64 D, const float* P, i6
 // unit mod 4); the sums are written by the matrix group only.
 // The certified decision is k_kmeans_filter_as MODE 1's (same MFMA chains,
 // bound, kq and finiteness checks; 4-bit register tags per centre tile).
-// Accumulation: the block's per-centre sums live in LDS as fp32 [256][D]
-// (columns XOR-swizzled by the centre).  Lane (j, h) of wave s holds columns
-// D/4 s + D/8 h .. + D/8 of row j, so a wave adds its rows from the registers
+// Accumulation: the block's per-centre sums live in LDS as fp32 [256][D].
+// Lane (jr, hr) of wave s holds columns D/4 s + D/8 hr .. + D/8 of row jr
+// (row-rotated quads, see below), so a wave adds its rows from the registers
 // the loads landed in and waves never share an address.  Two rows of one
 // centre in one unit would race in a plain read-add-write, so the adds go in
-// rounds: a row's round is its rank among the unit's rows of its centre --
-// rounds 0-2 from a per-wave byte table (a row joins round k when it wins
-// its centre's slot at the k-th write / read-back, the LDS unit's fixed
-// choice), later ones from ballots over the distinct labels (a loop of at
-// most 32 steps: each removes one label; a device trap guards the bound).
+// rounds: a row's round is its rank among the unit's rows of its centre,
+// from one LDS atomic increment per decided row on a counter table (the
+// decision's wave; the lanes of one instruction that hit one counter are
+// ordered the same way every time), and the round loop runs to the unit's
+// largest rank (< 32 by construction: no data-dependent bound to guard).
 // The order of every add is fixed: the sums are deterministic.  Every KP_FW
 // units the fp32 sums go by plain stores to the block's partial slot for
 // that window and are cleared; the slots are summed in fp64 in a fixed order
@@ -2179,7 +2180,7 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
   typedef KpStep<KS, NCT> C;
   constexpr int D = C::D, CPW = C::CPW, CPL = C::CPL, NQ = C::NQ, RS = C::RS, U = C::U, NR = C::NR;
   extern __shared__ __attribute__((aligned(16))) unsigned char kp_lds[];
-  float* sums = (float*)kp_lds;                          // [256][D] fp32, column c of centre d at c ^ (d & (D - 4))
+  float* sums = (float*)kp_lds;                          // [256][D] fp32
   unsigned int* cnts = (unsigned int*)(sums + 256 * D);  // [256] decided rows per centre
   unsigned char* xh = (unsigned char*)(cnts + 256);      // [2][U][RS] fp16 x' (by unit parity)
   unsigned char* exv = xh + (size_t)2 * U * RS;          // [2][U][KP_XS]: (b1, b2) of waves 0-3, then their 4 indices
@@ -2187,13 +2188,27 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
   int* dres = (int*)(p2p + (size_t)4 * U * KP_XS);       // [4][U]: label (low 16 bits, -1: undecided) | add round << 16
   unsigned int* rcnt = (unsigned int*)(dres + 4 * U);    // [256] rows per centre so far in the unit (rank counters)
   unsigned long long* ccl = (unsigned long long*)(rcnt + 256);  // [8 tiles][32] -cc/2 as 3 bf16 pieces + a zero
+  // (j, h): the MFMA / fold / decision lanes (row j = lane & 31, k-half or
+  // centre half h = lane >> 5).  (jr, hr): the raw-column lanes (row jr =
+  // lane >> 1, column half hr = lane & 1) of the loads, the staging and the
+  // sums adds: lane (jr, hr) of wave s holds columns col0 .. col0 + D/8 of
+  // row jr as NQ 4-column quads, rotated by the row: register q holds quad
+  // (q + jr) mod NQ.  So the 8 lanes of one
+  // ds_write_b128 group (4 rows x 2 halves) store 8 different quads -- 8
+  // distinct bank groups whatever the rows' centres -- and a ds_read_b128
+  // group meets at most 2-way conflicts (a random centre-dependent swizzle
+  // cost ~3x on both).
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, grp = w >> 2, s = w & 3, j = lane & 31, h = lane >> 5;
-  const int col0 = CPW * s + CPL * h;
+  const int jr = lane >> 1, hr = lane & 1;
+  const int col0 = CPW * s + CPL * hr;
   for (int i = t; i < 256 * D + 256; i += KP_WAVES * 64) sums[i] = 0.f;  // (cnts: the same bits)
   for (int i = t; i < 256; i += KP_WAVES * 64) rcnt[i] = 0u;
-  float mu[CPL];
+  auto qof = [&](int q) __attribute__((always_inline)) { return (q + jr) & (NQ - 1); };
+  float mu[CPL];  // rotated like the raw columns
 #pragma unroll
-  for (int e = 0; e < CPL; ++e) mu[e] = muf[col0 + e];
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) mu[4 * q + e] = muf[col0 + 4 * qof(q) + e];
 
   // A operands: wave s screens centre tiles 2s and 2s + 1 (lane (j, h):
   // centre 32 ct + j, dims 16 ks + 8 h .. + 8 of k-step ks)
@@ -2252,31 +2267,29 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
   kb_acc acc0 = (kb_acc){}, acc1 = (kb_acc){};
   auto load = [&](kb_f4 (&r)[NQ], int u) __attribute__((always_inline)) {  // clamped: always a valid address
     const i64 un = bk + (i64)(u < nit ? u : nit - 1) * G;
-    i64 row = un * U + j;
+    i64 row = un * U + jr;
     row = row < N ? row : N - 1;
     const float* p = P + row * ldp + col0;
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) r[q] = *(const kb_f4*)(p + 4 * q);
+    for (int q = 0; q < NQ; ++q) r[q] = *(const kb_f4*)(p + 4 * qof(q));
   };
   auto stage = [&](const kb_f4 (&r)[NQ], int u) __attribute__((always_inline)) {  // unit u -> xh[u & 1], p2p[u & 3]
-    _Float16 hv[CPL];
+    typedef _Float16 kh_4 __attribute__((ext_vector_type(4)));
     kfs_f2 p2v = (kfs_f2){0.f, 0.f};
+    unsigned char* hrow = xh + ((size_t)(u & 1) * U + jr) * RS + 2 * col0;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
+      kh_4 hv;
 #pragma unroll
       for (int e = 0; e < 4; e += 2) {
         const kfs_f2 x = (kfs_f2){r[q][e], r[q][e + 1]} - (kfs_f2){mu[4 * q + e], mu[4 * q + e + 1]};
         p2v = __builtin_elementwise_fma(x, x, p2v);
-        hv[4 * q + e] = (_Float16)x[0];
-        hv[4 * q + e + 1] = (_Float16)x[1];
+        hv[e] = (_Float16)x[0];
+        hv[e + 1] = (_Float16)x[1];
       }
+      *(kh_4*)(hrow + 8 * qof(q)) = hv;
     }
-    unsigned char* hrow = xh + ((size_t)(u & 1) * U + j) * RS + 2 * col0;
-#pragma unroll
-    for (int gq = 0; gq < CPL / 8; ++gq)
-      *(kh_f8*)(hrow + 16 * gq) = (kh_f8){hv[8 * gq], hv[8 * gq + 1], hv[8 * gq + 2], hv[8 * gq + 3],
-                                          hv[8 * gq + 4], hv[8 * gq + 5], hv[8 * gq + 6], hv[8 * gq + 7]};
-    *(float*)(p2p + ((size_t)(u & 3) * U + j) * KP_XS + 4 * (2 * s + h)) = p2v[0] + p2v[1];
+    *(float*)(p2p + ((size_t)(u & 3) * U + jr) * KP_XS + 4 * (2 * s + hr)) = p2v[0] + p2v[1];
   };
   // lane j and lane j + 32 exchange x: both get (x of lane j, x of lane j + 32)
   auto sw32 = [](float x, float& lo, float& hi) __attribute__((always_inline)) {
@@ -2391,7 +2404,7 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     const i64 una = bk + (i64)(av ? ua : 0) * G;
     const i64 grow = una * U + j;
     const bool rlive = av && grow < N;
-    const int dr = dres[(ua & 3) * U + j];
+    const int dr = dres[(ua & 3) * U + jr];  // the add lanes' rows
     const unsigned char* bp = xh + ((size_t)(tt & 1) * U + j) * RS + 16 * h;
     // B fragments three k-steps ahead: under load an LDS read takes longer
     // than one MFMA pair, and a read issued one step ahead stalled every pair
@@ -2412,8 +2425,7 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     }
     const int d = av ? (int)(short)(dr & 0xffff) : -1;
     const int rnd = av ? (int)((unsigned int)dr >> 16) : 0xffff;
-    float* const srow = sums + (d >= 0 ? d : 0) * D;
-    const int sw = (d >= 0 ? d : 0) & (D - 4);  // XOR by a multiple of 4: the lane's 4-column groups stay whole
+    float* const srow = sums + (d >= 0 ? d : 0) * D + col0;
     auto mk = [&](auto kc) __attribute__((always_inline)) {
       constexpr int ks = decltype(kc)::value;
       if constexpr (ks + PF < KS) bq[(ks + PF) & 3] = *(const kh_f8*)(bp + 32 * (ks + PF));
@@ -2431,16 +2443,17 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
       if (rnd == k) {
         kb_f4 v[NQ];
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) v[q] = *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw));
+        for (int q = 0; q < NQ; ++q) v[q] = *(kb_f4*)(srow + 4 * qof(q));
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) *(kb_f4*)(srow + ((col0 + 4 * q) ^ sw)) = v[q] + r[q];
-        if (s == 0 && h == 0) cnts[d] += 1u;
+        for (int q = 0; q < NQ; ++q) *(kb_f4*)(srow + 4 * qof(q)) = v[q] + r[q];
+        if (s == 0 && hr == 0) cnts[d] += 1u;
       }
     // labels (-1 for an undecided row: the list passes write it) and the
     // unit's undecided-row mask; every store issued
+    const int dlab = av ? (int)(short)(dres[(ua & 3) * U + j] & 0xffff) : -1;  // the label lanes' rows
     i64* la = h == 0 && rlive ? labels + grow : (i64*)dummy;
-    *la = (i64)d;
-    const unsigned long long m = __ballot(d < 0 && rlive) & 0xffffffffull;
+    *la = (i64)dlab;
+    const unsigned long long m = __ballot(dlab < 0 && rlive) & 0xffffffffull;
     unsigned long long* ma = lane == 0 && av ? und_mask + una : dummy + 1;
     *ma = m;
     load(r, tt + KP_AHEAD);
@@ -2457,7 +2470,7 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
         float* pb = part + ((i64)bk * nwin + tt / KP_FW - 1) * K * D;
         for (int i = 4 * t; i < K * D; i += 4 * KP_WAVES * 64) {
           const int dd = i / D, cl = i % D;
-          kb_f4* src = (kb_f4*)(sums + dd * D + (cl ^ (dd & (D - 4))));
+          kb_f4* src = (kb_f4*)(sums + dd * D + cl);
           *(kb_f4*)(pb + i) = *src;
           *src = (kb_f4){0.f, 0.f, 0.f, 0.f};
         }
@@ -2507,7 +2520,7 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     float* pb = part + ((i64)bk * nwin + wdone) * K * D;
     for (int i = 4 * t; i < K * D; i += 4 * KP_WAVES * 64) {
       const int dd = i / D, cl = i % D;
-      *(kb_f4*)(pb + i) = *(kb_f4*)(sums + dd * D + (cl ^ (dd & (D - 4))));
+      *(kb_f4*)(pb + i) = *(kb_f4*)(sums + dd * D + cl);
     }
     for (int win = wdone + 1; win < nwin; ++win)
       for (int i = 4 * t; i < K * D; i += 4 * KP_WAVES * 64)

@@ -48,6 +48,9 @@ for s in $STEPS; do
       cd $R && step gemmgfl 600 ./tools/bin/gemm_tune 32768 2 gfl > $O/gemmgfl.txt 2>&1 ;;
     kmdiag)
       cd $R && step kmdiag 150 python3 -u tools/km_diag.py 1200000 > $O/kmdiag.log 2>&1 ;;
+    kpprof)
+      # per-segment cycles of the fused step (tools/kp_prof.sh build)
+      cd $R && step kpprof 240 python3 tools/kp_prof.py 100000000 > $O/kpprof.txt 2>&1 ;;
     kmtests)
       cd $R && step kmtests 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
         -p no:cacheprovider -k "kmeans" > $O/kmtests.log 2>&1 ;;

@@ -23,7 +23,7 @@ extern "C" int spx_dev_kp_prof(unsigned long long* host_out) {
 #define KPT(k) { const unsigned long long now_ = __builtin_amdgcn_s_memtime(); pacc_[k] += now_ - plast_; plast_ = now_; }
 '''
 ins('template <int KS, int NCT>\nstruct KpStep {', prof, after=False)
-ins('  const int col0 = CPW * s + CPL * h;\n',
+ins('  const int col0 = CPW * s + CPL * hr;\n',
     '  unsigned long long pacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, plast_ = __builtin_amdgcn_s_memtime();\n')
 ins('    __syncthreads();\n    if constexpr (c == 0)\n', '    KPT(7)\n', after=False)
 ins('    __syncthreads();\n    if constexpr (c == 0)\n', '') 
