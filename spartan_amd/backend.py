@@ -533,11 +533,17 @@ class HipBackend:
       if codegen.rowdots(root) and U == 4:
         U = 8
       rowinv = tuple(s for k, s in enumerate(slots) if vstr[k][1] == 0)
-    sig = ('reduce', root.sig(), tuple(ins), tuple(classes), kind, op, V, U, rowinv)
+    # a fused row dot's lane group width (and whether the vector path covers
+    # the columns exactly) is compiled in: its per-row lane sum is then
+    # straight-line DPP (codegen.gen_reduce)
+    klpr, kfull = None, False
+    if kind == 'cols' and codegen.rowdots(root):
+      klpr, kfull = lpr, bool(vec_ok and CT == 1 and I == lpr * per)
+    sig = ('reduce', root.sig(), tuple(ins), tuple(classes), kind, op, V, U, rowinv, klpr, kfull)
     fn = self._sig_fns.get(sig)
     if fn is None:
-      src, kname = codegen.named(codegen.gen_reduce(root, ins, classes, kind, op, V, U, rowinv), 'spx_reduce',
-                                 kind)
+      src, kname = codegen.named(codegen.gen_reduce(root, ins, classes, kind, op, V, U, rowinv, klpr, kfull),
+                                 'spx_reduce', kind)
       fn = self._sig_fns[sig] = self.kernel(src, kname)
     self.launch(fn, nblk, args)
     if not direct:

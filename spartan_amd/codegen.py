@@ -639,7 +639,7 @@ def _acc_update(op, j, val, idx_expr):
   return 'acc%d = comb(acc%d, %s);' % (j, j, val)
 
 
-def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
+def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=(), lpr=None, full=False):
   """Fused map+reduce.  kind 'rows' (reduce over contiguous R of (O, R), one
   or more blocks per segment), 'rowsp' (the same for short R: several
   segments per wave, LPR lanes each, butterfly combine) or 'cols' (reduce over
@@ -647,6 +647,13 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
 
   classes: per-input addressing class of the vectorised dimension (R for rows,
   I for cols): 'c', 'b' or 'g'.
+
+  'cols' only: ``lpr`` fixes the lanes per row group at compile time (else
+  the launch's aux[2]); ``full`` (with ``lpr``) promises I == lpr * vec, so
+  the vector path needs no column mask.  A fused row dot's per-row lane sum
+  then compiles to 4 straight DPP adds: with a run-time LPR every row paid
+  6 uniform branches, and the column masks a select per element -- cfg5's
+  loop body was 641 instructions per 8 rows, issue-bound beside the loads.
   """
   assert op in REDOPS and kind in ('rows', 'rowsp', 'cols')
   rds = rowdots(root)
@@ -842,10 +849,13 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
   else:
     U = unroll or cols_unroll(inputs, classes, vec)
 
-    def one_row(V, rv, sfx, masked):
+    def one_row(V, rv, sfx, masked, bcu=None):
       """Loads + (row dots) + accumulator updates of row ``rv`` into names
       suffixed ``sfx``; split in (load lines, compute lines) so an unrolled
-      body issues every row's loads before the first use."""
+      body issues every row's loads before the first use.  ``bcu``: this
+      row's index u in an unrolled step whose per-row ('b') inputs were loaded
+      once, row u by lane u of the 16-lane group (``yb<s>``): the value comes
+      by DPP row_newbcast:u instead of a load per row."""
       ld, cp = [], []
       base = lambda s, c: 'o * a.str[%d][0] + %s * a.str[%d][1] + %s * a.str[%d][2]' % (s, rv, s, c, s)
       for (s, dt), cls in zip(inputs, classes):
@@ -853,6 +863,14 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
         names = ['x%d_%d%s' % (s, j, sfx) for j in range(V)]
         if s in rowinv:
           ld += ['%s %s = x%d_%d_ri;' % (ct, n, s, j) for j, n in enumerate(names)]
+          continue
+        if bcu is not None and s in bcast:
+          # (with the compute lines: the broadcast waits for the one load,
+          # which must not hold back the rows' loads)
+          v = 'dpp_mov<%d>(yb%d)' % (0x150 + bcu, s)
+          cp.append('const %s xbb%d%s = %s;' % (ct, s, sfx, v))
+          cp += ['%s %s = %s;' % (ct, n, ('colok ? xbb%d%s : (%s)0' % (s, sfx, ct)) if masked else 'xbb%d%s' % (s, sfx))
+                 for n in names]
           continue
         srcs, pre = load_srcs(s, dt, cls, V, base(s, 'cc' if masked else 'col'))
         ld.append('%s %s;' % (ct, ' '.join(names).replace(' ', ', ')))
@@ -897,13 +915,19 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
         return ['%s[off + %d * s_in]' % (p, j) for j in range(V)], pre
       return ['%s[off]' % p], pre
 
+    # per-row inputs of a row-dot kernel with 16-lane row groups: one load per
+    # unrolled step (lane u of the group fetches row u), DPP broadcasts
+    bcast = ()
+    if rds and lpr == 16 and U > 1 and U <= 16:
+      bcast = tuple(s for (s, dt), cls in zip(inputs, classes) if cls == 'b' and s not in rowinv)
+
     def body(V):
       masked = bool(rds)
       b = []
       # row-dot kernels: every lane of a row group takes part in the DPP row
       # sum, so lanes past the last column read column 0 and use zeros
       b.append('{' if masked else 'if (col < I) {')
-      b.append('  const bool colok = col < I; (void)colok;')
+      b.append('  const bool colok = %s; (void)colok;' % ('true' if (full and lpr and V == vec) else 'col < I'))
       b.append('  const i64 cc = colok ? col : 0; (void)cc;')
       for (s, dt), cls in zip(inputs, classes):
         if s in rowinv:  # row stride 0: loaded once, outside the row loop
@@ -921,9 +945,15 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
       if U > 1:
         b.append('  for (; r + %d * STEP < r1; r += %d * STEP) {' % (U - 1, U))
         lds, cps = [], []
+        for s_ in bcast:
+          ct = ctype(dict(inputs)[s_])
+          b.append('    %s yb%d;' % (ct, s_))
+          b.append('    { const i64 rb = r + (cl < %d ? cl : 0) * STEP;' % U)
+          b.append('      yb%d = ((const GLOBAL %s*)a.ptr[%d])[o * a.str[%d][0] + rb * a.str[%d][1]]; }'
+                   % (s_, ct, s_, s_, s_))
         for u in range(U):
           b.append('    const i64 r_%d = r + %d * STEP;' % (u, u))
-          ld, cp = one_row(V, 'r_%d' % u, '_u%d' % u, masked)
+          ld, cp = one_row(V, 'r_%d' % u, '_u%d' % u, masked, u if bcast else None)
           lds += ld
           cps += cp
         b += ['    ' + x for x in lds + cps]
@@ -937,8 +967,13 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=()):
 
     L.append('KERN void spx_reduce(KArgs a) {')
     L.append('  const i64 O = a.dim[0], R = a.dim[1], I = a.dim[2];')
-    L.append('  const i64 P = a.aux[0], chunk = a.aux[1], lpr_log = a.aux[2], CT = a.aux[3];')
-    L.append('  const i64 LPR = (i64)1 << lpr_log, RPW = 64 >> lpr_log;')
+    if lpr:
+      assert lpr & (lpr - 1) == 0 and 1 <= lpr <= 64
+      L.append('  const i64 P = a.aux[0], chunk = a.aux[1], CT = a.aux[3];')
+      L.append('  constexpr i64 lpr_log = %d, LPR = %d, RPW = %d;' % (lpr.bit_length() - 1, lpr, 64 // lpr))
+    else:
+      L.append('  const i64 P = a.aux[0], chunk = a.aux[1], lpr_log = a.aux[2], CT = a.aux[3];')
+      L.append('  const i64 LPR = (i64)1 << lpr_log, RPW = 64 >> lpr_log;')
     L.append('  const i64 blk = bidx(); const i64 ct = blk % CT; const i64 rest = blk / CT;')
     L.append('  const i64 o = rest % O, p = rest / O;')
     L.append('  const u32 t = tid(); const i64 lane = t & 63, w = t >> 6;')

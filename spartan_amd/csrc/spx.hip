@@ -2161,7 +2161,7 @@ static_assert(KP_FW % KP_UNR == 0 && KP_UNR == 2 * KP_NR && KP_AHEAD + KP_LAG ==
               "flush points fall on the unrolled body's first slot; the ring cycles once per body");
 static size_t kp_lds_bytes(int D) {
   return (size_t)256 * D * 4 + 256 * 4 + (size_t)2 * KP_U * kfs_rs(D) + (size_t)2 * KP_U * KP_XS +
-         (size_t)4 * KP_U * KP_XS + (size_t)4 * KP_U * 4 + 256 * 4 + (size_t)8 * 32 * 8;
+         (size_t)4 * KP_U * KP_XS + (size_t)4 * KP_U * 4 + 256 * 4 + (size_t)8 * 32 * 8 + (size_t)D * 4;
 }
 
 template <int KS, int NCT>
@@ -2188,6 +2188,7 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
   int* dres = (int*)(p2p + (size_t)4 * U * KP_XS);       // [4][U]: label (low 16 bits, -1: undecided) | add round << 16
   unsigned int* rcnt = (unsigned int*)(dres + 4 * U);    // [256] rows per centre so far in the unit (rank counters)
   unsigned long long* ccl = (unsigned long long*)(rcnt + 256);  // [8 tiles][32] -cc/2 as 3 bf16 pieces + a zero
+  float* mus = (float*)(ccl + 8 * 32);                   // [D] the centring vector mu
   // (j, h): the MFMA / fold / decision lanes (row j = lane & 31, k-half or
   // centre half h = lane >> 5).  (jr, hr): the raw-column lanes (row jr =
   // lane >> 1, column half hr = lane & 1) of the loads, the staging and the
@@ -2204,11 +2205,7 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
   for (int i = t; i < 256 * D + 256; i += KP_WAVES * 64) sums[i] = 0.f;  // (cnts: the same bits)
   for (int i = t; i < 256; i += KP_WAVES * 64) rcnt[i] = 0u;
   auto qof = [&](int q) __attribute__((always_inline)) { return (q + jr) & (NQ - 1); };
-  float mu[CPL];  // rotated like the raw columns
-#pragma unroll
-  for (int q = 0; q < NQ; ++q)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) mu[4 * q + e] = muf[col0 + 4 * qof(q) + e];
+  for (int i = t; i < D; i += KP_WAVES * 64) mus[i] = muf[i];
 
   // A operands: wave s screens centre tiles 2s and 2s + 1 (lane (j, h):
   // centre 32 ct + j, dims 16 ks + 8 h .. + 8 of k-step ks)
@@ -2273,7 +2270,12 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
 #pragma unroll
     for (int q = 0; q < NQ; ++q) r[q] = *(const kb_f4*)(p + 4 * qof(q));
   };
-  auto stage = [&](const kb_f4 (&r)[NQ], int u) __attribute__((always_inline)) {  // unit u -> xh[u & 1], p2p[u & 3]
+  auto mu_load = [&](kb_f4 (&mu4)[NQ]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) mu4[q] = *(const kb_f4*)(mus + col0 + 4 * qof(q));
+  };
+  // unit u -> xh[u & 1], p2p[u & 3]
+  auto stage = [&](const kb_f4 (&r)[NQ], const kb_f4 (&mu4)[NQ], int u) __attribute__((always_inline)) {
     typedef _Float16 kh_4 __attribute__((ext_vector_type(4)));
     kfs_f2 p2v = (kfs_f2){0.f, 0.f};
     unsigned char* hrow = xh + ((size_t)(u & 1) * U + jr) * RS + 2 * col0;
@@ -2282,7 +2284,7 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
       kh_4 hv;
 #pragma unroll
       for (int e = 0; e < 4; e += 2) {
-        const kfs_f2 x = (kfs_f2){r[q][e], r[q][e + 1]} - (kfs_f2){mu[4 * q + e], mu[4 * q + e + 1]};
+        const kfs_f2 x = (kfs_f2){r[q][e], r[q][e + 1]} - (kfs_f2){mu4[q][e], mu4[q][e + 1]};
         p2v = __builtin_elementwise_fma(x, x, p2v);
         hv[e] = (_Float16)x[0];
         hv[e + 1] = (_Float16)x[1];
@@ -2362,15 +2364,22 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     // (lanes j < 32: one per row; the lanes of one instruction that hit one
     // address are ordered the same way every time, so the add order -- and
     // the sums -- are deterministic), the counters reset right behind it;
-    // fold of the second tile beside the round trip
+    // fold of the second tile beside the round trip.  The row is counted here
+    // too, by an LDS atomic add with no return (integers: any order gives the
+    // same count; a read-modify-write per add round cost a round trip each)
     const bool act = d >= 0;
     unsigned int rk = 0;
-    if (s == 0 && h == 0 && act)
+    if (s == 0 && h == 0 && act) {
       rk = __hip_atomic_fetch_add(rcnt + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_add(cnts + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     if (fv && scr1) fold16(acc1, 2 * s + 1, lo1, sec1, il1);
     __builtin_amdgcn_sched_barrier(0);
     if (s == 0 && h == 0 && act) __hip_atomic_store(rcnt + d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    // (5) merge the fold's tiles and halves, the candidates out
+    // (5) merge the fold's tiles and halves, the candidates out (mu's reads
+    // for the stage first)
+    kb_f4 mu4[NQ];
+    mu_load(mu4);
     const float fb1 = ks_max(lo0, lo1), fb2 = ks_med3(lo0, lo1, ks_max(sec0, sec1));
     const int fib = lo0 >= lo1 ? il0 : il1;
     float c1l, c1h, c2l, c2h, cfl, cfh;
@@ -2388,7 +2397,7 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     }
     __builtin_amdgcn_sched_barrier(0);
     // (6) stage of unit t + 1
-    if (us < nit) stage(rs, us);
+    if (us < nit) stage(rs, mu4, us);
     const int rnd = act ? (int)rk : 0xffff;  // add round (0xffff: no add)
     if (s == 0 && h == 0) dres[(u2 & 3) * U + j] = (d & 0xffff) | (rnd << 16);
   };
@@ -2426,8 +2435,18 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     const int d = av ? (int)(short)(dr & 0xffff) : -1;
     const int rnd = av ? (int)((unsigned int)dr >> 16) : 0xffff;
     float* const srow = sums + (d >= 0 ? d : 0) * D + col0;
+    // round 0's reads go out before the last MFMAs (the sums rows are
+    // stable: only this group writes them in this slot), their latency under
+    // the MFMA chains
+    kb_f4 v0[NQ];
     auto mk = [&](auto kc) __attribute__((always_inline)) {
       constexpr int ks = decltype(kc)::value;
+      if constexpr (ks == KS - 1) {  // (earlier: the registers spill)
+        if (rnd == 0) {
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) v0[q] = *(kb_f4*)(srow + 4 * qof(q));
+        }
+      }
       if constexpr (ks + PF < KS) bq[(ks + PF) & 3] = *(const kh_f8*)(bp + 32 * (ks + PF));
       if (mf && scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[0][ks], bq[ks & 3], acc0, 0, 0, 0);
       if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[1][ks], bq[ks & 3], acc1, 0, 0, 0);
@@ -2436,21 +2455,27 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     ks_unroll(mk, std::make_integer_sequence<int, KS>{});
     if (mf && scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cc0, ones, acc0, 0, 0, 0);
     if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cc1, ones, acc1, 0, 0, 0);
+    const int dlv = dres[(ua & 3) * U + j];  // the label lanes' rows
     // the add rounds, after the MFMAs are issued (a wave's LDS operations run
     // in issue order: round k + 1 reads what round k wrote); rounds are
     // ranks, so the loop ends with the unit's largest rank (< 32)
-    for (int k = 0; __ballot(rnd >= k && rnd != 0xffff) != 0ull; ++k)
+    if (rnd == 0) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) *(kb_f4*)(srow + 4 * qof(q)) = v0[q] + r[q];
+    }
+    // (a rank is < U by construction -- at most U rows per unit -- so the
+    // cap k < U never binds; it bounds the loop whatever dres holds)
+    for (int k = 1; k < U && __ballot(rnd >= k && rnd != 0xffff) != 0ull; ++k)
       if (rnd == k) {
         kb_f4 v[NQ];
 #pragma unroll
         for (int q = 0; q < NQ; ++q) v[q] = *(kb_f4*)(srow + 4 * qof(q));
 #pragma unroll
         for (int q = 0; q < NQ; ++q) *(kb_f4*)(srow + 4 * qof(q)) = v[q] + r[q];
-        if (s == 0 && hr == 0) cnts[d] += 1u;
       }
     // labels (-1 for an undecided row: the list passes write it) and the
     // unit's undecided-row mask; every store issued
-    const int dlab = av ? (int)(short)(dres[(ua & 3) * U + j] & 0xffff) : -1;  // the label lanes' rows
+    const int dlab = av ? (int)(short)(dlv & 0xffff) : -1;
     i64* la = h == 0 && rlive ? labels + grow : (i64*)dummy;
     *la = (i64)dlab;
     const unsigned long long m = __ballot(dlab < 0 && rlive) & 0xffffffffull;
@@ -2496,7 +2521,11 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
         __builtin_nontemporal_store(0ull, dummy + 2 + (lane & 1) + 4 * k);
         load(ring[k], GR + 2 * k);
       }
-      if constexpr (GR == 0) stage(ring[0], 0);
+      if constexpr (GR == 0) {
+        kb_f4 mu4[NQ];
+        mu_load(mu4);
+        stage(ring[0], mu4, 0);
+      }
     }
     for (int t0 = 0; t0 < nrun; t0 += KP_UNR) {
       ks_unroll([&](auto cc) __attribute__((always_inline)) {

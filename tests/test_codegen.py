@@ -80,3 +80,25 @@ def test_rowdot_cols_compile(dt):
     codegen.gen_reduce(root, ins, ['c', 'b', 'c'], 'rows', 'sum', 1)
   with pytest.raises(NotImplementedError):
     codegen.gen_map(root, ins, ['c', 'b', 'c'], 2, 1, False)
+
+
+@pytest.mark.parametrize('dt', [F32, F64])
+def test_rowdot_cols_fixed_lane_groups(dt):
+  """The cfg5 form of the row-dot kernel: lanes per row group compiled in
+  (LPR 16: the row sum is straight-line DPP, no run-time branches), no column
+  mask on the vector path, and the per-row input (y) loaded once per unrolled
+  step and handed to the step's rows by DPP row_newbcast (one load instead of
+  U), in both the vector and the scalar path.  Compiles for both dtypes."""
+  from spartan_amd.codegen import RowDot
+  x, yv, w = In(0, dt), In(1, dt), In(2, dt)
+  root = Op('multiply', [x, Op('subtract', [RowDot(x, w), yv])])
+  ins = [(0, dt), (1, dt), (2, dt)]
+  V = codegen.vec_width([dt])
+  src = codegen.gen_reduce(root, ins, ['c', 'b', 'c'], 'cols', 'sum', V, 8, (2,), lpr=16, full=True)
+  assert 'constexpr i64 lpr_log = 4, LPR = 16, RPW = 4;' in src
+  assert 'const bool colok = true;' in src
+  assert src.count('dpp_mov<%d>(yb1)' % 0x150) == 2 and 'dpp_mov<%d>(yb1)' % (0x150 + 7) in src
+  _compile(src)
+  # without a fixed width: the run-time form (aux[2]) and no broadcasts
+  src = codegen.gen_reduce(root, ins, ['c', 'b', 'c'], 'cols', 'sum', V, 8, (2,))
+  assert 'lpr_log = a.aux[2]' in src and 'yb1' not in src

@@ -51,6 +51,13 @@ for s in $STEPS; do
     kpprof)
       # per-segment cycles of the fused step (tools/kp_prof.sh build)
       cd $R && step kpprof 240 python3 tools/kp_prof.py 100000000 > $O/kpprof.txt 2>&1 ;;
+    ablate)
+      # k_kmeans_pp ablation builds (tools/kp_ablate.sh), kernel-traced one by one
+      for f in $R/tools/bin/libspx_abl_*.so; do
+        n=$(basename $f .so)
+        cd /tmp && step $n 120 rocprofv3 --kernel-trace --stats -d $O/abl/$n -o p --output-format csv \
+          -- python3 $R/tools/km_step_once.py 100000000 3 step $f > $O/$n.log 2>&1
+      done ;;
     kmtests)
       cd $R && step kmtests 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
         -p no:cacheprovider -k "kmeans" > $O/kmtests.log 2>&1 ;;

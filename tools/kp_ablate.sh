@@ -1,0 +1,43 @@
+#!/bin/bash
+# Dev builds: k_kmeans_pp ablations (work removed by text substitution on a
+# copy of spx.hip -- the product source carries no switches) ->
+# tools/bin/libspx_abl_<name>.so, timed by tools/km_step_once.py under a
+# kernel trace (the results are wrong by design; only the time is read).
+#   tools/kp_ablate.sh name...   (names: base norounds noloop nostage noatomic nobarrier)
+set -e
+here=$(cd "$(dirname "$0")/.." && pwd)
+mkdir -p "$here/tools/bin"
+build() {
+  local name=$1 src=$here/tools/bin/spx_abl_$1.hip
+  python3 - "$here/spartan_amd/csrc/spx.hip" "$src" "$name" <<'PY'
+import sys
+s = open(sys.argv[1]).read()
+name = sys.argv[3]
+subs = {
+  'base': [],
+  'norounds': [('const int rnd = av ? (int)((unsigned int)dr >> 16) : 0xffff;', 'const int rnd = 0xffff;')],
+  'noloop': [('for (int k = 1; k < U && __ballot', 'for (int k = 1; k < 1 && __ballot')],
+  'nostage': [('if (us < nit) stage(', 'if (us < 0) stage(')],
+  'noatomic': [('rk = __hip_atomic_fetch_add(rcnt + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);', 'rk = 0;')],
+  'nobarrier': [('    constexpr int GR = decltype(gc)::value, c = decltype(cc)::value;\n    __syncthreads();\n',
+                 '    constexpr int GR = decltype(gc)::value, c = decltype(cc)::value;\n')],
+}[name]
+for a, b in subs:
+    assert s.count(a) == 1, '%s: %r found %d times' % (name, a[:60], s.count(a))
+    s = s.replace(a, b)
+root = sys.argv[2].rsplit('/tools/', 1)[0]
+s = s.replace('#include "../../include/spx.h"', '#include "%s/include/spx.h"' % root)
+s = s.replace('#include "gemm_kernels.h"', '#include "%s/spartan_amd/csrc/gemm_kernels.h"' % root)
+open(sys.argv[2], 'w').write(s)
+PY
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared -std=c++17 \
+    -mllvm -amdgpu-promote-alloca-to-vector-limit=1024 -o "$here/tools/bin/libspx_abl_$name.so.tmp" "$src" \
+    "$here/spartan_amd/csrc/tiling.cpp" "$here/spartan_amd/csrc/comm.cpp" -ldl
+  mv "$here/tools/bin/libspx_abl_$name.so.tmp" "$here/tools/bin/libspx_abl_$name.so"
+  echo "built tools/bin/libspx_abl_$name.so"
+}
+pids=()
+for n in "$@"; do build "$n" & pids+=($!); done
+rc=0
+for p in "${pids[@]}"; do wait "$p" || rc=1; done
+exit $rc

@@ -14,7 +14,8 @@ sys.path.insert(0, ROOT)
 from spartan_amd import backend  # noqa: E402
 
 SEG = ['barrier wait', 'matrix: MFMAs + add round 0', 'matrix: add rounds 1+', 'matrix: stores + loads',
-       'vector: loads + fold 0 + decide', 'vector: rank + fold 1 + exv', 'vector: stage',
+       'vector: part 1 (v3: fold 0 + decide; v5: fold + exv)', 'vector: part 2 (v3: rank + fold 1)',
+       'vector: stage',
        'pre-barrier (flush)']
 
 

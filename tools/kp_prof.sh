@@ -31,9 +31,13 @@ s = s.replace('    KPT(7)\n    __syncthreads();\n    if constexpr (c == 0)\n', '
 ins('    if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cc1, ones, acc1, 0, 0, 0);\n', '    KPT(1)\n')
 ins('    // labels (-1 for an undecided row', '    KPT(2)\n', after=False)
 ins('    load(r, tt + KP_AHEAD);\n', '    KPT(3)\n')
-ins('    // (4) each decided row', '    KPT(4)\n', after=False)
-ins('    // (6) stage of unit t + 1\n', '    KPT(5)\n', after=False)
-ins('    if (s == 0 && h == 0) dres[', '    KPT(6)\n', after=False)
+if '    // (4) each decided row' in s:  # decision in the vector role (round-4 v3 / v4)
+    ins('    // (4) each decided row', '    KPT(4)\n', after=False)
+    ins('    // (6) stage of unit t + 1\n', '    KPT(5)\n', after=False)
+    ins('    if (s == 0 && h == 0) dres[', '    KPT(6)\n', after=False)
+else:  # decision in the matrix role: vector = fold + exv (4), stage (6)
+    ins('    __builtin_amdgcn_sched_barrier(0);\n    if (us < nit) {\n', '    KPT(4)\n', after=False)
+    ins('      stage(rs, mu4, us);\n    }\n', '    KPT(6)\n')
 ins('  if (t < K) pcnt[(i64)bk * K + t] = cnts[t];\n}\n',
     '', after=True)
 s = s.replace('  if (t < K) pcnt[(i64)bk * K + t] = cnts[t];\n}\n\ntemplate <int KS, int NCT>\nstatic void kp_launch',
