@@ -13,8 +13,18 @@ build() {
 import sys
 s = open(sys.argv[1]).read()
 name = sys.argv[3]
+NR = ('const int rnd = av ? (int)((unsigned int)dr >> 16) : 0xffff;', 'const int rnd = 0xffff;')
 subs = {
   'base': [],
+  # on top of norounds (no adds): what the rest of the slot costs
+  'r_nofold': [NR, ('    if (fv && scr0) fold16(acc0, 2 * s, lo0, sec0, il0);\n', '    lo0 = acc0[0]; sec0 = acc0[1];\n'),
+               ('    if (fv && scr1) fold16(acc1, 2 * s + 1, lo1, sec1, il1);\n', '    lo1 = acc1[0]; sec1 = acc1[1];\n')],
+  'r_nomfma': [NR, ('      if (mf && scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[0][ks], bq[ks & 3], acc0, 0, 0, 0);\n', '      acc0[ks] += (float)bq[ks & 3][0];\n'),
+               ('      if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[1][ks], bq[ks & 3], acc1, 0, 0, 0);\n', '      acc1[ks] += (float)bq[ks & 3][1];\n')],
+  'r_nostage': [NR, ('if (us < nit) stage(', 'if (us < 0) stage(')],
+  'r_noload': [NR, ('    load(r, tt + KP_AHEAD);\n  };', '  };')],
+  'r_nobarrier': [NR, ('    constexpr int GR = decltype(gc)::value, c = decltype(cc)::value;\n    __syncthreads();\n',
+                 '    constexpr int GR = decltype(gc)::value, c = decltype(cc)::value;\n')],
   'norounds': [('const int rnd = av ? (int)((unsigned int)dr >> 16) : 0xffff;', 'const int rnd = 0xffff;')],
   'noloop': [('for (int k = 1; k < U && __ballot', 'for (int k = 1; k < 1 && __ballot')],
   'nostage': [('if (us < nit) stage(', 'if (us < 0) stage(')],
