@@ -2474,12 +2474,17 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
         for (int q = 0; q < NQ; ++q) *(kb_f4*)(srow + 4 * qof(q)) = v[q] + r[q];
       }
     // labels (-1 for an undecided row: the list passes write it) and the
-    // unit's undecided-row mask; every store issued
+    // unit's undecided-row mask; every store issued.  Lanes j and j + 32
+    // write the same label to the same word, and all 64 lanes the same mask
+    // word: the dummy word takes only ghost rows / units (a few per block).
+    // (With the idle lanes of every store aimed at ONE dummy word, all CUs'
+    // stores met on one L2 line; the vmcnt waits that count those stores
+    // cost ~3.7 ms per cfg3 pass -- profiles/r04_kp_ablate_v4.txt.)
     const int dlab = av ? (int)(short)(dlv & 0xffff) : -1;
-    i64* la = h == 0 && rlive ? labels + grow : (i64*)dummy;
+    i64* la = rlive ? labels + grow : (i64*)dummy;
     *la = (i64)dlab;
     const unsigned long long m = __ballot(dlab < 0 && rlive) & 0xffffffffull;
-    unsigned long long* ma = lane == 0 && av ? und_mask + una : dummy + 1;
+    unsigned long long* ma = av ? und_mask + una : dummy + 1;
     *ma = m;
     load(r, tt + KP_AHEAD);
   };

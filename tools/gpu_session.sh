@@ -85,6 +85,20 @@ for s in $STEPS; do
         -d $O/kfs_a -o p --output-format csv -- python3 $R/tools/km_step_once.py 100000000 2 > $O/kfs_a.log 2>&1
       step kfs_b 120 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_VALU_MFMA_BUSY_CYCLES SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE \
         -d $O/kfs_b -o p --output-format csv -- python3 $R/tools/km_step_once.py 100000000 2 > $O/kfs_b.log 2>&1 ;;
+    kfsmem)
+      # vector-memory counters over the fused step: product build, then the
+      # coalesced-load ablation if built (tools/kp_ablate.sh coal)
+      cd /tmp
+      for v in product coal; do
+        lib=""; [ $v = coal ] && lib=$R/tools/bin/libspx_abl_coal.so
+        [ $v = coal ] && [ ! -f "$lib" ] && continue
+        step kfsmem_a_$v 120 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum \
+          TCP_PENDING_STALL_CYCLES_sum TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum GRBM_GUI_ACTIVE \
+          -d $O/kfsmem_a_$v -o p --output-format csv -- python3 $R/tools/km_step_once.py 100000000 2 step $lib > $O/kfsmem_a_$v.log 2>&1
+        step kfsmem_b_$v 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum \
+          TCP_TD_TCP_STALL_CYCLES_sum TD_TC_STALL_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE \
+          -d $O/kfsmem_b_$v -o p --output-format csv -- python3 $R/tools/km_step_once.py 100000000 2 step $lib > $O/kfsmem_b_$v.log 2>&1
+      done ;;
     kfslds)
       # LDS counters over the fused k-means step (bank conflicts vs all LDS-array cycles)
       cd /tmp
