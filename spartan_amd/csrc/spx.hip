@@ -2407,6 +2407,10 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
   // between them; then that unit's labels and undecided bits; then the loads
   // of unit t + 4 into the ring entry unit t - 4 leaves.
   auto matrix_role = [&](int tt, kb_f4 (&r)[NQ]) __attribute__((always_inline)) {
+    // the matrix role is the slot's critical path: its wave issues first when
+    // both waves of a SIMD are ready (-0.3 ms per cfg3 pass; the vector role
+    // first: +0.2 ms, profiles/r04_kp_ablate_v4.txt)
+    __builtin_amdgcn_s_setprio(1);
     const bool mf = tt < nit;
     const int ua = tt - KP_LAG;
     const bool av = ua >= 0 && ua < nit;
@@ -2487,6 +2491,7 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     unsigned long long* ma = av ? und_mask + una : dummy + 1;
     *ma = m;
     load(r, tt + KP_AHEAD);
+    __builtin_amdgcn_s_setprio(0);
   };
 
   // one slot of the unrolled body (compile-time copy c of KP_UNR, group GR)

@@ -23,6 +23,19 @@ subs = {
                ('      if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[1][ks], bq[ks & 3], acc1, 0, 0, 0);\n', '      acc1[ks] += (float)bq[ks & 3][1];\n')],
   'r_nostage': [NR, ('if (us < nit) stage(', 'if (us < 0) stage(')],
   'r_noload': [NR, ('    load(r, tt + KP_AHEAD);\n  };', '  };')],
+  # every load instruction reads whole 128-B row segments (8 lanes per row; wrong data, same bytes)
+  'coal': [('    const float* p = P + row * ldp + col0;\n#pragma unroll\n    for (int q = 0; q < NQ; ++q) r[q] = *(const kb_f4*)(p + 4 * qof(q));\n',
+            '    const float* p = P + (un * U + (lane >> 3)) * ldp + CPW * s + 4 * (lane & 7);\n#pragma unroll\n    for (int q = 0; q < NQ; ++q) r[q] = *(const kb_f4*)(p + 8 * q * ldp);\n')],
+  'r_coal': [NR, ('    const float* p = P + row * ldp + col0;\n#pragma unroll\n    for (int q = 0; q < NQ; ++q) r[q] = *(const kb_f4*)(p + 4 * qof(q));\n',
+            '    const float* p = P + (un * U + (lane >> 3)) * ldp + CPW * s + 4 * (lane & 7);\n#pragma unroll\n    for (int q = 0; q < NQ; ++q) r[q] = *(const kb_f4*)(p + 8 * q * ldp);\n')],
+  # wave priority by role (s_setprio 1 while in the role)
+  'prio_mat': [('  auto matrix_role = [&](int tt, kb_f4 (&r)[NQ]) __attribute__((always_inline)) {\n',
+                '  auto matrix_role = [&](int tt, kb_f4 (&r)[NQ]) __attribute__((always_inline)) {\n    __builtin_amdgcn_s_setprio(1);\n'),
+               ('    load(r, tt + KP_AHEAD);\n  };', '    load(r, tt + KP_AHEAD);\n    __builtin_amdgcn_s_setprio(0);\n  };')],
+  'prio_vec': [('  auto vector_role = [&](int tt, const kb_f4 (&rs)[NQ]) __attribute__((always_inline)) {\n',
+                '  auto vector_role = [&](int tt, const kb_f4 (&rs)[NQ]) __attribute__((always_inline)) {\n    __builtin_amdgcn_s_setprio(1);\n'),
+               ('    if (s == 0 && h == 0) dres[(u2 & 3) * U + j] = (d & 0xffff) | (rnd << 16);\n  };',
+                '    if (s == 0 && h == 0) dres[(u2 & 3) * U + j] = (d & 0xffff) | (rnd << 16);\n    __builtin_amdgcn_s_setprio(0);\n  };')],
   'r_nobarrier': [NR, ('    constexpr int GR = decltype(gc)::value, c = decltype(cc)::value;\n    __syncthreads();\n',
                  '    constexpr int GR = decltype(gc)::value, c = decltype(cc)::value;\n')],
   'norounds': [('const int rnd = av ? (int)((unsigned int)dr >> 16) : 0xffff;', 'const int rnd = 0xffff;')],
