@@ -36,6 +36,19 @@ subs = {
                 '  auto vector_role = [&](int tt, const kb_f4 (&rs)[NQ]) __attribute__((always_inline)) {\n    __builtin_amdgcn_s_setprio(1);\n'),
                ('    if (s == 0 && h == 0) dres[(u2 & 3) * U + j] = (d & 0xffff) | (rnd << 16);\n  };',
                 '    if (s == 0 && h == 0) dres[(u2 & 3) * U + j] = (d & 0xffff) | (rnd << 16);\n    __builtin_amdgcn_s_setprio(0);\n  };')],
+  # the staging of unit t + 1 first in the vector role (its LDS writes drain
+  # under the fold and the decision instead of in front of the barrier)
+  'stagefirst': [('    const kb_f4 p4 = *(const kb_f4*)(pr + 16 * h);\n',
+                  '    const kb_f4 p4 = *(const kb_f4*)(pr + 16 * h);\n    {\n      kb_f4 mu4s[NQ];\n      mu_load(mu4s);\n      if (us < nit) stage(rs, mu4s, us);\n    }\n'),
+                 ('    kb_f4 mu4[NQ];\n    mu_load(mu4);\n    const float fb1', '    const float fb1'),
+                 ('    if (us < nit) stage(rs, mu4, us);\n', '')],
+  'sf_dres': [('    const kb_f4 p4 = *(const kb_f4*)(pr + 16 * h);\n',
+                  '    const kb_f4 p4 = *(const kb_f4*)(pr + 16 * h);\n    {\n      kb_f4 mu4s[NQ];\n      mu_load(mu4s);\n      if (us < nit) stage(rs, mu4s, us);\n    }\n'),
+                 ('    kb_f4 mu4[NQ];\n    mu_load(mu4);\n    const float fb1', '    const float fb1'),
+                 ('    if (us < nit) stage(rs, mu4, us);\n', ''),
+                 ('    if (s == 0 && h == 0 && act) __hip_atomic_store(rcnt + d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);\n',
+                  '    if (s == 0 && h == 0 && act) __hip_atomic_store(rcnt + d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);\n    if (s == 0 && h == 0) dres[(u2 & 3) * U + j] = (d & 0xffff) | ((act ? (int)rk : 0xffff) << 16);\n'),
+                 ('    const int rnd = act ? (int)rk : 0xffff;  // add round (0xffff: no add)\n    if (s == 0 && h == 0) dres[(u2 & 3) * U + j] = (d & 0xffff) | (rnd << 16);\n', '')],
   'r_nobarrier': [NR, ('    constexpr int GR = decltype(gc)::value, c = decltype(cc)::value;\n    __syncthreads();\n',
                  '    constexpr int GR = decltype(gc)::value, c = decltype(cc)::value;\n')],
   'norounds': [('const int rnd = av ? (int)((unsigned int)dr >> 16) : 0xffff;', 'const int rnd = 0xffff;')],
