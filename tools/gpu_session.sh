@@ -58,6 +58,9 @@ for s in $STEPS; do
         cd /tmp && step $n 120 rocprofv3 --kernel-trace --stats -d $O/abl/$n -o p --output-format csv \
           -- python3 $R/tools/km_step_once.py 100000000 3 step $f > $O/$n.log 2>&1
       done ;;
+    kmcounts)
+      cd $R && step kmcounts 120 python3 tools/km_counts.py 100000000 > $O/kmcounts.txt 2>&1 && \
+        step kmcounts_first 120 python3 tools/km_counts.py 100000000 first >> $O/kmcounts.txt 2>&1 ;;
     kmtests)
       cd $R && step kmtests 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
         -p no:cacheprovider -k "kmeans" > $O/kmtests.log 2>&1 ;;
