@@ -190,12 +190,12 @@ int spx_kmeans_accumulate(int dtype, int64_t N, int64_t D, int64_t K, const void
  * kmeans_count_mapper / kmeans_center_mapper of one KMeans.fit iteration
  * (k_means_.py:126-136).  For fp32 points with K <= 256 and D in {64, 128}
  * the decided rows are labelled AND accumulated in one pass over the points
- * (k_kmeans_fs2); their sums run in fp32 per block and window of 256 64-row
+ * (k_kmeans_pp); their sums run in fp32 per block and window of 504 32-row
  * units -- one centre's chain is as long as that centre's rows in the window,
- * ~64 on average at K = 256 on uniform data and up to 16384 when one centre
+ * ~63 on average at K = 256 on uniform data and up to 16128 when one centre
  * takes every row (K = 1 or 2, skewed data) -- and the window sums are added
  * in fp64 in a fixed order.  The a-priori bound is that of an fp32 sum of
- * <= 16384 terms per window (<= 16384 u sum |x|, u = 2^-24); the reference's
+ * <= 16128 terms per window (<= 16128 u sum |x|, u = 2^-24); the reference's
  * own kmeans_center_mapper sums ALL of a centre's rows in one fp32 chain
  * (k_means_.py:67-89), so this is never looser than the reference.  Measured
  * within 1e-5 of sum |x| in every test, including the long-chain cases.
