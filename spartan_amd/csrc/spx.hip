@@ -2816,14 +2816,21 @@ __global__ __launch_bounds__(256) void k_kmeans_cand16(const float* __restrict__
           sq[j] = d0 * d0;
           sq[j + 1] = d1 * d1;
         }
+        // lane t's dims follow lane t - 1's: the running sum goes round the
+        // group by DPP row_newbcast (a VALU move; the ds_bpermute of __shfl put
+        // an LDS round trip into each of the chain's 16 steps: 0.52 -> 0.46 ms
+        // at cfg3; two candidates' chains interleaved measured slower)
         double acc = 0.0;
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
+        ks_unroll([&](auto tc) __attribute__((always_inline)) {
+          constexpr int t = decltype(tc)::value;
           double a = acc;
 #pragma unroll
           for (int j = 0; j < DPL; ++j) a = a + sq[j];
-          acc = __shfl(a, t, 16);  // lane t's dims follow lane t - 1's
-        }
+          const unsigned long long u = __builtin_bit_cast(unsigned long long, a);
+          const unsigned int lo = (unsigned int)__builtin_amdgcn_update_dpp(0, (int)(unsigned int)u, 0x150 + t, 0xF, 0xF, false);
+          const unsigned int hi = (unsigned int)__builtin_amdgcn_update_dpp(0, (int)(unsigned int)(u >> 32), 0x150 + t, 0xF, 0xF, false);
+          acc = __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+        }, std::make_integer_sequence<int, 16>{});
         double dist = sqrt(acc);
         if (r32) dist = (double)(float)dist;  // fp32-rounded distances: equal values tie, first index wins
         if (bi < 0 || dist < best || (dist == best && c < bi)) {

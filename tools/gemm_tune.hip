@@ -107,6 +107,15 @@ int main(int argc, char** argv) {
                157.3);
     return 0;
   }
+  if (which == "gfl2") {  // tile / grouping sweep of the GFL 512 form
+    run<float>(S, rounds,
+               {VG(float, 256, 128, 16, 4, 2, 8, 512), VG(float, 256, 128, 16, 4, 2, 4, 512),
+                VG(float, 256, 128, 16, 4, 2, 16, 512), VG(float, 128, 256, 16, 2, 4, 8, 512),
+                VG(float, 256, 256, 16, 4, 4, 8, 512), VG(float, 256, 128, 32, 4, 2, 8, 256),
+                VG(float, 128, 128, 16, 2, 2, 8, 512), VG(float, 256, 128, 16, 4, 2, 8, 1024)},
+               157.3);
+    return 0;
+  }
   if (which == "seg2") {  // two-level accumulation at <= 128 registers (32 x 64 / 64 x 32 wave tiles)
     run<float>(S, rounds,
                {V(float, 256, 128, 16, 4, 2, 8), VS(float, 256, 128, 16, 4, 2, 8, 16), VS(float, 128, 128, 16, 4, 2, 8, 16),

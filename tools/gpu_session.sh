@@ -44,6 +44,8 @@ for s in $STEPS; do
     dottests)
       cd $R && step dottests 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
         -p no:cacheprovider -k "dot or gemm" > $O/dottests.log 2>&1 ;;
+    gemmgfl2)
+      cd $R && step gemmgfl2 900 ./tools/bin/gemm_tune 32768 2 gfl2 > $O/gemmgfl2.txt 2>&1 ;;
     gemmgfl)
       cd $R && step gemmgfl 600 ./tools/bin/gemm_tune 32768 2 gfl > $O/gemmgfl.txt 2>&1 ;;
     kmdiag)
