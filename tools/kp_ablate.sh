@@ -49,6 +49,9 @@ subs = {
                  ('    if (s == 0 && h == 0 && act) __hip_atomic_store(rcnt + d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);\n',
                   '    if (s == 0 && h == 0 && act) __hip_atomic_store(rcnt + d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);\n    if (s == 0 && h == 0) dres[(u2 & 3) * U + j] = (d & 0xffff) | ((act ? (int)rk : 0xffff) << 16);\n'),
                  ('    const int rnd = act ? (int)rk : 0xffff;  // add round (0xffff: no add)\n    if (s == 0 && h == 0) dres[(u2 & 3) * U + j] = (d & 0xffff) | (rnd << 16);\n', '')],
+  # register-ring depth of the gathered accumulation (list mode in the step)
+  'ka4': [('constexpr int KA_STAGES = 3;', 'constexpr int KA_STAGES = 4;')],
+  'ka2': [('constexpr int KA_STAGES = 3;', 'constexpr int KA_STAGES = 2;')],
   'r_nobarrier': [NR, ('    constexpr int GR = decltype(gc)::value, c = decltype(cc)::value;\n    __syncthreads();\n',
                  '    constexpr int GR = decltype(gc)::value, c = decltype(cc)::value;\n')],
   'norounds': [('const int rnd = av ? (int)((unsigned int)dr >> 16) : 0xffff;', 'const int rnd = 0xffff;')],
