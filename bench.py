@@ -411,7 +411,7 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
   import torch
   from spartan_amd import workloads
   X = expr.rand(npts * ctx.world_size, D, dtype=np.float32, seed=21).force()
-  workloads.kmeans_fit(X, K, 1)          # warm-up + initial centres = first K points
+  workloads.kmeans_fit(X, K, iters)      # warm-up (every path of the timed loop) from the first K points
   sync()
   comm.barrier()
   t0 = time.perf_counter()

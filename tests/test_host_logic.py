@@ -155,6 +155,27 @@ def test_kmeans_driver_host(host_ctx):
     np.testing.assert_array_equal(labels.glom(), l2)
 
 
+def test_kmeans_driver_empty_cluster_host(host_ctx):
+  """kmeans_fit launches iteration i + 1 with device-divided centres before it
+  reads iteration i's counts; an empty cluster (here a centre far from every
+  point in iteration 0, and reseeds that stay empty) makes it relaunch the
+  iteration with the host rule's reseeded centres -- the results must be the
+  sequential loop's (the oracle's), centres and labels."""
+  from oracle import workloads as OW
+  for W in (1, 2):
+    host_ctx(W)
+    from spartan_amd import expr, workloads
+    pts = rng.rand((400, 6), 23, np.float32)
+    c0 = np.vstack([pts[:3].astype(np.float64), np.full((1, 6), 50.0), pts[3:4].astype(np.float64)])
+    info = {}
+    c, labels = workloads.kmeans_fit(expr.from_numpy(pts), 5, 4, centers=c0, info=info)
+    c2, l2 = OW.kmeans_fit(pts, 5, 4, W, centers=c0)
+    np.testing.assert_allclose(c, c2, rtol=1e-6)
+    np.testing.assert_array_equal(labels.glom(), l2)
+    _, l3 = OW.kmeans_fit(pts, 5, 1, W, centers=info['assign_centers'])
+    np.testing.assert_array_equal(labels.glom(), l3)
+
+
 def test_dot_reduce_fusion_rewrites_lreg(host_ctx):
   """DotReduceFusion folds dot(x, w_host) into the axis-0 reduction of
   x * (dot(x, w) - y): one ReduceExpr, no DotExpr left, same gradient."""

@@ -63,6 +63,8 @@ for s in $STEPS; do
     kmcounts)
       cd $R && step kmcounts 120 python3 tools/km_counts.py 100000000 > $O/kmcounts.txt 2>&1 && \
         step kmcounts_first 120 python3 tools/km_counts.py 100000000 first >> $O/kmcounts.txt 2>&1 ;;
+    kmfit)
+      cd $R && step kmfit 240 python3 tools/km_fit_timing.py 100000000 2 $KMFIT_OLD > $O/kmfit.txt 2>&1 ;;
     kmtests)
       cd $R && step kmtests 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
         -p no:cacheprovider -k "kmeans" > $O/kmtests.log 2>&1 ;;
