@@ -2005,7 +2005,10 @@ __global__ __launch_bounds__(256) void k_ks_compact(i64 N, const unsigned long l
                                                     const i64* __restrict__ rows_in,
                                                     const unsigned int* __restrict__ nrows_in, i64* __restrict__ out,
                                                     unsigned int* __restrict__ cnt,
-                                                    const unsigned int* __restrict__ base_in = nullptr) {
+                                                    const unsigned int* __restrict__ base_in = nullptr,
+                                                    const i64* __restrict__ vals_in = nullptr,
+                                                    i64* __restrict__ vals_out = nullptr) {
+  // vals_in / vals_out (optional): vals_out[pos] = vals_in[slot] beside the list
   __shared__ unsigned int wsum[4];
   __shared__ unsigned int base;
   const i64 nlim = rows_in ? (i64)*nrows_in : N;
@@ -2047,6 +2050,7 @@ __global__ __launch_bounds__(256) void k_ks_compact(i64 N, const unsigned long l
       } else {  // point order (k_kmeans_pp)
         slot = tl * 32 + l;
       }
+      if (vals_out) vals_out[pos] = vals_in[slot];
       out[pos++] = rows_in ? rows_in[slot] : slot;
     }
   }
@@ -2339,8 +2343,14 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     int il0 = 0, il1 = 0;
     if (fv && scr0) fold16(acc0, 2 * s, lo0, sec0, il0);
     __builtin_amdgcn_sched_barrier(0);
-    // (3) decide: top-2 over the 4 waves' candidates, the certified rule
-    int d;
+    // (3) decide: top-2 over the 4 waves' candidates, the certified rule.
+    // d: the centre the row is added to -- its label when decided, and,
+    // PROVISIONALLY, the screen's best for a finite undecided row (the list
+    // passes settle its label; the few whose label then differs are moved
+    // by a correction pass, spx_kmeans_step).  dl: the label code stored
+    // for the row: the label, -2 - d (provisional) or -1 (not added:
+    // non-finite, or a ghost row).
+    int d, dl;
     {
       const float b1 = ks_max(e4[0], e4[2]), b2 = ks_med3(e4[0], e4[2], ks_max(e4[1], e4[3]));
       const int ib = e4[0] >= e4[2] ? i2[0] : i2[1];
@@ -2357,7 +2367,9 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
       const float e = __builtin_fmaf(__builtin_fmaf(kq[2], pn, kq[1]), pn, kq[0]) * 1.0001f;
       const bool fin = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim && isfinite(B1) && isfinite(B2);
       const bool dec = fin && B1 - B2 > 1.0001f * e;
-      d = rlive && dec ? IB : -1;
+      const bool add = rlive && fin && IB < (int)K;
+      d = add ? IB : -1;
+      dl = !add ? -1 : dec ? IB : -2 - IB;
     }
     // (4) each decided row's rank among the unit's rows of its centre (its
     // add round): one LDS atomic increment per row on wave 0's counter table
@@ -2399,7 +2411,7 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     // (6) stage of unit t + 1
     if (us < nit) stage(rs, mu4, us);
     const int rnd = act ? (int)rk : 0xffff;  // add round (0xffff: no add)
-    if (s == 0 && h == 0) dres[(u2 & 3) * U + j] = (d & 0xffff) | (rnd << 16);
+    if (s == 0 && h == 0) dres[(u2 & 3) * U + j] = (dl & 0xffff) | (rnd << 16);
   };
 
   // matrix role of slot t: the MFMAs of unit t (if t < nit), with the add
@@ -2436,7 +2448,8 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
       acc0 = (kb_acc){};
       acc1 = (kb_acc){};
     }
-    const int d = av ? (int)(short)(dr & 0xffff) : -1;
+    const int dcode = av ? (int)(short)(dr & 0xffff) : -1;
+    const int d = dcode >= 0 ? dcode : dcode <= -2 ? -2 - dcode : -1;  // the centre the row is added to
     const int rnd = av ? (int)((unsigned int)dr >> 16) : 0xffff;
     float* const srow = sums + (d >= 0 ? d : 0) * D + col0;
     // round 0's reads go out before the last MFMAs (the sums rows are
@@ -2914,7 +2927,9 @@ __global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(4 * 
                                                              const i64* __restrict__ labels, double* __restrict__ psum,
                                                              unsigned long long* __restrict__ pcnt, int ndb,
                                                              const i64* __restrict__ rows = nullptr,
-                                                             const unsigned int* __restrict__ nrows = nullptr) {
+                                                             const unsigned int* __restrict__ nrows = nullptr,
+                                                             const i64* __restrict__ lab_list = nullptr) {
+  // lab_list (with a row list): entry i's label is lab_list[i], not labels[row]
   if (rows) N = (i64)*nrows;
   constexpr int VE = 16 / (int)sizeof(TP);                // elements per 16-byte load
   constexpr int CH = KA_THREADS * VE / KA_DB;             // points per chunk (64 f32 / 32 f64)
@@ -2969,7 +2984,8 @@ __global__ __launch_bounds__(KA_THREADS) __attribute__((amdgpu_waves_per_eu(4 * 
         pf[s][j] = P[pr * ldp + d];
       }
     }
-    if (t < CH) plab[s] = labels[rows ? lidx[s] : (p0 + t < N ? p0 + t : N - 1)];
+    if (t < CH)
+      plab[s] = lab_list ? lab_list[p0 + t < N ? p0 + t : N - 1] : labels[rows ? lidx[s] : (p0 + t < N ? p0 + t : N - 1)];
     if (rows) load_idx(s, ch + ST * G);
   };
 #pragma unroll
@@ -3056,12 +3072,20 @@ __global__ __launch_bounds__(256) void k_kmeans_reduce(i64 n, i64 G, const P* __
   red[sl][j] = s;
   __syncthreads();
   if (sl == 0 && i < n) {
-    T v = add ? out[i] : T(0);
-    v += red[0][j];
-    v += red[1][j];
-    v += red[2][j];
-    v += red[3][j];
-    out[i] = v;
+    if (add == 2) {  // out -= the sum (the provisional adds' correction)
+      T q = red[0][j];
+      q += red[1][j];
+      q += red[2][j];
+      q += red[3][j];
+      out[i] = out[i] - q;
+    } else {
+      T v = add ? out[i] : T(0);
+      v += red[0][j];
+      v += red[1][j];
+      v += red[2][j];
+      v += red[3][j];
+      out[i] = v;
+    }
   }
 }
 
@@ -3355,6 +3379,37 @@ extern "C" int spx_kmeans_accumulate(int dtype, int64_t N, int64_t D, int64_t K,
   return SPX_OK;
 }
 
+// The provisional adds' correction (spx_kmeans_step): list slot i (row
+// scr[i], label code prov[i] from k_kmeans_pp, final label labels[row] from
+// the list passes) needs an add under its final label when it was not added
+// (code -1) or was added under another centre, and then a subtraction under
+// that centre (pv[i]).  LAYOUT 2 masks over the list slots: bit l of word w
+// <-> slot 32 w + l.  Words past the list are left as they are (zeroed).
+__global__ __launch_bounds__(256) void k_km_movers(const i64* __restrict__ scr, const unsigned int* __restrict__ nlist,
+                                                    const i64* __restrict__ prov, const i64* __restrict__ labels,
+                                                    unsigned long long* __restrict__ add_mask,
+                                                    unsigned long long* __restrict__ sub_mask, i64* __restrict__ pv) {
+  const i64 n = *nlist;
+  const i64 nr = (n + 63) / 64 * 64;
+  const int lane = threadIdx.x & 63;
+  for (i64 i = (i64)blockIdx.x * 256 + threadIdx.x; i < nr; i += (i64)gridDim.x * 256) {  // wave-uniform bounds
+    bool ad = false, sb = false;
+    if (i < n) {
+      const i64 code = prov[i], f = labels[scr[i]];
+      const i64 p = code <= -2 ? -2 - code : -1;
+      sb = p >= 0 && f != p;
+      ad = code == -1 || sb;
+      pv[i] = p;
+    }
+    const unsigned long long ma = __ballot(ad), ms = __ballot(sb);
+    if (lane == 0 || lane == 32) {
+      const i64 wd = i / 32;  // i = 64 b + lane: words 2 b and 2 b + 1
+      add_mask[wd] = lane == 0 ? (ma & 0xffffffffull) : (ma >> 32);
+      sub_mask[wd] = lane == 0 ? (ms & 0xffffffffull) : (ms >> 32);
+    }
+  }
+}
+
 // ------------------------------------------------------- fused k-means step
 // spx_kmeans_step = spx_kmeans_assign + spx_kmeans_accumulate with the same
 // results (labels bit for bit; counts exact; sums deterministic, within the
@@ -3388,8 +3443,9 @@ extern "C" int64_t spx_kmeans_step_workspace(int dtype, int64_t N, int64_t D, in
   const int64_t c = spx_kmeans_accumulate_workspace(dtype, N, D, K);
   if (a < 0 || c < 0) return -1;
   const i64 G = kfs_grid(N);
+  // ... | slice sums | provisional label codes of the list (N i64) + 2 counters
   return (a + 255) / 256 * 256 + (c + 255) / 256 * 256 + kfs_part_bytes(N, D, K) + G * K * 8 + (kfs_nblk(N) + 1) * 4 + 512 +
-         (int64_t)KR_S * K * D * 8;
+         (int64_t)KR_S * K * D * 8 + 256 + N * 8 + 64;
 }
 
 extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
@@ -3438,25 +3494,54 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
   // the screen's undecided rows, in row order (the gathered accumulation's order)
   k_ks_count<16><<<(unsigned)nb, 256, 0, S(stream)>>>(N, w.und_mask, bcnt);
   k_exscan_u32<<<1, 1024, 0, S(stream)>>>(bcnt, nb, w.counters + 3);
-  k_ks_compact<16, 2><<<(unsigned)nb, 256, 0, S(stream)>>>(N, w.und_mask, nullptr, nullptr, w.scr_list, nullptr, bcnt);
+  // the slice sums live past the compaction counts and the dummy word, the
+  // list's provisional label codes and two list counters past them
+  const i64 n = K * D;
+  double* slices = (double*)(((uintptr_t)(bcnt + nb + 1) + 64 + 255) & ~(uintptr_t)255);
+  i64* prov = (i64*)(((uintptr_t)(slices + (i64)KR_S * n) + 255) & ~(uintptr_t)255);
+  unsigned int* mcnt = (unsigned int*)(prov + N);
+  // the list, with each row's label code from k_kmeans_pp beside it
+  k_ks_compact<16, 2><<<(unsigned)nb, 256, 0, S(stream)>>>(N, w.und_mask, nullptr, nullptr, w.scr_list, nullptr, bcnt,
+                                                            labels, prov);
   LAUNCH_CHECK("spx_kmeans_step(compact)");
   (void)ntiles;
   int rc = km_resolve(S(stream), N, D, K, Pf, ldp, centers, labels, w, nct, r32);
   if (rc) return rc;
-  // the undecided rows' sums and counts, gathered through the row list
-  // (an LDS-sum form of this pass, the fused kernel's adds over gathered 64-row
-  // units, measured 1.18-2.27 ms against this kernel's 1.1 ms: not kept)
+  // The list rows' sums and counts: k_kmeans_pp added every finite undecided
+  // row provisionally under its screen-best centre; now that the labels are
+  // final, the rows it did not add (non-finite) and the ones whose label
+  // moved are added under the final label, and the movers subtracted from
+  // the provisional centre -- two gathered passes over the movers instead of
+  // one over the whole list (6.2 % of cfg3's rows; ~0.6 % move).  Lists in
+  // slot order (count, scan, compact), partials combined in a fixed order.
   i64 G2, ndb, ncb;
   ka_grid(dtype, N, D, K, &G2, &ndb, &ncb);
   if (ndb * ncb > 65535) return set_err(SPX_ENOTSUP, "spx_kmeans_step: K*D too large");
   double* psum2 = (double*)wc;
   unsigned long long* pcnt2 = (unsigned long long*)(psum2 + G2 * K * D);
+  const i64 nw = (N + 31) / 32 + 2;
+  i64* pv = (i64*)w.cand_list;  // the list passes are done with the candidate list
+  unsigned long long* add_mask = (unsigned long long*)(pv + N);
+  unsigned long long* sub_mask = add_mask + nw;
+  i64* subp = (i64*)(sub_mask + nw);
+  HIP_TRY(hipMemsetAsync(add_mask, 0, (size_t)2 * nw * 8, S(stream)));
+  {
+    const i64 g = (N + 255) / 256;
+    k_km_movers<<<(unsigned)(g < 2048 ? (g < 1 ? 1 : g) : 2048), 256, 0, S(stream)>>>(w.scr_list, w.counters + 3, prov,
+                                                                                     labels, add_mask, sub_mask, pv);
+  }
+  LAUNCH_CHECK("spx_kmeans_step(movers)");
+  auto listed = [&](const unsigned long long* mask, i64* out, unsigned int* cnt, const i64* vin, i64* vout) {
+    k_ks_count<16><<<(unsigned)nb, 256, 0, S(stream)>>>(N, mask, bcnt);
+    k_exscan_u32<<<1, 1024, 0, S(stream)>>>(bcnt, nb, cnt);
+    k_ks_compact<16, 2><<<(unsigned)nb, 256, 0, S(stream)>>>(N, mask, w.scr_list, w.counters + 3, out, nullptr, bcnt,
+                                                              vin, vout);
+  };
+  listed(add_mask, w.und_list, mcnt, nullptr, nullptr);
+  LAUNCH_CHECK("spx_kmeans_step(compact adds)");
   k_kmeans_accum<float><<<dim3((unsigned)G2, (unsigned)(ndb * ncb)), KA_THREADS, 0, S(stream)>>>(
-      N, D, K, Pf, ldp, labels, psum2, pcnt2, (int)ndb, w.scr_list, w.counters + 3);
-  LAUNCH_CHECK("spx_kmeans_step(accumulate undecided rows)");
-  const i64 n = K * D;
-  // the slice sums live past the compaction counts and the dummy word
-  double* slices = (double*)(((uintptr_t)(bcnt + nb + 1) + 64 + 255) & ~(uintptr_t)255);
+      N, D, K, Pf, ldp, labels, psum2, pcnt2, (int)ndb, w.und_list, mcnt);
+  LAUNCH_CHECK("spx_kmeans_step(accumulate list adds)");
   if (n % 4 == 0) {
     k_kmeans_slices<<<dim3((unsigned)((n / 4 + 255) / 256), KR_S), 256, 0, S(stream)>>>(n, G * nwin, partF, slices);
     k_kmeans_reduce<double><<<(unsigned)((n + 63) / 64), 256, 0, S(stream)>>>(n, KR_S, slices, sums,
@@ -3471,6 +3556,17 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
   k_kmeans_reduce<unsigned long long><<<(unsigned)((K + 63) / 64), 256, 0, S(stream)>>>(
       K, G2, pcnt2, (unsigned long long*)counts, 1);
   LAUNCH_CHECK("spx_kmeans_step(reduce)");
+  // the movers out of their provisional centres (the same partial buffers,
+  // reused after the adds' reduce)
+  listed(sub_mask, w.full_list, mcnt + 1, pv, subp);
+  LAUNCH_CHECK("spx_kmeans_step(compact subtractions)");
+  k_kmeans_accum<float><<<dim3((unsigned)G2, (unsigned)(ndb * ncb)), KA_THREADS, 0, S(stream)>>>(
+      N, D, K, Pf, ldp, labels, psum2, pcnt2, (int)ndb, w.full_list, mcnt + 1, subp);
+  LAUNCH_CHECK("spx_kmeans_step(accumulate list subtractions)");
+  k_kmeans_reduce<double><<<(unsigned)((n + 63) / 64), 256, 0, S(stream)>>>(n, G2, psum2, sums, 2);
+  k_kmeans_reduce<unsigned long long><<<(unsigned)((K + 63) / 64), 256, 0, S(stream)>>>(
+      K, G2, pcnt2, (unsigned long long*)counts, 2);
+  LAUNCH_CHECK("spx_kmeans_step(reduce subtractions)");
   return SPX_OK;
 }
 
