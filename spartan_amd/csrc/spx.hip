@@ -715,6 +715,38 @@ extern "C" int spx_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* 
 }
 
 // ================================================================ k-means
+// The provisional adds' bookkeeping of spx_kmeans_step (k_kmeans_pp added
+// every finite undecided row under its screen-best centre p and left the
+// label code -2 - p, or -1 for a row it did not add): when a list pass
+// writes such a row's final label it sets the row's bit in `add` if the row
+// must be added under that label (not added, or added under another centre)
+// and in `sub`, with pside[row] = p, if it must come out of p.  The struct
+// sits in the workspace at counters + 4, null outside the step.
+struct KmMove {
+  unsigned long long* add;
+  unsigned long long* sub;
+  i64* pside;
+};
+__device__ __forceinline__ void km_label(i64* labels, const unsigned int* counters, i64 row, i64 lab) {
+  const KmMove* mv = (const KmMove*)(counters + 4);
+  unsigned long long* const add = mv->add;
+  if (add) {
+    const i64 code = labels[row];
+    const i64 p = code <= -2 ? -2 - code : -1;
+    const bool sb = p >= 0 && p != lab;
+    const unsigned long long bit = 1ull << (row & 31);
+    if (code == -1 || sb) atomicOr(add + (row >> 5), bit);
+    if (sb) {
+      atomicOr(mv->sub + (row >> 5), bit);
+      mv->pside[row] = p;
+    }
+  }
+  labels[row] = lab;
+}
+__global__ void k_km_setmove(KmMove* dst, unsigned long long* add, unsigned long long* sub, i64* pside) {
+  if (threadIdx.x == 0) *dst = KmMove{add, sub, pside};
+}
+
 // Assignment: labels[p] = argmin_c ||P[p] - C[c]||_2 in exactly the order of
 // scipy.spatial.distance.cdist (k_means_.py:58 via kmeans_dist_mapper): fp64,
 // s = sum_d (x_d - c_d)^2 accumulated sequentially over d with separately
@@ -783,7 +815,8 @@ __global__ __launch_bounds__(256) void k_kmeans_assign(i64 N, i64 D, i64 K, cons
     }
   }
   if (valid) {
-    labels[p] = bi;
+    if (rows) km_label(labels, nrows, p, bi);  // list mode: nrows is the workspace's counters
+    else labels[p] = bi;
     if (mind) mind[p] = best;
   }
   }
@@ -1453,7 +1486,7 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
     const bool fin = isfinite(p2f) && isfinite(e) && pn * cmax < 1e36 && cmax * cmax < 1e36 &&
                      mun * cmax < 1e36 && isfinite(b1) && isfinite(b2);
     const bool dec = fin && (double)b2 - (double)b1 > 2.0 * e;
-    if (live && dec) labels[grow] = i1;
+    if (live && dec) km_label(labels, counters, grow, i1);
     if (live && !fin) full_list[atomicAdd(&counters[0], 1u)] = grow;
     // undecided rows: one slot each (one atomic per wave), then per register
     // q holding such a row, the masks of the centres with a' <= b1 + 2e by
@@ -1976,7 +2009,7 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
     const bool fin = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim && isfinite(b1) && isfinite(b2);
     // acc = -a'/2: a' gap > 2e  <=>  acc gap b1 - b2 > e
     const bool dec = fin && b1 - b2 > 1.0001f * e;
-    if (live && dec) labels[grow] = i1;
+    if (live && dec) km_label(labels, counters, grow, i1);
     if (MODE == 0 && live && !fin) full_list[atomicAdd(&counters[0], 1u)] = grow;
     const bool needc = live && !dec && (MODE == 1 || fin);
     // the tile's undecided rows as one lane mask, compacted into a row list
@@ -2779,7 +2812,7 @@ __global__ __launch_bounds__(256) void k_kmeans_cand(i64 D, const TP* __restrict
         bi = oi;
       }
     }
-    if (sub == 0) labels[row] = bi;
+    if (sub == 0) km_label(labels, counters, row, bi);
   }
 }
 
@@ -2852,7 +2885,7 @@ __global__ __launch_bounds__(256) void k_kmeans_cand16(const float* __restrict__
         }
       }
     }
-    if (s == 0) labels[row] = bi;
+    if (s == 0) km_label(labels, counters, row, bi);
   }
 }
 
@@ -3142,7 +3175,7 @@ extern "C" int64_t spx_kmeans_assign_workspace(int dtype, int64_t N, int64_t D, 
   // CT (D x Kp f32) | cn (Kp f64) | cmax | counters | full list (N i64) | candidate list (N KfCand, K <= 256)
   // | undecided-row list (N i64, K <= 256) | screen's undecided-row list (N i64, K <= 256)
   // | per-tile undecided lane masks (ceil(N / 32) u64, K <= 256) | centre mean (D f32, K <= 256)
-  return (D * Kp * 4 + 15) / 16 * 16 + Kp * 8 + 32 + 16 + N * 8 +
+  return (D * Kp * 4 + 15) / 16 * 16 + Kp * 8 + 32 + 64 + N * 8 +
          (Kp == KF_BN ? N * (i64)sizeof(KfCand) + 2 * N * 8 + (N + 31) / 32 * 8 + D * 4 : 0);
 }
 
@@ -3174,8 +3207,8 @@ static KmWs km_carve(void* workspace, i64 N, i64 D, i64 Kp) {
   ws += Kp * 8;
   w.cmax = (double*)ws;
   ws += 32;
-  w.counters = (unsigned int*)ws;
-  ws += 16;
+  w.counters = (unsigned int*)ws;  // 4 counters, then a KmMove at counters + 4
+  ws += 64;
   w.full_list = (i64*)ws;
   ws += N * 8;
   w.cand_list = (KfCand*)ws;
@@ -3274,7 +3307,7 @@ extern "C" int spx_kmeans_assign(int dtype, int64_t N, int64_t D, int64_t K, con
     return set_err(SPX_EINVAL, "spx_kmeans_assign: workspace %zu < %lld bytes", workspace_bytes, (long long)need);
   const i64 Kp = kf_kp(K);
   const KmWs w = km_carve(workspace, N, D, Kp);
-  HIP_TRY(hipMemsetAsync(w.counters, 0, 4 * sizeof(unsigned int), S(stream)));
+  HIP_TRY(hipMemsetAsync(w.counters, 0, 64, S(stream)));  // the counters and a null KmMove
   const int gp = kf_persistent_grid(N);
   if (km_screen_ok(dtype, K, D, points, ldp)) {
     // fp16 screen (A-stationary, k_kmeans_filter_as MODE 1) over every row,
@@ -3379,37 +3412,6 @@ extern "C" int spx_kmeans_accumulate(int dtype, int64_t N, int64_t D, int64_t K,
   return SPX_OK;
 }
 
-// The provisional adds' correction (spx_kmeans_step): list slot i (row
-// scr[i], label code prov[i] from k_kmeans_pp, final label labels[row] from
-// the list passes) needs an add under its final label when it was not added
-// (code -1) or was added under another centre, and then a subtraction under
-// that centre (pv[i]).  LAYOUT 2 masks over the list slots: bit l of word w
-// <-> slot 32 w + l.  Words past the list are left as they are (zeroed).
-__global__ __launch_bounds__(256) void k_km_movers(const i64* __restrict__ scr, const unsigned int* __restrict__ nlist,
-                                                    const i64* __restrict__ prov, const i64* __restrict__ labels,
-                                                    unsigned long long* __restrict__ add_mask,
-                                                    unsigned long long* __restrict__ sub_mask, i64* __restrict__ pv) {
-  const i64 n = *nlist;
-  const i64 nr = (n + 63) / 64 * 64;
-  const int lane = threadIdx.x & 63;
-  for (i64 i = (i64)blockIdx.x * 256 + threadIdx.x; i < nr; i += (i64)gridDim.x * 256) {  // wave-uniform bounds
-    bool ad = false, sb = false;
-    if (i < n) {
-      const i64 code = prov[i], f = labels[scr[i]];
-      const i64 p = code <= -2 ? -2 - code : -1;
-      sb = p >= 0 && f != p;
-      ad = code == -1 || sb;
-      pv[i] = p;
-    }
-    const unsigned long long ma = __ballot(ad), ms = __ballot(sb);
-    if (lane == 0 || lane == 32) {
-      const i64 wd = i / 32;  // i = 64 b + lane: words 2 b and 2 b + 1
-      add_mask[wd] = lane == 0 ? (ma & 0xffffffffull) : (ma >> 32);
-      sub_mask[wd] = lane == 0 ? (ms & 0xffffffffull) : (ms >> 32);
-    }
-  }
-}
-
 // ------------------------------------------------------- fused k-means step
 // spx_kmeans_step = spx_kmeans_assign + spx_kmeans_accumulate with the same
 // results (labels bit for bit; counts exact; sums deterministic, within the
@@ -3426,7 +3428,12 @@ static i64 kfs_grid(i64 N) {  // one block per CU, at most one per 32-row unit
   return nunits < ncu ? (nunits < 1 ? 1 : nunits) : ncu;
 }
 
-static i64 kfs_nblk(i64 N) { return ((N + 31) / 32 + 256 * 16 - 1) / (256 * 16); }
+// the step's mask compactions: one 32-row mask word per thread (KFS_TPT), so
+// the gathers beside the list (label codes, k_ks_compact vals) have one or two
+// rows per thread in flight, not a thread's 16 words' worth in a row (234 us
+// for the list's codes at cfg3 with 16)
+constexpr int KFS_TPT = 1;
+static i64 kfs_nblk(i64 N) { return ((N + 31) / 32 + 256 * KFS_TPT - 1) / (256 * KFS_TPT); }
 
 // windows of k_kmeans_pp's fp32 partials per block (the block with the most units)
 static i64 kp_nwin(i64 N) {
@@ -3443,9 +3450,10 @@ extern "C" int64_t spx_kmeans_step_workspace(int dtype, int64_t N, int64_t D, in
   const int64_t c = spx_kmeans_accumulate_workspace(dtype, N, D, K);
   if (a < 0 || c < 0) return -1;
   const i64 G = kfs_grid(N);
-  // ... | slice sums | provisional label codes of the list (N i64) + 2 counters
+  // ... | slice sums | the moved rows' provisional centres (N i64) | 2 row
+  // masks ((N / 32 + 2) u64 each) | 2 list counters
   return (a + 255) / 256 * 256 + (c + 255) / 256 * 256 + kfs_part_bytes(N, D, K) + G * K * 8 + (kfs_nblk(N) + 1) * 4 + 512 +
-         (int64_t)KR_S * K * D * 8 + 256 + N * 8 + 64;
+         (int64_t)KR_S * K * D * 8 + 256 + N * 8 + 2 * ((N + 31) / 32 + 2) * 8 + 64;
 }
 
 extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
@@ -3483,7 +3491,7 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
   __bf16* CBl = CBh + (i64)32 * nct * D;
   float* cnf = (float*)w.cn;
   float* cnf2 = cnf + KF_BN;
-  HIP_TRY(hipMemsetAsync(w.counters, 0, 4 * sizeof(unsigned int), S(stream)));
+  HIP_TRY(hipMemsetAsync(w.counters, 0, 64, S(stream)));  // the counters and a null KmMove
   k_kmeans_prep_b3<<<1, 1024, 0, S(stream)>>>(D, K, 32 * nct, centers, CBh, CBl, cnf, w.cmax, mcoef, cnf2, w.muf);
   LAUNCH_CHECK("spx_kmeans_step(prep)");
   unsigned long long* dummy = (unsigned long long*)(((uintptr_t)(bcnt + nb + 1) + 63) & ~(uintptr_t)63);
@@ -3492,19 +3500,26 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
                w.und_mask, partF, (int)nwin, pcntF, dummy);
   LAUNCH_CHECK("spx_kmeans_step(fused screen + accumulate)");
   // the screen's undecided rows, in row order (the gathered accumulation's order)
-  k_ks_count<16><<<(unsigned)nb, 256, 0, S(stream)>>>(N, w.und_mask, bcnt);
+  k_ks_count<KFS_TPT><<<(unsigned)nb, 256, 0, S(stream)>>>(N, w.und_mask, bcnt);
   k_exscan_u32<<<1, 1024, 0, S(stream)>>>(bcnt, nb, w.counters + 3);
-  // the slice sums live past the compaction counts and the dummy word, the
-  // list's provisional label codes and two list counters past them
+  // the slice sums live past the compaction counts and the dummy word; the
+  // moved rows' provisional centres, the two row masks and two list counters
+  // past them
   const i64 n = K * D;
   double* slices = (double*)(((uintptr_t)(bcnt + nb + 1) + 64 + 255) & ~(uintptr_t)255);
-  i64* prov = (i64*)(((uintptr_t)(slices + (i64)KR_S * n) + 255) & ~(uintptr_t)255);
-  unsigned int* mcnt = (unsigned int*)(prov + N);
-  // the list, with each row's label code from k_kmeans_pp beside it
-  k_ks_compact<16, 2><<<(unsigned)nb, 256, 0, S(stream)>>>(N, w.und_mask, nullptr, nullptr, w.scr_list, nullptr, bcnt,
-                                                            labels, prov);
+  i64* pside = (i64*)(((uintptr_t)(slices + (i64)KR_S * n) + 255) & ~(uintptr_t)255);
+  const i64 nw = (N + 31) / 32 + 2;
+  unsigned long long* add_rows = (unsigned long long*)(pside + N);
+  unsigned long long* sub_rows = add_rows + nw;
+  unsigned int* mcnt = (unsigned int*)(sub_rows + nw);
+  k_ks_compact<KFS_TPT, 2><<<(unsigned)nb, 256, 0, S(stream)>>>(N, w.und_mask, nullptr, nullptr, w.scr_list, nullptr, bcnt);
   LAUNCH_CHECK("spx_kmeans_step(compact)");
   (void)ntiles;
+  // the list passes mark, as they write final labels, the rows to add
+  // under them and the rows to take out of their provisional centre
+  HIP_TRY(hipMemsetAsync(add_rows, 0, (size_t)2 * nw * 8, S(stream)));
+  k_km_setmove<<<1, 64, 0, S(stream)>>>((KmMove*)(w.counters + 4), add_rows, sub_rows, pside);
+  LAUNCH_CHECK("spx_kmeans_step(move bookkeeping)");
   int rc = km_resolve(S(stream), N, D, K, Pf, ldp, centers, labels, w, nct, r32);
   if (rc) return rc;
   // The list rows' sums and counts: k_kmeans_pp added every finite undecided
@@ -3519,25 +3534,12 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
   if (ndb * ncb > 65535) return set_err(SPX_ENOTSUP, "spx_kmeans_step: K*D too large");
   double* psum2 = (double*)wc;
   unsigned long long* pcnt2 = (unsigned long long*)(psum2 + G2 * K * D);
-  const i64 nw = (N + 31) / 32 + 2;
-  i64* pv = (i64*)w.cand_list;  // the list passes are done with the candidate list
-  unsigned long long* add_mask = (unsigned long long*)(pv + N);
-  unsigned long long* sub_mask = add_mask + nw;
-  i64* subp = (i64*)(sub_mask + nw);
-  HIP_TRY(hipMemsetAsync(add_mask, 0, (size_t)2 * nw * 8, S(stream)));
-  {
-    const i64 g = (N + 255) / 256;
-    k_km_movers<<<(unsigned)(g < 2048 ? (g < 1 ? 1 : g) : 2048), 256, 0, S(stream)>>>(w.scr_list, w.counters + 3, prov,
-                                                                                     labels, add_mask, sub_mask, pv);
-  }
-  LAUNCH_CHECK("spx_kmeans_step(movers)");
   auto listed = [&](const unsigned long long* mask, i64* out, unsigned int* cnt, const i64* vin, i64* vout) {
-    k_ks_count<16><<<(unsigned)nb, 256, 0, S(stream)>>>(N, mask, bcnt);
+    k_ks_count<KFS_TPT><<<(unsigned)nb, 256, 0, S(stream)>>>(N, mask, bcnt);
     k_exscan_u32<<<1, 1024, 0, S(stream)>>>(bcnt, nb, cnt);
-    k_ks_compact<16, 2><<<(unsigned)nb, 256, 0, S(stream)>>>(N, mask, w.scr_list, w.counters + 3, out, nullptr, bcnt,
-                                                              vin, vout);
+    k_ks_compact<KFS_TPT, 2><<<(unsigned)nb, 256, 0, S(stream)>>>(N, mask, nullptr, nullptr, out, nullptr, bcnt, vin, vout);
   };
-  listed(add_mask, w.und_list, mcnt, nullptr, nullptr);
+  listed(add_rows, w.und_list, mcnt, nullptr, nullptr);
   LAUNCH_CHECK("spx_kmeans_step(compact adds)");
   k_kmeans_accum<float><<<dim3((unsigned)G2, (unsigned)(ndb * ncb)), KA_THREADS, 0, S(stream)>>>(
       N, D, K, Pf, ldp, labels, psum2, pcnt2, (int)ndb, w.und_list, mcnt);
@@ -3558,7 +3560,8 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
   LAUNCH_CHECK("spx_kmeans_step(reduce)");
   // the movers out of their provisional centres (the same partial buffers,
   // reused after the adds' reduce)
-  listed(sub_mask, w.full_list, mcnt + 1, pv, subp);
+  i64* subp = (i64*)w.cand_list;  // the list passes are done with the candidate list
+  listed(sub_rows, w.full_list, mcnt + 1, pside, subp);
   LAUNCH_CHECK("spx_kmeans_step(compact subtractions)");
   k_kmeans_accum<float><<<dim3((unsigned)G2, (unsigned)(ndb * ncb)), KA_THREADS, 0, S(stream)>>>(
       N, D, K, Pf, ldp, labels, psum2, pcnt2, (int)ndb, w.full_list, mcnt + 1, subp);
