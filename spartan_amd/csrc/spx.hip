@@ -3416,13 +3416,17 @@ extern "C" int spx_kmeans_accumulate(int dtype, int64_t N, int64_t D, int64_t K,
 // spx_kmeans_step = spx_kmeans_assign + spx_kmeans_accumulate with the same
 // results (labels bit for bit; counts exact; sums deterministic, within the
 // fp32-chain bound below of the fp64 sums) and, in the certified screen's
-// domain, ONE pass over the points for the decided rows: k_kmeans_pp
-// labels and accumulates them; the rows it leaves undecided (a few %) are
-// listed in row order, resolved by km_resolve and accumulated by
-// k_kmeans_accum over that list.  Partials are combined in a fixed order.
-// Workspace: spx_kmeans_assign's | spx_kmeans_accumulate's | fused partial
-// sums (G x K x D f64) | fused partial counts (G x K u64) | compaction block
-// counts.
+// domain, ONE pass over the points: k_kmeans_pp labels and accumulates the
+// rows it decides, and accumulates the finite rows it leaves undecided (a
+// few %) PROVISIONALLY under their screen-best centre; those are listed in
+// row order and resolved by km_resolve, whose label writes mark the rows that
+// moved (and the non-finite ones, which were not added); k_kmeans_accum then
+// adds them under their final label and takes the movers out of their
+// provisional centre (two short gathered passes).  Partials are combined in a
+// fixed order.  Workspace: spx_kmeans_assign's | spx_kmeans_accumulate's |
+// fused partial sums (G x K x D f64) | fused partial counts (G x K u64) |
+// compaction block counts | slice sums | provisional centres of the movers
+// (N i64) | two row masks | two list counters.
 static i64 kfs_grid(i64 N) {  // one block per CU, at most one per 32-row unit
   const i64 nunits = (N + KP_U - 1) / KP_U, ncu = num_cus();
   return nunits < ncu ? (nunits < 1 ? 1 : nunits) : ncu;
