@@ -617,11 +617,14 @@ extern "C" int spx_argreduce_combine(int op, int dtype, const void* vals, const 
 // fp32: 256x128x16, 8 waves (with the k-contiguous A staging: 141.4 TF = 89.9 %
 // of 157.3 at 32768^3 against 135.6 TF for the 256x256x16 16-wave tile,
 // profiles/r02_gemm_tune_ak.txt)
-// fp32: one accumulator set, flushed into C every 512 K-tiles (gemm_kernels.h
-// GFL): chains of 4096 MFMA steps instead of K / 2, at the one-chain form's
-// registers and occupancy (round 3's register two-level form, SEG, cost 6 %;
-// GFL 128 / 256 / 512: 139.1 / 140.1 / 140.8 TF, profiles/r04_gemm_gfl.txt)
-constexpr int SPX_GEMM_GFL = 512;
+// fp32: one accumulator set, flushed into C every 1024 K-tiles (gemm_kernels.h
+// GFL): chains of 8192 MFMA steps instead of K / 2 (two flushes at cfg4's
+// K = 32768), at the one-chain form's registers and occupancy (round 3's
+// register two-level form, SEG, cost 6 %; GFL 128 / 256 / 512 / 1024: 139.1 /
+// 140.1 / 140.8 / 141.2 TF, profiles/r04_gemm_gfl.txt, r04_gemm_gfl2_sweep.txt;
+// test_dot_cfg4_full_size -- full rows and columns at K = 32768 under the
+// CPU-or-closer rule -- green at 1024)
+constexpr int SPX_GEMM_GFL = 1024;
 typedef spx_mfma::Config<float, 256, 128, 16, 4, 2, 8, 0, SPX_GEMM_GFL> GemmF32Big;
 typedef spx_mfma::Config<float, 128, 128, 16, 2, 2, 8, 0, SPX_GEMM_GFL> GemmF32Small;
 

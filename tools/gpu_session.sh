@@ -65,6 +65,8 @@ for s in $STEPS; do
         step kmcounts_first 120 python3 tools/km_counts.py 100000000 first >> $O/kmcounts.txt 2>&1 ;;
     kmfit)
       cd $R && step kmfit 240 python3 tools/km_fit_timing.py 100000000 2 $KMFIT_OLD > $O/kmfit.txt 2>&1 ;;
+    dotbench)
+      cd $R && step dotbench 600 python3 bench.py --workloads 0 --cpu-baseline 0 --steps 2 --warmup 1 > $O/dotbench.json 2> $O/dotbench.err ;;
     kmtests)
       cd $R && step kmtests 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
         -p no:cacheprovider -k "kmeans" > $O/kmtests.log 2>&1 ;;
