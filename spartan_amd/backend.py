@@ -244,6 +244,10 @@ def compile_code_object(src):
 _NCU = []
 NT_STORE_BYTES = 64 << 20  # map outputs at least this large: non-temporal stores
 ROWS_GRID_PER_CU = 2  # rows reductions: 1.824 ms vs 1.836 uncapped at cfg2 axis 1 (profiles/r02_cfg2_grid.txt)
+# fused row-dot column reductions (cfg5's gradient): blocks per CU and rows
+# unrolled per lane group (profiles/r04_lreg_sweep*.txt; tools/lreg_sweep.py)
+ROWDOT_BLOCKS_PER_CU = 16
+ROWDOT_UNROLL = 8
 
 
 def _num_cus():
@@ -496,7 +500,7 @@ class HipBackend:
       # 64-column tile) with sixteen and rows unrolled 8 deep (3.866 ms per
       # lreg iteration against 3.959 at eight and 4; profiles/r04_lreg_sweep.txt)
       rowdot = bool(codegen.rowdots(root))
-      tb = (2 if CT > 1 else 16 if rowdot else 8) * _num_cus()
+      tb = (2 if CT > 1 else ROWDOT_BLOCKS_PER_CU if rowdot else 8) * _num_cus()
       if base < tb:
         P = max(1, min(-(-tb // base), -(-R // (rows_per_step * 4))))
       chunk = -(-R // P)
@@ -530,8 +534,8 @@ class HipBackend:
     U, rowinv = None, ()
     if kind == 'cols':
       U = codegen.cols_unroll(ins, classes, V, [vstr[k][1] for k in range(len(slots))])
-      if codegen.rowdots(root) and U == 4:
-        U = 8
+      if codegen.rowdots(root):
+        U = ROWDOT_UNROLL
       rowinv = tuple(s for k, s in enumerate(slots) if vstr[k][1] == 0)
     # a fused row dot's lane group width (and whether the vector path covers
     # the columns exactly) is compiled in: its per-row lane sum is then

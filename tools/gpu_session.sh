@@ -113,6 +113,8 @@ for s in $STEPS; do
       cd /tmp
       step kfs_lds 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_WAVES GRBM_GUI_ACTIVE \
         -d $O/kfs_lds -o p --output-format csv -- python3 $R/tools/km_step_once.py 100000000 2 > $O/kfs_lds.log 2>&1 ;;
+    lregsweep)
+      cd $R && step lregsweep 600 python3 tools/lreg_sweep.py 100000000 10 2 > $O/lregsweep.txt 2>&1 ;;
     lregtune)
       cd $R && step lregtune 300 ./tools/bin/lreg_tune 100000000 3 > $O/lregtune.txt 2>&1 ;;
     gemmseg2)

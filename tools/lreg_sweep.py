@@ -26,14 +26,13 @@ def main():
   Y = expr.rand(N, 1, dtype=np.float32, seed=42).force()
   w = np.random.default_rng(43).random((D, 1)).astype(np.float32)
   Xe, Ye = expr.lazify(X), expr.lazify(Y)
-  real_unroll, real_ncu = codegen.cols_unroll, backend._num_cus
-  confs = list(itertools.product([2, 4, 8], [4, 8, 16]))  # (rows unrolled, blocks per CU)
+  real = (backend.ROWDOT_UNROLL, backend.ROWDOT_BLOCKS_PER_CU)
+  confs = list(itertools.product([4, 8, 12], [7, 8, 14, 16, 21, 28]))  # (rows unrolled, blocks per CU)
   res = {c: [] for c in confs}
   be = backend.get()
   for r in range(rounds):
     for U, bpc in confs:
-      codegen.cols_unroll = lambda *a, U=U, **k: U
-      backend._num_cus = lambda bpc=bpc: real_ncu() * bpc // 8   # tb = 8 * _num_cus() for one column tile
+      backend.ROWDOT_UNROLL, backend.ROWDOT_BLOCKS_PER_CU = U, bpc
       be._sig_fns.clear()
       be._reduce_plans.clear()
       from spartan_amd.expr import plan_cache
@@ -46,7 +45,7 @@ def main():
       ms = (time.perf_counter() - t0) / reps * 1e3
       res[(U, bpc)].append(ms)
       print('round %d U=%d blocks/CU=%d: %.3f ms per iteration' % (r, U, bpc, ms), flush=True)
-  codegen.cols_unroll, backend._num_cus = real_unroll, real_ncu
+  backend.ROWDOT_UNROLL, backend.ROWDOT_BLOCKS_PER_CU = real
   print('best of %d rounds (ms per sgd iteration, 26.0 GB each):' % rounds)
   for c in confs:
     b = min(res[c])
