@@ -1584,9 +1584,9 @@ __host__ __device__ constexpr int ks_waves(int) { return KS_WAVES; }
 // zero bf16][16-byte pad], 2 D + 48 bytes: also an odd multiple of 4 banks
 // for D = 64 and 128, so conflict-free the same way.
 __host__ __device__ constexpr int ks_row_bytes(int D, int mode = 0) { return (mode == 0 ? 4 : 2) * D + 48; }
-// (MODE 1 adds the D fp32 centre mean after the rows)
+// (then the D fp32 centre mean, which both modes subtract from the points)
 static size_t ks_lds_bytes(i64 D, int nct, int mode = 0) {
-  return (size_t)32 * nct * ks_row_bytes((int)D, mode) + (mode == 1 ? 4 * D : 0);
+  return (size_t)32 * nct * ks_row_bytes((int)D, mode) + 4 * D;
 }
 typedef _Float16 kh_f8 __attribute__((ext_vector_type(8)));
 
@@ -1742,7 +1742,7 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
       *(kb_bf8*)(row + CCOFF) = (kb_bf8){b1, b2, b3, z, z, z, z, z};
       *(kb_bf8*)(row + CCOFF + 16) = (kb_bf8){z, z, z, z, z, z, z, z};
     }
-    if constexpr (MODE == 1) {
+    {
       float* mul = (float*)(kb_lds + NC * RB);
       for (int i = t; i < D; i += ks_waves(MODE) * 64) mul[i] = muf[i];
     }
@@ -1757,12 +1757,13 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
   // one accumulator chain: 48 (bf16x3) or 16 (fp16) products per k-step
   // over KS k-steps
   const double chain = (MODE == 0 ? 48.0 : 16.0) * (double)KS;
-  // error of x.c' per |x|: bf16x3 (u + 3.1 * 2^-18 + chain) cmax.  fp16
-  // screen, per |x'|: u cmax (x' = fl(x - mu)) + 2^-11 cmax (x' to fp16) +
+  // error of x'.c' per |x'| (both modes centre the points, x' = fl(x - mu),
+  // u cmax): bf16x3 (u + u + 3.1 * 2^-18 + chain) cmax.  fp16
+  // screen: u cmax (x') + 2^-11 cmax (x' to fp16) +
   // 1.001 dcmax (c' to fp16, measured) + the chain over |xh| |ch| <=
   // 1.001 |x'| (cmax + dcmax)
   const double dcmax = MODE == 1 ? cmax_p[3] : 0.0;
-  const double eS = MODE == 0 ? (u32 + 3.1 * 3.814697265625e-06 + 2.0 * (chain + 3.0) * u32) * 1.01 * cmax
+  const double eS = MODE == 0 ? (2.0 * u32 + 3.1 * 3.814697265625e-06 + 2.0 * (chain + 3.0) * u32) * 1.01 * cmax
                               : (u32 * cmax + 4.8828125e-04 * cmax + 1.001 * dcmax +
                                  2.0 * (chain + 3.0) * u32 * 1.001 * (cmax + dcmax)) * 1.01;
   float kq[3];
@@ -1810,7 +1811,7 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
     // |p|^2 only feeds the bound (x 1.001 slack): four independent partial
     // chains instead of one 64-deep dependent fma chain
     float p2q[4] = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (MODE == 1) {  // x' = x - mu, mu read from LDS in the lane's dim order
+    {  // x' = x - mu, mu read from LDS in the lane's dim order
       const float* mul = (const float*)(kb_lds + NC * RB) + 4 * h;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -3249,8 +3250,10 @@ static int km_resolve(hipStream_t s, i64 N, i64 D, i64 K, const float* Pf, i64 l
   const i64 need_as = (ntiles + KS_WAVES - 1) / KS_WAVES;
   const int grid_as = (int)(need_as < ncu ? need_as : ncu);
   const unsigned int cgrid1 = (unsigned int)((ntiles + 255) / 256);
-  ks_launch_n<0>(nct, s, N, D, Pf, ldp, CBh, CBl, cnf, w.cmax, labels, w.counters, w.full_list, w.und_mask,
-                 w.scr_list, w.counters + 3, nullptr, grid_as);
+  // the bf16x3 list pass centres the points as the screen does: it ranks by
+  // |c'|^2 - 2 x'.c' (cnf2 of the prep) with x' = fl(x - mu)
+  ks_launch_n<0>(nct, s, N, D, Pf, ldp, CBh, CBl, cnf + KF_BN, w.cmax, labels, w.counters, w.full_list, w.und_mask,
+                 w.scr_list, w.counters + 3, w.muf, grid_as);
   LAUNCH_CHECK("spx_kmeans_assign(filter A-stationary, list)");
   k_ks_compact<1><<<cgrid1, 256, 0, s>>>(N, w.und_mask, w.scr_list, w.counters + 3, w.und_list, w.counters + 2);
   LAUNCH_CHECK("spx_kmeans_assign(compact)");
