@@ -1231,7 +1231,7 @@ __device__ __forceinline__ void kc_coef(double eS, double cmax, double mun, doub
   k[2] = (float)(k2 * up);
 }
 
-static size_t kb_lds_bytes(i64 D, int nct) { return (size_t)2 * 32 * nct * (D + 8) * 2 + (size_t)32 * nct * 4; }
+static size_t kb_lds_bytes(i64 D, int nct) { return (size_t)2 * 32 * nct * (D + 8) * 2 + (size_t)32 * nct * 4 + 4 * D; }
 
 // Step (B) of the bf16x3 filter epilogue, as a function (tools/perm_probe.hip
 // checks it against a brute-force top-2).
@@ -1304,16 +1304,20 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
                                                                     i64* __restrict__ full_list,
                                                                     KfCand* __restrict__ cand_list,
                                                                     const i64* __restrict__ rows_in,
-                                                                    const unsigned int* __restrict__ nrows_in) {
+                                                                    const unsigned int* __restrict__ nrows_in,
+                                                                    const float* __restrict__ muf) {
   // rows_in != NULL (list mode): only the *nrows_in points rows_in[0..n) --
   // the rows the A-stationary filter left undecided; slot s of the list plays
-  // the role of row s below
+  // the role of row s below.  The points are centred like the centres (x' =
+  // fl(x - mu), mu = muf in LDS): a' = |c'|^2 - 2 x'.c' (cnf = cnf2 of the
+  // prep), so the bound and the candidate masks scale with |x'|, not |x|.
   extern __shared__ __attribute__((aligned(16))) unsigned char kb_lds[];
   constexpr int NC = 32 * NCT;
   const int Dp = (int)D + 8;
   __bf16* Bh = (__bf16*)kb_lds;
   __bf16* Bl = Bh + NC * Dp;
   float* cns = (float*)(Bl + NC * Dp);
+  float* mul = cns + NC;  // mu in the row's dim order
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, h = lane >> 5;
   {
     // k-order inside every 16-dim step is permuted (dim quads 1 and 2
@@ -1329,6 +1333,7 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
       *(kb_u2*)&Bl[c * Dp + 4 * pq] = *(const kb_u2*)&CBl[(i64)c * D + 4 * q];
     }
     for (int i = t; i < NC; i += KB_WAVES * 64) cns[i] = cnf[i];
+    for (int i = t; i < (int)D; i += KB_WAVES * 64) mul[i] = muf[i];
   }
   __syncthreads();
   float cnr[NCT];  // |c|^2 of this lane's centre in every tile
@@ -1344,7 +1349,8 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
   // chain length of one accumulator: 48 KB_GRP products into a fresh
   // accumulator, then KS / KB_GRP adds
   const double chain = 48.0 * KB_GRP + (double)(KS / KB_GRP);
-  const double eS = (u32 + 3.1 * 3.814697265625e-06 + 2.0 * (chain + 3.0) * u32) * 1.01 * cmax;
+  // (one u cmax per |x'| for x' = fl(x - mu))
+  const double eS = (2.0 * u32 + 3.1 * 3.814697265625e-06 + 2.0 * (chain + 3.0) * u32) * 1.01 * cmax;
   const i64 nslots = rows_in ? (i64)*nrows_in : N;
   if (nslots == 0) return;
   const i64 ntiles = (nslots + 31) / 32;
@@ -1377,10 +1383,11 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
         for (int g = 0; g < KB_GRP; ++g) {
           const int s = g0 + g, ks = ks0 + s;
           float x[8];
+          const kb_f4 m0 = *(const kb_f4*)(mul + ks * 16 + 4 * h), m1 = *(const kb_f4*)(mul + ks * 16 + 8 + 4 * h);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            x[j] = ra[s][0][j];
-            x[j + 4] = ra[s][1][j];
+            x[j] = ra[s][0][j] - m0[j];
+            x[j + 4] = ra[s][1][j] - m1[j];
           }
           {
             int nks = ks + 4;
@@ -1533,8 +1540,8 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
 template <int NCT>
 static void kb_launch(hipStream_t s, i64 N, i64 D, const float* P, i64 ldp, const __bf16* CBh, const __bf16* CBl,
                       const float* cnf, const double* cmax, i64* labels, unsigned int* counters, i64* full_list,
-                      KfCand* cand_list, int grid, const i64* rows_in = nullptr,
-                      const unsigned int* nrows_in = nullptr) {
+                      KfCand* cand_list, int grid, const i64* rows_in, const unsigned int* nrows_in,
+                      const float* muf) {
   const size_t lds = kb_lds_bytes(D, NCT);
   static bool attr = false;
   if (!attr) {
@@ -1543,7 +1550,7 @@ static void kb_launch(hipStream_t s, i64 N, i64 D, const float* P, i64 ldp, cons
     attr = true;
   }
   k_kmeans_filter_b3<NCT><<<grid, KB_WAVES * 64, lds, s>>>(N, D, P, ldp, CBh, CBl, cnf, cmax, labels, counters,
-                                                           full_list, cand_list, rows_in, nrows_in);
+                                                           full_list, cand_list, rows_in, nrows_in, muf);
 }
 
 // ---------------------------------------------------------------------------
@@ -3258,10 +3265,10 @@ static int km_resolve(hipStream_t s, i64 N, i64 D, i64 K, const float* Pf, i64 l
   k_ks_compact<1><<<cgrid1, 256, 0, s>>>(N, w.und_mask, w.scr_list, w.counters + 3, w.und_list, w.counters + 2);
   LAUNCH_CHECK("spx_kmeans_assign(compact)");
   switch (nct) {
-    case 1: kb_launch<1>(s, N, D, Pf, ldp, CBh, CBl, cnf, w.cmax, labels, w.counters, w.full_list, w.cand_list, ncu, w.und_list, w.counters + 2); break;
-    case 2: kb_launch<2>(s, N, D, Pf, ldp, CBh, CBl, cnf, w.cmax, labels, w.counters, w.full_list, w.cand_list, ncu, w.und_list, w.counters + 2); break;
-    case 4: kb_launch<4>(s, N, D, Pf, ldp, CBh, CBl, cnf, w.cmax, labels, w.counters, w.full_list, w.cand_list, ncu, w.und_list, w.counters + 2); break;
-    default: kb_launch<8>(s, N, D, Pf, ldp, CBh, CBl, cnf, w.cmax, labels, w.counters, w.full_list, w.cand_list, ncu, w.und_list, w.counters + 2); break;
+    case 1: kb_launch<1>(s, N, D, Pf, ldp, CBh, CBl, cnf + KF_BN, w.cmax, labels, w.counters, w.full_list, w.cand_list, ncu, w.und_list, w.counters + 2, w.muf); break;
+    case 2: kb_launch<2>(s, N, D, Pf, ldp, CBh, CBl, cnf + KF_BN, w.cmax, labels, w.counters, w.full_list, w.cand_list, ncu, w.und_list, w.counters + 2, w.muf); break;
+    case 4: kb_launch<4>(s, N, D, Pf, ldp, CBh, CBl, cnf + KF_BN, w.cmax, labels, w.counters, w.full_list, w.cand_list, ncu, w.und_list, w.counters + 2, w.muf); break;
+    default: kb_launch<8>(s, N, D, Pf, ldp, CBh, CBl, cnf + KF_BN, w.cmax, labels, w.counters, w.full_list, w.cand_list, ncu, w.und_list, w.counters + 2, w.muf); break;
   }
   LAUNCH_CHECK("spx_kmeans_assign(filter bf16x3, undecided rows)");
   const int gp = kf_persistent_grid(N);
