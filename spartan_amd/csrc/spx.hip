@@ -1958,6 +1958,10 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
       }
     } else {
       kb_acc a0, b0;
+      // the sweep at wave priority 1: with two waves per SIMD the one in its
+      // MFMA sweep issues first and the partner's split / decision VALU fills
+      // the gaps (list pass 1.22 -> 1.16 ms at cfg3, tools/kp_ablate.sh as_prio)
+      __builtin_amdgcn_s_setprio(1);
       chain(0, a0);
       if constexpr (NCT == 1) {
         fold(0, a0);
@@ -1973,6 +1977,7 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
         __builtin_amdgcn_sched_barrier(0);
         fold(NCT - 1, b0);
       }
+      __builtin_amdgcn_s_setprio(0);
     }
     float lo0[16];  // this lane's best per register (its centre r over all tiles)
 #pragma unroll
@@ -2679,24 +2684,27 @@ __global__ __launch_bounds__(256) void k_ks_count(i64 N, const unsigned long lon
 
 // exclusive scan of n block counts in place (one block), the total into *total
 __global__ __launch_bounds__(1024) void k_exscan_u32(unsigned int* __restrict__ v, i64 n, unsigned int* __restrict__ total) {
-  __shared__ unsigned int part[1024];
+  // thread t owns a run of `per` entries; the run totals are scanned by a
+  // wave scan + the 16 wave totals (the first version scanned all 1024 run
+  // totals serially in thread 0: ~19 us of LDS round trips)
+  __shared__ unsigned int wsum[16];
   const i64 per = (n + 1023) / 1024;
   const i64 a = threadIdx.x * per, b = a + per < n ? a + per : n;
   unsigned int s = 0;
   for (i64 i = a; i < b; ++i) s += v[i];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned int run = 0;
-    for (int i = 0; i < 1024; ++i) {
-      const unsigned int x = part[i];
-      part[i] = run;
-      run += x;
-    }
-    *total = run;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned int inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned int y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
   }
+  if (lane == 63) wsum[w] = inc;
   __syncthreads();
-  unsigned int run = part[threadIdx.x];
+  unsigned int base = 0;
+  for (int k = 0; k < w; ++k) base += wsum[k];
+  if (threadIdx.x == 1023) *total = base + inc;
+  unsigned int run = base + inc - s;
   for (i64 i = a; i < b; ++i) {
     const unsigned int x = v[i];
     v[i] = run;
@@ -3111,7 +3119,11 @@ __global__ __launch_bounds__(256) void k_kmeans_reduce(i64 n, i64 G, const P* __
   const int j = threadIdx.x & 63, sl = threadIdx.x >> 6;
   const i64 i = (i64)blockIdx.x * 64 + j;
   T s = T(0);
+  // unrolled: the loads of 8 g's in flight (one at a time, each L2 / HBM
+  // latency was paid in series: ~20 us for K = 256 counts); the adds keep
+  // their order
   if (i < n)
+#pragma unroll 8
     for (i64 g = sl; g < G; g += 4) s += (T)part[g * n + i];
   red[sl][j] = s;
   __syncthreads();

@@ -58,6 +58,13 @@ subs = {
   'noloop': [('for (int k = 1; k < U && __ballot', 'for (int k = 1; k < 1 && __ballot')],
   'nostage': [('if (us < nit) stage(', 'if (us < 0) stage(')],
   'noatomic': [('rk = __hip_atomic_fetch_add(rcnt + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);', 'rk = 0;')],
+  # k_kmeans_filter_as MODE 0 (the bf16x3 list pass): wave priority 1 over the
+  # centre sweep (as_prio) or over the split / decision instead (as_prio_epi)
+  'as_prio': [('      kb_acc a0, b0;\n      chain(0, a0);\n', '      kb_acc a0, b0;\n      __builtin_amdgcn_s_setprio(1);\n      chain(0, a0);\n'),
+              ('        fold(NCT - 1, b0);\n      }\n    }\n    float lo0[16];', '        fold(NCT - 1, b0);\n      }\n      __builtin_amdgcn_s_setprio(0);\n    }\n    float lo0[16];')],
+  'as_prio_epi': [('  for (; tile < ntiles; tile += stride) {\n    load(tile);', '  for (; tile < ntiles; tile += stride) {\n    __builtin_amdgcn_s_setprio(1);\n    load(tile);'),
+                  ('      kb_acc a0, b0;\n      chain(0, a0);\n', '      kb_acc a0, b0;\n      __builtin_amdgcn_s_setprio(0);\n      chain(0, a0);\n'),
+                  ('        fold(NCT - 1, b0);\n      }\n    }\n    float lo0[16];', '        fold(NCT - 1, b0);\n      }\n      __builtin_amdgcn_s_setprio(1);\n    }\n    float lo0[16];')],
   'nobarrier': [('    constexpr int GR = decltype(gc)::value, c = decltype(cc)::value;\n    __syncthreads();\n',
                  '    constexpr int GR = decltype(gc)::value, c = decltype(cc)::value;\n')],
 }[name]
