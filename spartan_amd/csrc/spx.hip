@@ -1346,9 +1346,11 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
   const double mcoef = cmax_p[1], mun = cmax_p[2];
   const double u32 = 5.9604644775390625e-08;
   const int KS = (int)D / 16;
-  // chain length of one accumulator: 48 KB_GRP products into a fresh
-  // accumulator, then KS / KB_GRP adds
-  const double chain = 48.0 * KB_GRP + (double)(KS / KB_GRP);
+  // chain length of one accumulator: the 48 KB_GRP products of a group go
+  // into a fresh accumulator, small cross terms first (32 KB_GRP additions of
+  // partial sums <= 2 * 2^-8 * 1.004 |x'| cmax, then 16 KB_GRP of <= 1.016
+  // |x'| cmax: within 16.5 KB_GRP of |x'| cmax), then KS / KB_GRP adds
+  const double chain = 16.5 * KB_GRP + (double)(KS / KB_GRP);
   // (one u cmax per |x'| for x' = fl(x - mu))
   const double eS = (2.0 * u32 + 3.1 * 3.814697265625e-06 + 2.0 * (chain + 3.0) * u32) * 1.01 * cmax;
   const i64 nslots = rows_in ? (i64)*nrows_in : N;
@@ -1424,13 +1426,16 @@ __global__ __launch_bounds__(KB_WAVES * 64) void k_kmeans_filter_b3(i64 N, i64 D
           // fresh accumulator that is then added to the running sum: the
           // rounding bound is that chain + D / (16 KB_GRP) adds instead of
           // one 3D-long chain
+          // (the small cross terms of the group first, then its xh.ch terms:
+          // only those 16 KB_GRP additions see partial sums of size |x'| cmax)
           kb_acc tk = (kb_acc){};
 #pragma unroll
           for (int g = 0; g < KB_GRP; ++g) {
-            tk = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[g], bh[ct & 1][g], tk, 0, 0, 0);
             tk = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[g], bl[ct & 1][g], tk, 0, 0, 0);
             tk = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[g], bh[ct & 1][g], tk, 0, 0, 0);
           }
+#pragma unroll
+          for (int g = 0; g < KB_GRP; ++g) tk = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[g], bh[ct & 1][g], tk, 0, 0, 0);
           acc[ct] += tk;
         }
       }
@@ -1763,7 +1768,10 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
   const double u32 = 5.9604644775390625e-08;
   // one accumulator chain: 48 (bf16x3) or 16 (fp16) products per k-step
   // over KS k-steps
-  const double chain = (MODE == 0 ? 48.0 : 16.0) * (double)KS;
+  // (MODE 0: the two-phase chain below -- 32 KS additions of partial sums
+  // <= 2 * 2^-8 * 1.004 |x'| cmax, then 16 KS of <= 1.016 |x'| cmax, within
+  // 16.5 KS additions of |x'| cmax, and the 1.01 factor of eS covers the rest)
+  const double chain = (MODE == 0 ? 16.5 : 16.0) * (double)KS;
   // error of x'.c' per |x'| (both modes centre the points, x' = fl(x - mu),
   // u cmax): bf16x3 (u + u + 3.1 * 2^-18 + chain) cmax.  fp16
   // screen: u cmax (x') + 2^-11 cmax (x' to fp16) +
@@ -1874,11 +1882,34 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
         c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bh, c0, 0, 0, 0);
       }
     };
+    // MODE 0 runs a tile's chain in two phases: the small cross terms xh.cl
+    // and xl.ch of every k-step first (their partial sums stay below
+    // 2 * 2^-8 |x'| cmax), then the xh.ch terms -- so only the 16 KS
+    // additions of the second phase see partial sums of size |x'| cmax and
+    // the chain bound is ~16.5 KS additions instead of 48 KS (B hi is read
+    // twice per k-step).  Step i of NST: MODE 0 i < KS small terms of k-step
+    // i, else the big term of k-step i - KS; MODE 1 = kstep(i).
+    constexpr int NST = MODE == 0 ? 2 * KS : KS;
+    auto step = [&](int i, const unsigned char* rp, kb_acc& c0) {
+      if constexpr (MODE == 0) {
+        if (i < KS) {
+          const kb_bf8 bh = *(const kb_bf8*)(rp + 32 * i);
+          const kb_bf8 bl = *(const kb_bf8*)(rp + 2 * D + 32 * i);
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl, c0, 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh, c0, 0, 0, 0);
+        } else {
+          const kb_bf8 bh = *(const kb_bf8*)(rp + 32 * (i - KS));
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i - KS], bh, c0, 0, 0, 0);
+        }
+      } else {
+        kstep(i, rp, c0);
+      }
+    };
     auto chain = [&](int ct, kb_acc& c0) {
       c0 = (kb_acc){};
       const unsigned char* rp = rowp + ct * 32 * RB;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) kstep(ks, rp, c0);
+      for (int i = 0; i < NST; ++i) step(i, rp, c0);
       c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, *(const kb_bf8*)(rp + CCOFF), c0, 0, 0, 0);
     };
     // fold tile ct's acc, tagged with ct, into the running top-2 (3 VALU per
@@ -1901,10 +1932,10 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
       c0 = (kb_acc){};
       const unsigned char* rp = rowp + ct * 32 * RB;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        kstep(ks, rp, c0);
+      for (int i = 0; i < NST; ++i) {
+        step(i, rp, c0);
 #pragma unroll
-        for (int qq = 0; qq < 16 / KS; ++qq) fold1(ks * (16 / KS) + qq, pct, p0[ks * (16 / KS) + qq]);
+        for (int qq = 0; qq < 16 / NST; ++qq) fold1(i * (16 / NST) + qq, pct, p0[i * (16 / NST) + qq]);
       }
       c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, *(const kb_bf8*)(rp + CCOFF), c0, 0, 0, 0);
     };
