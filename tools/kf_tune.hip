@@ -72,7 +72,7 @@ int main(int argc, char** argv) {
   i64* full_list = (i64*)q;
   q += N * 8;
   KfCand* cand = (KfCand*)q;
-  k_kmeans_prep<<<1, 256>>>(D, K, Kp, C, CT, cn, cmax);
+  k_kmeans_prep<<<1, 256>>>(D, K, Kp, C, CT, cn, cmax, 0.0);  // fp64 distances: no fp32 tie margin
   i64* lab;
   CK(hipMalloc(&lab, N * 8));
   std::vector<i64> ref(N), got(N);
