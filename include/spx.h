@@ -132,6 +132,12 @@ int spx_copy_region(int dst_dtype, void* dst, const int64_t* dst_shape,
  * (v_mfma_f64_16x16x4_f64).  Replaces tiles[0].dot(tiles[1]) in
  * dot_map2_mapper (spartan/expr/dot.py:195-212), dot_outer_mapper (:217-233)
  * and dot_map2_np_mapper (:172-187).
+ * Memory: C must be coarse-grained device memory (hipMalloc / a torch CUDA
+ * tensor).  The fp32 kernel flushes its accumulators into C every 1024
+ * K-tiles (fp32 chains of <= 8192 MFMA steps at any K): with K > 16384, or
+ * with beta != 0, C is updated by no-return fp32 atomic adds, which are not
+ * reliably performed on fine-grained or host-coherent allocations.  One wave
+ * owns each element of C, so the adds land in program order (deterministic).
  */
 int spx_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
              const void* B, int64_t ldb, void* C, int64_t ldc, double alpha,
@@ -194,11 +200,16 @@ int spx_kmeans_accumulate(int dtype, int64_t N, int64_t D, int64_t K, const void
  * units -- one centre's chain is as long as that centre's rows in the window,
  * ~63 on average at K = 256 on uniform data and up to 16128 when one centre
  * takes every row (K = 1 or 2, skewed data) -- and the window sums are added
- * in fp64 in a fixed order.  The a-priori bound is that of an fp32 sum of
- * <= 16128 terms per window (<= 16128 u sum |x|, u = 2^-24); the reference's
- * own kmeans_center_mapper sums ALL of a centre's rows in one fp32 chain
- * (k_means_.py:67-89), so this is never looser than the reference.  Measured
- * within 1e-5 of sum |x| in every test, including the long-chain cases.
+ * in fp64 in a fixed order.  A row the screen cannot decide is added
+ * PROVISIONALLY to its screen-best centre p when its centred norm |x - mu| is
+ * at most 4 (max_c |c - mu| + |mu|), and moved in fp64 afterwards if its final
+ * label differs (farther rows are gathered in fp64 instead).  So a window
+ * chain holds the centre's own rows plus at most a few such movers of the
+ * data's own scale, and its a-priori bound is that of an fp32 sum of <= 16128
+ * terms of that scale (<= 16128 u (sum |x| + |movers|), u = 2^-24); the
+ * reference's own kmeans_center_mapper sums ALL of a centre's rows in one fp32
+ * chain (k_means_.py:67-89).  Measured within 1e-5 of sum |x| in every test,
+ * including the long-chain cases and far undecided outliers.
  * Other shapes run the two calls.  workspace_bytes >=
  * spx_kmeans_step_workspace(dtype, N, D, K). */
 int64_t spx_kmeans_step_workspace(int dtype, int64_t N, int64_t D, int64_t K);

@@ -916,10 +916,13 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=(), lpr
       return ['%s[off]' % p], pre
 
     # per-row inputs of a row-dot kernel with 16-lane row groups: one load per
-    # unrolled step (lane u of the group fetches row u), DPP broadcasts
+    # unrolled step (lane u of the group fetches row u), DPP broadcasts --
+    # for 4- and 8-byte values only (dpp_mov moves one or two dwords; a bool,
+    # int8 or fp16 row input keeps its per-row load)
     bcast = ()
     if rds and lpr == 16 and U > 1 and U <= 16:
-      bcast = tuple(s for (s, dt), cls in zip(inputs, classes) if cls == 'b' and s not in rowinv)
+      bcast = tuple(s for (s, dt), cls in zip(inputs, classes)
+                    if cls == 'b' and s not in rowinv and np.dtype(dt).itemsize in (4, 8))
 
     def body(V):
       masked = bool(rds)

@@ -2336,9 +2336,21 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
   float kq[3];
   kc_coef(eS, cmax, mun, mcoef, D, kq, xk1, xk0);
   const bool cok = cmax * cmax < 1e36 && mun * cmax < 1e36 && cmax < 3.0e4 && dcmax == dcmax;
-  const float pn_lim = (float)(cmax > 0.0 ? 1e36 / cmax : 1e36);
+  // rows with |x'| >= pn_lim are left undecided and not added (label code
+  // -1): the list passes label them exactly and the gathered accumulation
+  // adds them in fp64.  Besides the fp32 range limit, pn_lim keeps far
+  // outliers (|x'| > 4 (cmax + |mu|)) out of the fp32 window sums: a
+  // provisionally added row that moved afterwards would leave the fp32
+  // rounding of its own add in p's chain (the test with far
+  // undecided outliers).  A far row that the screen could decide takes the
+  // list passes instead -- exact either way, and such rows are rare.
+  const float pn_lim = (float)fmin(cmax > 0.0 ? 1e36 / cmax : 1e36, 4.0 * (cmax + mun) + 1e-30);
 
   const int G = gridDim.x, bk = blockIdx.x;
+  // block bk takes units bk, bk + G, ...: in every slot the grid reads one
+  // contiguous stretch of G units (G x 16 KiB).  (Round 5: one contiguous
+  // range of units per block -- 256 streams far apart -- ran 0.1-0.2 ms
+  // SLOWER at cfg3, gpurun_out/r5f.)
   const i64 nunits = (N + U - 1) / U;
   const int nit = bk < nunits ? (int)((nunits - 1 - bk) / G + 1) : 0;
   // slots 0 .. nit + KP_LAG - 1 (unit nit - 1 is added in slot nit - 1 + KP_LAG), whole bodies
@@ -2470,8 +2482,6 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     if (s == 0 && h == 0 && act) __hip_atomic_store(rcnt + d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     // (5) merge the fold's tiles and halves, the candidates out (mu's reads
     // for the stage first)
-    kb_f4 mu4[NQ];
-    mu_load(mu4);
     const float fb1 = ks_max(lo0, lo1), fb2 = ks_med3(lo0, lo1, ks_max(sec0, sec1));
     const int fib = lo0 >= lo1 ? il0 : il1;
     float c1l, c1h, c2l, c2h, cfl, cfh;
@@ -2489,15 +2499,23 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     }
     __builtin_amdgcn_sched_barrier(0);
     // (6) stage of unit t + 1
-    if (us < nit) stage(rs, mu4, us);
+    if (us < nit) {
+      kb_f4 mu4[NQ];
+      mu_load(mu4);
+      stage(rs, mu4, us);
+    }
     const int rnd = act ? (int)rk : 0xffff;  // add round (0xffff: no add)
     if (s == 0 && h == 0) dres[(u2 & 3) * U + j] = (dl & 0xffff) | (rnd << 16);
   };
 
-  // matrix role of slot t: the MFMAs of unit t (if t < nit), with the add
-  // rounds of unit t - 4 (raw columns in r, label and round from dres)
-  // between them; then that unit's labels and undecided bits; then the loads
-  // of unit t + 4 into the ring entry unit t - 4 leaves.
+  // matrix role of slot t: the MFMAs of unit t (if t < nit) with, woven
+  // between them, the add rounds of unit t - 4 (raw columns in r, label and
+  // round from dres), that unit's labels and undecided bits and the loads of
+  // unit t + 4 into the ring entry unit t - 4 leaves.  Each MFMA pair holds
+  // the matrix pipe for 64 cycles; an LDS read-add-write round, the stores
+  // and the loads issue in those shadows instead of after the chain (round 5:
+  // the chain, then the rounds, the stores and the loads made this role the
+  // slot's critical path).
   auto matrix_role = [&](int tt, kb_f4 (&r)[NQ]) __attribute__((always_inline)) {
     // the matrix role is the slot's critical path: its wave issues first when
     // both waves of a SIMD are ready (-0.3 ms per cfg3 pass; the vector role
@@ -2510,11 +2528,12 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     const i64 grow = una * U + j;
     const bool rlive = av && grow < N;
     const int dr = dres[(ua & 3) * U + jr];  // the add lanes' rows
+    const int dlv = dres[(ua & 3) * U + j];  // the label lanes' rows
     const unsigned char* bp = xh + ((size_t)(tt & 1) * U + j) * RS + 16 * h;
     // B fragments three k-steps ahead: under load an LDS read takes longer
     // than one MFMA pair, and a read issued one step ahead stalled every pair
-    constexpr int PF = KS < 3 ? KS : 3;
-    kh_f8 bq[4];
+    constexpr int PF = KS < 2 ? KS : 2, NB = PF + 1;
+    kh_f8 bq[NB];
 #pragma unroll
     for (int p = 0; p < PF; ++p) bq[p] = *(const kh_f8*)(bp + 32 * p);
     typedef unsigned int u4v __attribute__((ext_vector_type(4)));
@@ -2532,44 +2551,25 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     const int d = dcode >= 0 ? dcode : dcode <= -2 ? -2 - dcode : -1;  // the centre the row is added to
     const int rnd = av ? (int)((unsigned int)dr >> 16) : 0xffff;
     float* const srow = sums + (d >= 0 ? d : 0) * D + col0;
-    // round 0's reads go out before the last MFMAs (the sums rows are
-    // stable: only this group writes them in this slot), their latency under
-    // the MFMA chains
-    kb_f4 v0[NQ];
-    auto mk = [&](auto kc) __attribute__((always_inline)) {
-      constexpr int ks = decltype(kc)::value;
-      if constexpr (ks == KS - 1) {  // (earlier: the registers spill)
-        if (rnd == 0) {
+    // the add rounds (a wave's LDS operations run in issue order: round k + 1
+    // reads what round k wrote); a row's round is its rank, so round k has
+    // work only if some row of the unit has rank >= k.  Rounds 0 .. NRU - 1
+    // are straight-line steps between the MFMA pairs: the reads of round k at
+    // step RDk, its read-add-writes at step WRk; rounds NRU and later
+    // (a unit with NRU + 1 rows of one centre: rare) run in a loop after the
+    // chain's last k-step.
+    constexpr int NRU = KS >= 8 ? 3 : 2;
+    constexpr int WR0 = 1, RD1 = 2, WR1 = KS >= 8 ? 4 : 3, RD2 = 5, WR2 = 7;
+    kb_f4 v[NQ];
+    auto rd = [&]() __attribute__((always_inline)) {
 #pragma unroll
-          for (int q = 0; q < NQ; ++q) v0[q] = *(kb_f4*)(srow + 4 * qof(q));
-        }
-      }
-      if constexpr (ks + PF < KS) bq[(ks + PF) & 3] = *(const kh_f8*)(bp + 32 * (ks + PF));
-      if (mf && scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[0][ks], bq[ks & 3], acc0, 0, 0, 0);
-      if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[1][ks], bq[ks & 3], acc1, 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
+      for (int q = 0; q < NQ; ++q) v[q] = *(kb_f4*)(srow + 4 * qof(q));
     };
-    ks_unroll(mk, std::make_integer_sequence<int, KS>{});
-    if (mf && scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cc0, ones, acc0, 0, 0, 0);
-    if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cc1, ones, acc1, 0, 0, 0);
-    const int dlv = dres[(ua & 3) * U + j];  // the label lanes' rows
-    // the add rounds, after the MFMAs are issued (a wave's LDS operations run
-    // in issue order: round k + 1 reads what round k wrote); rounds are
-    // ranks, so the loop ends with the unit's largest rank (< 32)
-    if (rnd == 0) {
+    auto wr = [&]() __attribute__((always_inline)) {
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) *(kb_f4*)(srow + 4 * qof(q)) = v0[q] + r[q];
-    }
-    // (a rank is < U by construction -- at most U rows per unit -- so the
-    // cap k < U never binds; it bounds the loop whatever dres holds)
-    for (int k = 1; k < U && __ballot(rnd >= k && rnd != 0xffff) != 0ull; ++k)
-      if (rnd == k) {
-        kb_f4 v[NQ];
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) v[q] = *(kb_f4*)(srow + 4 * qof(q));
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) *(kb_f4*)(srow + 4 * qof(q)) = v[q] + r[q];
-      }
+      for (int q = 0; q < NQ; ++q) *(kb_f4*)(srow + 4 * qof(q)) = v[q] + r[q];
+    };
+    if (rnd == 0) rd();
     // labels (-1 for an undecided row: the list passes write it) and the
     // unit's undecided-row mask; every store issued.  Lanes j and j + 32
     // write the same label to the same word, and all 64 lanes the same mask
@@ -2577,13 +2577,39 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     // (With the idle lanes of every store aimed at ONE dummy word, all CUs'
     // stores met on one L2 line; the vmcnt waits that count those stores
     // cost ~3.7 ms per cfg3 pass -- profiles/r04_kp_ablate_v4.txt.)
-    const int dlab = av ? (int)(short)(dlv & 0xffff) : -1;
-    i64* la = rlive ? labels + grow : (i64*)dummy;
-    *la = (i64)dlab;
-    const unsigned long long m = __ballot(dlab < 0 && rlive) & 0xffffffffull;
-    unsigned long long* ma = av ? und_mask + una : dummy + 1;
-    *ma = m;
+    auto stores = [&]() __attribute__((always_inline)) {
+      const int dlab = av ? (int)(short)(dlv & 0xffff) : -1;
+      i64* la = rlive ? labels + grow : (i64*)dummy;
+      *la = (i64)dlab;
+      const unsigned long long m = __ballot(dlab < 0 && rlive) & 0xffffffffull;
+      unsigned long long* ma = av ? und_mask + una : dummy + 1;
+      *ma = m;
+    };
+    auto mk = [&](auto kc) __attribute__((always_inline)) {
+      constexpr int ks = decltype(kc)::value;
+      if constexpr (ks + PF < KS) bq[(ks + PF) % NB] = *(const kh_f8*)(bp + 32 * (ks + PF));
+      if (mf && scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[0][ks], bq[ks % NB], acc0, 0, 0, 0);
+      if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[1][ks], bq[ks % NB], acc1, 0, 0, 0);
+      if constexpr (ks == WR0) { if (rnd == 0) wr(); }
+      if constexpr (ks == RD1) { if (rnd == 1) rd(); }
+      if constexpr (ks == WR1) { if (rnd == 1) wr(); }
+      if constexpr (NRU > 2 && ks == RD2) { if (rnd == 2) rd(); }
+      if constexpr (NRU > 2 && ks == WR2) { if (rnd == 2) wr(); }
+      if constexpr (ks == KS - 2) stores();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    ks_unroll(mk, std::make_integer_sequence<int, KS>{});
+    // (a rank is < U by construction -- at most U rows per unit -- so the
+    // cap k < U never binds; it bounds the loop whatever dres holds)
+    for (int k = NRU; k < U && __ballot(rnd >= k && rnd != 0xffff) != 0ull; ++k)
+      if (rnd == k) {
+        rd();
+        wr();
+      }
     load(r, tt + KP_AHEAD);
+    __builtin_amdgcn_sched_barrier(0);
+    if (mf && scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cc0, ones, acc0, 0, 0, 0);
+    if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cc1, ones, acc1, 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
 

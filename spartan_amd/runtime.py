@@ -7,12 +7,15 @@ running the same (SPMD) program.  A tile *worker* index (the reference's
 ``TileId.worker``, spartan/core.pyx:16-41) is owned by rank ``worker % world``.
 Every rank computes the same tile plan, runs the kernels for the tiles it owns
 on its own GPU, and exchanges data through RCCL collectives over xGMI.  By
-default (world > 1 on GPUs) they are issued through libspx.so's C ABI
-(``spx_allreduce`` & co., comm.py) on a communicator this module creates, with
-torch.distributed (gloo) as the host control plane; a start-up self-test falls
-back to torch.distributed's own RCCL process group if that communicator
-cannot be created or computes a wrong result.  gloo alone carries the
-CPU-only tests.
+default (world > 1 on GPUs) they run on torch.distributed's RCCL process group
+(backend 'nccl' = RCCL on ROCm); ``SPARTAN_DIST_BACKEND=rccl`` issues them
+through libspx.so's C ABI instead (``spx_allreduce`` & co., comm.py) on a
+communicator this module creates, with torch.distributed (gloo) as the host
+control plane and a start-up self-test that falls back to torch's RCCL group
+if that communicator cannot be created or computes a wrong result.  The libspx
+communicator stays opt-in until a multi-GPU run has validated it (it has
+completed collectives at world 1 only).  gloo alone carries the CPU-only
+tests.
 """
 import os
 
@@ -64,12 +67,16 @@ class Context:
 
 
 def data_plane(device_type, env=None):
-  """The device-collective backend a multi-rank run starts with: 'rccl' (the
-  libspx C-ABI communicator) on GPUs unless SPARTAN_DIST_BACKEND names
-  another ('nccl': torch's RCCL group; 'gloo': host-staged rehearsal); 'gloo'
-  for CPU devices (tests)."""
+  """The device-collective backend a multi-rank run starts with: 'nccl'
+  (torch.distributed's RCCL group) on GPUs unless SPARTAN_DIST_BACKEND names
+  another ('rccl': the libspx C-ABI communicator, self-tested at start-up
+  with a fallback to 'nccl'; 'gloo': host-staged rehearsal); 'gloo' for CPU
+  devices (tests).  A collective that hangs on the libspx communicator keeps
+  its HIP stream blocked, so no fallback can rescue it: that is why 'rccl'
+  stays opt-in until a multi-GPU run has shown selftest='ok' with correct
+  results."""
   env = os.environ if env is None else env
-  backend = env.get('SPARTAN_DIST_BACKEND', 'rccl' if device_type == 'cuda' else 'gloo')
+  backend = env.get('SPARTAN_DIST_BACKEND', 'nccl' if device_type == 'cuda' else 'gloo')
   if backend not in ('nccl', 'rccl', 'gloo'):
     raise ValueError('SPARTAN_DIST_BACKEND must be nccl, rccl or gloo, not %r' % backend)
   if backend == 'rccl' and (env.get('SPARTAN_COMM') == 'torch' or device_type != 'cuda'):
@@ -110,17 +117,19 @@ def initialize(argv=None, device=None):
 
   Reads RANK / WORLD_SIZE / LOCAL_RANK from the torchrun environment and
   selects cuda:LOCAL_RANK.  With more than one rank on GPUs the data plane
-  is, by default, libspx.so's C-ABI RCCL communicator (``'rccl'``:
-  spx_comm_init, every device collective an ``spx_*`` call, comm.py), with
-  torch.distributed running gloo as the host control plane (the unique-id
-  hand-off, barriers, host maxima, the SPMD guard).  The communicator's
-  creation is bounded (``SPARTAN_RCCL_INIT_TIMEOUT`` s, default 120) and a
-  start-up self-test checks every collective on every rank; if either fails
-  on any rank, all ranks switch the device collectives to torch.distributed's
-  own RCCL process group (loudly) and re-run the test.
-  ``SPARTAN_DIST_BACKEND=nccl`` selects torch's RCCL group directly (the
-  control plane then gets its own gloo group), ``SPARTAN_DIST_BACKEND=gloo``
-  rehearses N ranks on fewer GPUs (device tensors staged through the host).
+  is, by default, torch.distributed's RCCL process group (``'nccl'``; the
+  control plane then gets its own gloo group).  ``SPARTAN_DIST_BACKEND=rccl``
+  selects libspx.so's C-ABI RCCL communicator (spx_comm_init, every device
+  collective an ``spx_*`` call, comm.py), with torch.distributed running gloo
+  as the host control plane (the unique-id hand-off, barriers, host maxima,
+  the SPMD guard).  That communicator's creation is bounded
+  (``SPARTAN_RCCL_INIT_TIMEOUT`` s, default 120) and a start-up self-test
+  checks every collective on every rank; if either fails on any rank, all
+  ranks switch the device collectives to torch.distributed's own RCCL process
+  group (loudly) and re-run the test on a fresh stream -- a collective that
+  HANGS on the libspx communicator is fatal (its stream stays blocked).
+  ``SPARTAN_DIST_BACKEND=gloo`` rehearses N ranks on fewer GPUs (device
+  tensors staged through the host).
   ``device`` overrides the device (tests run the host logic on 'cpu' with a
   test backend and gloo)."""
   global _ctx
@@ -195,7 +204,13 @@ def _fall_back_to_torch_rccl(err):
   _ctx.pg = dist.new_group(backend='nccl')
   _ctx.dist_backend = 'nccl'
   _ctx.rccl = None  # not destroyed: a communicator in an unknown state may block in ncclCommDestroy
-  bad = comm.selftest()
+  import torch
+  if _ctx.device.type == 'cuda':
+    # a fresh stream: the failed test's work may still sit on the current one
+    with torch.cuda.stream(torch.cuda.Stream(device=_ctx.device)):
+      bad = comm.selftest()
+  else:
+    bad = comm.selftest()
   _ctx.selftest = 'fallback (%s)' % err
   if bad:
     raise RuntimeError('spartan_amd: no working GPU data plane (libspx RCCL: %s; torch RCCL: %s)' % (err, bad))

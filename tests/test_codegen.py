@@ -102,3 +102,18 @@ def test_rowdot_cols_fixed_lane_groups(dt):
   # without a fixed width: the run-time form (aux[2]) and no broadcasts
   src = codegen.gen_reduce(root, ins, ['c', 'b', 'c'], 'cols', 'sum', V, 8, (2,))
   assert 'lpr_log = a.aux[2]' in src and 'yb1' not in src
+
+
+@pytest.mark.parametrize("rdt", [B, np.dtype(np.int8), np.dtype(np.int16)])
+def test_rowdot_narrow_row_input_compiles(rdt):
+  """A per-row input narrower than 4 bytes (a bool row mask, int8, int16) in
+  the fixed-width row-dot kernel keeps its per-row load: dpp_mov moves whole
+  dwords, so only 4- and 8-byte row inputs are DPP-broadcast."""
+  from spartan_amd.codegen import RowDot
+  x, yv, w, m = In(0, F32), In(1, F32), In(2, F32), In(3, rdt)
+  root = Op('multiply', [Op('multiply', [x, Op('subtract', [RowDot(x, w), yv])]), Cast(m, F32)])
+  ins = [(0, F32), (1, F32), (2, F32), (3, rdt)]
+  V = codegen.vec_width([F32])
+  src = codegen.gen_reduce(root, ins, ['c', 'b', 'c', 'b'], 'cols', 'sum', V, 8, (2,), lpr=16, full=True)
+  assert 'yb1' in src and 'yb3' not in src
+  _compile(src)

@@ -240,13 +240,15 @@ def test_world2_gloo(W):
     assert res.get(r) == 'ok', res.get(r)
 
 
-def test_default_data_plane_is_libspx_rccl():
-  """Round 4: at world > 1 on GPUs the device collectives default to the
-  libspx C-ABI RCCL communicator; SPARTAN_DIST_BACKEND overrides; CPU runs
-  use gloo."""
+def test_default_data_plane_is_torch_rccl():
+  """Round 5: at world > 1 on GPUs the device collectives default to
+  torch.distributed's RCCL group ('nccl'); the libspx C-ABI communicator is
+  opt-in (SPARTAN_DIST_BACKEND=rccl) until a multi-GPU run validates it; CPU
+  runs use gloo."""
   import pytest
   from spartan_amd import runtime
-  assert runtime.data_plane('cuda', {}) == 'rccl'
+  assert runtime.data_plane('cuda', {}) == 'nccl'
+  assert runtime.data_plane('cuda', {'SPARTAN_DIST_BACKEND': 'rccl'}) == 'rccl'
   assert runtime.data_plane('cuda', {'SPARTAN_DIST_BACKEND': 'nccl'}) == 'nccl'
   assert runtime.data_plane('cuda', {'SPARTAN_DIST_BACKEND': 'gloo'}) == 'gloo'
   assert runtime.data_plane('cuda', {'SPARTAN_COMM': 'torch'}) == 'nccl'

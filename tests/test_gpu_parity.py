@@ -1439,3 +1439,53 @@ def test_kmeans_step_same_row_units(ex, N):
   P = torch.as_tensor(np.tile(row, (N, 1))).cuda()
   lab, cnt = _step_check_all(be, P, torch.as_tensor(C).cuda())
   assert int(cnt[17]) == N
+
+
+def test_kmeans_step_far_undecided_outliers(ex):
+  """a row the screen cannot decide was added provisionally to
+  its screen-best centre p and moved in fp64 afterwards if its final label
+  differed -- leaving the fp32 rounding of ITS add in p's window chain.  For
+  a far outlier that rounding dominates p's sum.  Here 64 outliers sit
+  midway between two centres a, b (final label a by a 1e-4 nudge, the fp16
+  screen picks either) with a 2e4 component in one of the dims 120-127 where
+  every centre and every other row is ~0 (tiny values), so element (b, d) of
+  the sums has sum |x| of only ~1e-3 per row: a mover's fp32 add of 2e4 into
+  it swallows every later add there (error >> 1e-5 sum |x|).  Far rows must
+  stay out of the provisional adds (gathered in fp64 instead): labels exact,
+  counts exact, every element within 1e-5 of the fp64 sum |x|."""
+  import torch
+  from spartan_amd import backend
+  be = backend.get()
+  g = np.random.default_rng(2024)
+  N, D, K = 300_000, 128, 8
+  C = np.zeros((K, D))
+  C[:, :120] = g.random((K, 120))
+  pts = np.zeros((N, D), dtype=np.float32)
+  pts[:, :120] = g.random((N, 120))
+  pts[:, 120:] = 1e-3 * g.random((N, 8))
+  rows = g.choice(N, 64, replace=False)
+  for i, r in enumerate(rows):
+    a, b = i % K, (i + 1) % K
+    mid = 0.5 * (C[a, :120] + C[b, :120]) + 1e-4 * (C[a, :120] - C[b, :120])
+    pts[r, :120] = mid
+    pts[r, 120 + i % 8] = 2e4
+  P = torch.as_tensor(pts).cuda()
+  Cd = torch.as_tensor(C).cuda()
+  lab = torch.empty((N,), dtype=torch.int64, device='cuda')
+  sums = torch.empty((K, D), dtype=torch.float64, device='cuda')
+  cnt = torch.empty((K,), dtype=torch.int64, device='cuda')
+  be.kmeans_step(P, Cd, lab, sums, cnt)
+  exact = torch.empty_like(lab)
+  be.kmeans_assign(P, Cd, exact, exact_only=True)
+  assert torch.equal(lab, exact)
+  L = lab.cpu().numpy()
+  assert np.array_equal(L[rows], np.arange(64) % K)   # the nudge decides, as built
+  np.testing.assert_array_equal(cnt.cpu().numpy(), np.bincount(L, minlength=K))
+  p64 = pts.astype(np.float64)
+  ws = np.zeros((K, D))
+  wa = np.zeros((K, D))
+  np.add.at(ws, L, p64)
+  np.add.at(wa, L, np.abs(p64))
+  s = sums.cpu().numpy()
+  err = np.abs(s - ws) / wa
+  assert err.max() <= 1e-5, 'max |sum - fp64| / sum |x| = %.3g at %s' % (err.max(), np.unravel_index(err.argmax(), err.shape))

@@ -84,6 +84,26 @@ for s in $STEPS; do
       # the same on first-iteration centres (the first K points: skewed labels, more add rounds)
       cd /tmp && step kftrace 300 rocprofv3 --kernel-trace --stats -d $O/kftrace -o p --output-format csv \
         -- python3 $R/tools/km_step_once.py 100000000 5 first > $O/kftrace.log 2>&1 ;;
+    kab)
+      # A/B of libspx builds on one box: the fused step under a kernel trace,
+      # each build twice in alternation (KAB: names of tools/bin/libspx_NAME.so,
+      # 'product' = spartan_amd/libspx.so); the fused kernel's time per call
+      # is in $O/kab_NAME_i/p_kernel_stats.csv
+      for i in 1 2; do
+        for v in ${KAB:-base product}; do
+          lib=$R/tools/bin/libspx_$v.so; [ $v = product ] && lib=$R/spartan_amd/libspx.so
+          cd /tmp && step kab_${v}_$i 120 rocprofv3 --kernel-trace --stats -d $O/kab_${v}_$i -o p --output-format csv \
+            -- python3 $R/tools/km_step_once.py 100000000 5 step $lib > $O/kab_${v}_$i.log 2>&1
+        done
+      done ;;
+    kclk)
+      # clock and wave-state counters of the fused step per build (KAB names)
+      for v in ${KAB:-product}; do
+        lib=$R/tools/bin/libspx_$v.so; [ $v = product ] && lib=$R/spartan_amd/libspx.so
+        cd /tmp && step kclk_$v 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY \
+          SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU \
+          -d $O/kclk_$v -o p --output-format csv -- python3 $R/tools/km_step_once.py 100000000 2 step $lib > $O/kclk_$v.log 2>&1
+      done ;;
     kundtrace)
       cd /tmp && step kundtrace 300 rocprofv3 --kernel-trace --stats -d $O/kundtrace -o p --output-format csv \
         -- python3 $R/tools/km_und.py 100000000 > $O/kundtrace.log 2>&1 ;;
