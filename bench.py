@@ -113,6 +113,7 @@ def main():
     a1 = expr.sum(X * Y + expr.exp(Z), axis=1).optimized().force()
     return a0, a1
 
+  cold = cold_start(expr, X, Y, Z, sync)
   for _ in range(args.warmup):
     step()
   sync()
@@ -183,6 +184,10 @@ def main():
                    'axis1_ms': round(float(np.mean(ax1)) * 1e3, 4) if ax1 else None},
   }
   result['checked'] = check_cfg2(last, x, y, z, R, S)
+  result['cold_start'] = cold
+  # SURVEY 8(d) cfg2 also: axis=None, and the materialised map (16 B/elem)
+  result['cfg2_axis_none'] = bench_cfg2_extra('none', X, Y, Z, x, y, z, R, S, rows_local, be, expr, comm, sync)
+  result['cfg2_map'] = bench_cfg2_extra('map', X, Y, Z, x, y, z, R, S, rows_local, be, expr, comm, sync)
   del x, y, z, X, Y, Z, last
   torch.cuda.empty_cache()
 
@@ -293,6 +298,115 @@ def _ranks_seen():
   return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
+def cold_start(expr, X, Y, Z, sync):
+  """First evaluation in the process of sum(x*y+exp(z), axis=0).optimized()
+  .force() (DAG rewrite, plan, codegen, code-object load from the build()-time
+  cache, module load, the kernel itself), the second one (steady state: plan
+  replay, kernel), and the device compiler's time for that kernel's source
+  when it is in no cache (a salted copy, compiled into a temporary cache)."""
+  import tempfile
+  from spartan_amd import backend, codegen
+  from spartan_amd.config import FLAGS
+  out = {}
+  for k in ('first_eval_ms', 'second_eval_ms'):
+    sync()
+    t0 = time.perf_counter()
+    expr.sum(X * Y + expr.exp(Z), axis=0).optimized().force()
+    sync()
+    out[k] = round((time.perf_counter() - t0) * 1e3, 3)
+  f32 = np.dtype(np.float32)
+  In, Op = codegen.In, codegen.Op
+  tree = Op('add', [Op('multiply', [In(0, f32), In(1, f32)]), Op('exp', [In(2, f32)])])
+  src, _ = codegen.named(codegen.gen_reduce(tree, [(0, f32), (1, f32), (2, f32)], ['c'] * 3, 'cols', 'sum',
+                                            codegen.vec_width([f32])), 'spx_reduce', 'cols')
+  prev = FLAGS.kernel_cache_dir
+  try:
+    with tempfile.TemporaryDirectory() as td:
+      FLAGS.kernel_cache_dir = td
+      t0 = time.perf_counter()
+      backend.compile_code_object(src + '\n// cold-start probe %d %f\n' % (os.getpid(), time.time()))
+      out['compile_ms'] = round((time.perf_counter() - t0) * 1e3, 1)
+  except Exception as e:  # noqa: BLE001  (no device compiler: report, do not fail the bench)
+    out['compile_ms'] = None
+    out['compile_error'] = '%s: %s' % (type(e).__name__, str(e)[:200])
+  finally:
+    FLAGS.kernel_cache_dir = prev
+  out['note'] = ('first_eval_ms: the first .optimized().force() of the cfg2 axis-0 sum in this process (kernel '
+                 'from the build()-time code-object cache); compile_ms: device clang for that source uncached')
+  return out
+
+
+def bench_cfg2_extra(kind, X, Y, Z, x, y, z, R, S, rows_local, be, expr, comm, sync, steps=10, warm=2):
+  """SURVEY 8(d) cfg2 extras: 'none' = sum(x*y+exp(z)) over all elements
+  (per-rank partial, all-reduce; 12 B/elem), 'map' = the materialised map
+  (x*y+exp(z)).optimized().force() (16 B/elem: three reads, one write).
+  Wall time over ``steps`` evaluations (barrier + synchronize on both
+  sides, max over ranks) and the generated kernel's HIP-event time."""
+  import torch
+
+  def ev():
+    if kind == 'none':
+      return expr.sum(X * Y + expr.exp(Z)).optimized().force()
+    return (X * Y + expr.exp(Z)).optimized().force()
+  for _ in range(warm):
+    r = ev()
+    del r
+  sync()
+  comm.barrier()
+  sync()
+  be.kernel_events = []
+  t0 = time.perf_counter()
+  for _ in range(steps):
+    r = ev()
+    if kind == 'map':
+      last = r
+    del r
+  sync()
+  comm.barrier()
+  sync()
+  el = comm.max_over_ranks(time.perf_counter() - t0)
+  events = be.kernel_events
+  be.kernel_events = None
+  pre = 'spx_reduce' if kind == 'none' else 'spx_map'
+  ks = [s_.elapsed_time(e_) * 1e-3 for (n, s_, e_) in events if n.startswith(pre)]
+  per_elem = 12 if kind == 'none' else 16
+  nbytes = per_elem * R * S
+  blaunch = per_elem * rows_local * S
+  kavg = float(np.mean(ks)) if ks else None
+  out = {'GBps': round(nbytes * steps / el / 1e9, 1), 'ms_per_eval': round(el / steps * 1e3, 4),
+         'kernel_ms': round(kavg * 1e3, 4) if kavg else None,
+         'roofline': {'bound': 'hbm', 'achieved': round(blaunch / kavg / 1e9, 1) if kavg else None,
+                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                      'frac': round(blaunch / kavg / 1e9 / HBM_PEAK_GBS, 4) if kavg else None,
+                      'bytes_per_launch': blaunch,
+                      'kernel': ' / '.join(sorted({n for (n, _, _) in events if n.startswith(pre)}))}}
+  if kind == 'none':
+    want = None
+    got = float(expr.sum(X * Y + expr.exp(Z)).optimized().glom())
+    # against the (already checked) axis-1 sums, summed in fp64
+    want = float(expr.sum(expr.astype(expr.sum(X * Y + expr.exp(Z), axis=1), np.float64)).glom())
+    out['checked'] = _rel_ok(got, want, 1e-5)
+    out['config'] = 'sum(x*y+exp(z)) (axis=None), %d x %d fp32' % (R, S)
+  else:
+    from spartan_amd.array import distarray, extent as ext
+    ok = True
+    for i in (0, R // 2, R - 1):
+      reg = ext.create((i, 0), (i + 1, S), (R, S))
+      xr, yr, zr = (distarray.glom_region(t, reg).astype(np.float64).ravel() for t in (x, y, z))
+      got = distarray.glom_region(last, reg).astype(np.float64).ravel()
+      ok &= _rel_ok(got, xr * yr + np.exp(zr), 1e-6)
+    out['checked'] = bool(ok)
+    out['config'] = '(x*y+exp(z)).optimized().force(): materialised (%d, %d) fp32 result' % (R, S)
+    del last
+  torch.cuda.empty_cache()
+  return out
+
+
+def _kernel_ms(events, prefix):
+  ks = [s_.elapsed_time(e_) for (n, s_, e_) in events if n.startswith(prefix)]
+  return float(np.mean(ks)) if ks else None
+
+
 def bench_dot(S, ctx, be, expr, comm, sync, runs=10, warm=2):
   """dot(A, B) for S x S fp32 and fp64 (configs[3]); GFLOP/s over all ranks.
   SURVEY.md 8(d): median of ``runs`` timed evaluations after ``warm``
@@ -307,6 +421,7 @@ def bench_dot(S, ctx, be, expr, comm, sync, runs=10, warm=2):
       c = expr.dot(A, B).force()
       del c
     times = []
+    be.kernel_events = []
     for _ in range(runs):
       sync()
       comm.barrier()
@@ -319,6 +434,9 @@ def bench_dot(S, ctx, be, expr, comm, sync, runs=10, warm=2):
       times.append(comm.max_over_ranks(time.perf_counter() - t0))
       if len(times) < runs:
         del c
+    events = be.kernel_events
+    be.kernel_events = None
+    gemm_ms = [s_.elapsed_time(e_) for (n, s_, e_) in events if n == 'spx_gemm']
     checked = check_dot(c, A, B, S, dt, expr)
     del c
     el = float(np.median(times))
@@ -328,6 +446,11 @@ def bench_dot(S, ctx, be, expr, comm, sync, runs=10, warm=2):
                  'seconds_min_max': [round(min(times), 4), round(max(times), 4)],
                  'mfma_frac_per_gpu': round(flops / el / 1e12 / (peak * ctx.world_size), 4),
                  'checked': checked}
+    if gemm_ms and ctx.world_size == 1:
+      # the dominant kernel alone: spx_gemm's HIP-event time per dot (one call per dot at N = 1)
+      km = float(np.sum(gemm_ms)) / runs
+      out[name]['kernel_ms'] = round(km, 3)
+      out[name]['kernel_mfma_frac'] = round(flops / (km * 1e-3) / 1e12 / peak, 4)
     del a, b, A, B
     torch.cuda.empty_cache()
   out['config'] = ('dot(A, B), A, B ~ U[0,1) (%d, %d), K-split over ranks; median of %d runs after %d warm-ups'
@@ -418,6 +541,9 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
   from spartan_amd import workloads
   X = expr.rand(npts * ctx.world_size, D, dtype=np.float32, seed=21).force()
   workloads.kmeans_fit(X, K, iters)      # warm-up (every path of the timed loop) from the first K points
+  from spartan_amd import backend
+  be = backend.get()
+  be.kmeans_timing(True)  # HIP events around the one-pass kernel of each step (no host sync inside)
   sync()
   comm.barrier()
   t0 = time.perf_counter()
@@ -426,6 +552,8 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
   sync()
   comm.barrier()
   el = comm.max_over_ranks(time.perf_counter() - t0) / iters
+  kt = be.kmeans_times()
+  be.kmeans_timing(False)
   checked = check_kmeans(X, labels, info['assign_centers'], comm)
   checked_sums = check_kmeans_sums(X, labels, info['sums'], info['counts'], comm)
   n = npts * ctx.world_size
@@ -439,6 +567,12 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
          'f16_mfma_frac_per_gpu': round(2.0 * n * K * D / el / 1e12 / (2500.0 * ctx.world_size), 4),
          'hbm_GBps_one_pass': round(4.0 * n * D / el / 1e9, 1),
          'checked': checked and checked_sums, 'checked_labels': checked, 'checked_sums_counts': checked_sums,
+         'kernel_ms': [round(a, 3) for a, _ in kt], 'step_ms': [round(b, 3) for _, b in kt],
+         'kernel_hbm_frac': (round(4.0 * npts * D / (float(np.mean([a for a, _ in kt])) * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                   4) if kt else None),
+         'kernel_note': 'kernel_ms / step_ms: HIP events (spx_kmeans_timing) around k_kmeans_pp (the one-pass '
+                        'screen + accumulation) and around the whole spx_kmeans_step, per iteration; '
+                        'kernel_hbm_frac = the points (4 N D bytes, read once) / mean kernel_ms / 8 TB/s',
          'config': 'cfg3: %d x %d fp32 points (U[0,1), seed 21) per GPU, k=%d, centres = first %d points; '
                    'spx_kmeans_step: certified fp16-MFMA screen + per-centre sums of the rows it decides in one '
                    'pass over X, bf16x3-MFMA pass + exact-order fp64 recompute of its undecided rows (bit-exact '
@@ -520,13 +654,21 @@ def bench_lreg(npts, ctx, expr, comm, sync, D=64, iters=30):
   w = np.random.default_rng(43).random((D, 1)).astype(np.float32)
   Xe, Ye = expr.lazify(X), expr.lazify(Y)
   workloads.sgd_train(Xe, Ye, w, 1e-6, 2)  # warm-up (kernel compile / load, plan caches)
+  from spartan_amd import backend
+  be = backend.get()
   sync()
   comm.barrier()
+  be.kernel_events = []
   t0 = time.perf_counter()
   w_end = workloads.sgd_train(Xe, Ye, w, 1e-6, iters)
   sync()
   comm.barrier()
   el = comm.max_over_ranks(time.perf_counter() - t0) / iters
+  events = be.kernel_events
+  be.kernel_events = None
+  # the fused gradient kernel (generated spx_reduce_cols_*) and every kernel of the iteration
+  kred = _kernel_ms(events, 'spx_reduce')
+  kall = sum(s_.elapsed_time(e_) for (_, s_, e_) in events) / iters
   # checked at the starting w: the reference's step size (sgd.py:14, alpha =
   # 1e-6) diverges at this N, so after 30 steps w and the gradient have left
   # the fp32 range; the replayed plan and kernel are the ones timed
@@ -534,8 +676,15 @@ def bench_lreg(npts, ctx, expr, comm, sync, D=64, iters=30):
   del w_end
   n = npts * ctx.world_size
   nbytes = 4.0 * n * D + 4.0 * n   # one pass: X and y read once (DotReduceFusion)
+  nloc = nbytes / ctx.world_size
   out = {'ms_per_iter': round(el * 1e3, 3), 'algorithmic_GBps': round(nbytes / el / 1e9, 1),
          'hbm_frac_per_gpu': round(nbytes / el / 1e9 / (HBM_PEAK_GBS * ctx.world_size), 4),
+         'kernel_ms': round(kred, 4) if kred else None,
+         'kernel_hbm_frac': round(nloc / (kred * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if kred else None,
+         'device_ms_per_iter': round(kall, 4),
+         'kernel_note': 'kernel_ms: HIP events around the fused gradient kernel (X and y read once: 4 N (d + 1) '
+                        'bytes); device_ms_per_iter: every kernel of an iteration (gradient, finalize, w update); '
+                        'ms_per_iter - device_ms_per_iter = launch gaps and host work',
          'checked': checked,
          'config': 'cfg5: X %d x %d fp32, y %d x 1, w 64 x 1 (device-resident between iterations, '
                    'w - grad * alpha as a device map: no per-iteration host round trip); grad = sum(x * (dot(x, '

@@ -133,8 +133,8 @@ int spx_copy_region(int dst_dtype, void* dst, const int64_t* dst_shape,
  * dot_map2_mapper (spartan/expr/dot.py:195-212), dot_outer_mapper (:217-233)
  * and dot_map2_np_mapper (:172-187).
  * Memory: C must be coarse-grained device memory (hipMalloc / a torch CUDA
- * tensor).  The fp32 kernel flushes its accumulators into C every 1024
- * K-tiles (fp32 chains of <= 8192 MFMA steps at any K): with K > 16384, or
+ * tensor).  The fp32 kernel flushes its accumulators into C every 512
+ * K-tiles (fp32 chains of <= 4096 MFMA steps at any K): with K > 8192, or
  * with beta != 0, C is updated by no-return fp32 atomic adds, which are not
  * reliably performed on fine-grained or host-coherent allocations.  One wave
  * owns each element of C, so the adds land in program order (deterministic).
@@ -213,6 +213,14 @@ int spx_kmeans_accumulate(int dtype, int64_t N, int64_t D, int64_t K, const void
  * Other shapes run the two calls.  workspace_bytes >=
  * spx_kmeans_step_workspace(dtype, N, D, K). */
 int64_t spx_kmeans_step_workspace(int dtype, int64_t N, int64_t D, int64_t K);
+/* Timing aid (bench / profiling): spx_kmeans_timing(1) makes every later
+ * fused spx_kmeans_step record HIP events on its stream around its one-pass
+ * kernel and around the whole step (up to 256 calls; 0 turns it off and frees
+ * the events).  spx_kmeans_times waits for the recorded calls and writes their
+ * kernel / whole-step device times (ms) in call order, clears the record and
+ * returns how many it wrote (< 0 on error). */
+int spx_kmeans_timing(int enable);
+int spx_kmeans_times(double* fused_ms, double* step_ms, int max);
 int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const void* points, int64_t ldp,
                     const double* centers, int64_t* labels, double* sums, uint64_t* counts, int zero_first,
                     void* workspace, size_t workspace_bytes, int dist_dtype, void* stream);

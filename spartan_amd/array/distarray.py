@@ -350,6 +350,43 @@ def gather_regions(array, requests):
   {request index: device tensor} for the requests addressed to this rank."""
   if hasattr(array, 'gather'):  # a view (array/views.py): the same exchange on its base
     return array.gather(requests)
+  return _gather_plan(array, requests, False).finish()
+
+
+class _Gather:
+  """A gather in flight: ``finish`` makes the current stream wait for the
+  messages, stitches the received pieces into their buffers and returns
+  {request index: device tensor}."""
+
+  def __init__(self, out, handle, post):
+    self.out, self.handle, self.post = out, handle, post
+
+  def finish(self):
+    if self.handle is not None:
+      comm.wait_all([self.handle])
+      self.handle = None
+    be = backend.get()
+    for buf, rel, tmp, shape in self.post:
+      be.copy_region(buf, rel, tmp, (0,) * len(shape), shape)
+    self.post = []
+    return self.out
+
+
+def gather_regions_async(array, requests):
+  """``gather_regions`` whose messages run beside the current stream
+  (comm.exchange_async): returns a handle; its ``finish()`` (later, in the
+  same order on every rank) yields the tensors.  Lets a caller start the next
+  pieces' transfers while it computes on the pieces it already has (the
+  overlapped K-split dot, expr/dot.py).  A received piece that covers whole
+  rows of its request lands in the request's buffer directly (no staging
+  copy)."""
+  if hasattr(array, 'gather'):
+    out = array.gather(requests)
+    return _Gather(out, None, [])
+  return _gather_plan(array, requests, True)
+
+
+def _gather_plan(array, requests, asynchronous):
   import torch
   ctx = runtime.get()
   be = backend.get()
@@ -374,13 +411,24 @@ def gather_regions(array, requests):
       elif src == ctx.rank:
         sends.append((_sub_tensor(array.local[ex], inter).contiguous(), dst))
       elif dst == ctx.rank:
+        rel = _rel(inter, region)
+        if asynchronous and _whole_rows(rel, inter.shape, region.shape):
+          # rows [r0, r1) of a row-major buffer: one contiguous slice, received in place
+          recvs.append((buf.reshape(region.shape[0], -1)[rel[0]:rel[0] + inter.shape[0]], src))
+          continue
         tmp = torch.empty(inter.shape, dtype=tdt, device=ctx.device)
         recvs.append((tmp, src))
-        post.append((buf, _rel(inter, region), tmp, inter.shape))
+        post.append((buf, rel, tmp, inter.shape))
+  if asynchronous:
+    return _Gather(out, comm.exchange_async(sends, recvs), post)
   comm.exchange(sends, recvs)
-  for buf, rel, tmp, shape in post:
-    be.copy_region(buf, rel, tmp, (0,) * len(shape), shape)
-  return out
+  return _Gather(out, None, post)
+
+
+def _whole_rows(rel, shape, full):
+  """True when a piece at offset ``rel`` (a tuple) of ``shape`` spans every
+  trailing dim of the ``full`` buffer (so it is a contiguous row range)."""
+  return len(full) >= 1 and tuple(shape[1:]) == tuple(full[1:]) and all(u == 0 for u in rel[1:])
 
 
 def glom(array):

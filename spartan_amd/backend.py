@@ -98,6 +98,9 @@ _SIGS = {
     'spx_kmeans_step': ([ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                          ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                          ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
+    'spx_kmeans_timing': ([ctypes.c_int], ctypes.c_int),
+    'spx_kmeans_times': ([ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.c_int],
+                         ctypes.c_int),
     'spx_cdist': ([ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                    ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p], ctypes.c_int),
     'spx_bincount': ([ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int,
@@ -295,6 +298,32 @@ class HipBackend:
       self._fns[key] = f
       self._names[f.value] = name
       return f
+
+  def _aot_events(self, name):
+    """(start, end) HIP events around one ahead-of-time libspx call on the
+    current stream when bench timing is on (kernel_events), else None."""
+    if self.kernel_events is None:
+      return None
+    import torch
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    ev[0].record()
+    self.kernel_events.append((name, ev[0], ev[1]))
+    return ev
+
+  def kmeans_timing(self, enable):
+    """Record HIP events around the one-pass kernel of every later fused
+    spx_kmeans_step (bench.py's k-means kernel roofline)."""
+    _check(self.lib.spx_kmeans_timing(1 if enable else 0), 'spx_kmeans_timing')
+
+  def kmeans_times(self, max_calls=256):
+    """[(fused kernel ms, whole step ms)] of the steps recorded since
+    kmeans_timing(True) or the last call (waits for them)."""
+    a = (ctypes.c_double * max_calls)()
+    b = (ctypes.c_double * max_calls)()
+    n = self.lib.spx_kmeans_times(a, b, max_calls)
+    if n < 0:
+      _check(n, 'spx_kmeans_times')
+    return [(a[i], b[i]) for i in range(n)]
 
   def launch(self, fn, grid, args):
     if self.launch_log is not None:
@@ -686,9 +715,12 @@ class HipBackend:
     K2, N = B.shape
     assert K == K2 and tuple(C.shape) == (M, N)
     dt = np_dtype(A.dtype)
+    ev = self._aot_events('spx_gemm')
     _check(self.lib.spx_gemm(spx_dtype(dt), M, N, K, ctypes.c_void_p(A.data_ptr()), A.stride(0),
                              ctypes.c_void_p(B.data_ptr()), B.stride(0), ctypes.c_void_p(C.data_ptr()),
                              C.stride(0), float(alpha), float(beta), self.stream()), 'spx_gemm')
+    if ev is not None:
+      ev[1].record()
 
 
   # --------------------------------------------------------------- k-means

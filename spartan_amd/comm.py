@@ -2,17 +2,18 @@
 
 Data plane, by ``ctx.dist_backend``:
 
-* ``'rccl'`` (the GPU default at N > 1): every collective is a libspx.so
-  C-ABI call (``spx_allreduce`` / ``spx_reduce_scatter`` / ``spx_allgather``
-  / ``spx_broadcast`` / ``spx_reduce`` / ``spx_sendrecv``, include/spx.h) on
+* ``'nccl'`` (the GPU default at N > 1): torch.distributed's RCCL process
+  group (PyTorch's librccl; 'nccl' is RCCL on ROCm), also the fallback when
+  the libspx communicator cannot be created or fails its start-up self-test
+  (``selftest``).  The control plane runs on a gloo group of its own.
+* ``'rccl'`` (opt-in, ``SPARTAN_DIST_BACKEND=rccl``, until a multi-GPU run
+  validates it): every collective is a libspx.so C-ABI call
+  (``spx_allreduce`` / ``spx_reduce_scatter`` / ``spx_allgather`` /
+  ``spx_broadcast`` / ``spx_reduce`` / ``spx_sendrecv``, include/spx.h) on
   the RCCL communicator the runtime created, enqueued on the current HIP
   stream.  torch.distributed (gloo) is the host control plane only: the
   unique-id hand-off, ``barrier``, the SPMD guard and ``max_over_ranks`` of
   host floats.
-* ``'nccl'``: torch.distributed's own RCCL process group (PyTorch's
-  librccl): ``SPARTAN_DIST_BACKEND=nccl``, or the fallback when the libspx
-  communicator cannot be created or fails its start-up self-test
-  (``selftest``).  The control plane then runs on a gloo group of its own.
 * ``'gloo'``: CPU tests, and the one-GPU multi-rank rehearsal
   (``SPARTAN_DIST_BACKEND=gloo``), where device tensors are staged through
   host memory.
@@ -316,6 +317,72 @@ def wait_all(handles):
       h.wait()
 
 
+class _Works:
+  """torch.distributed async works; ``wait`` makes the current stream wait
+  for them (NCCL works do not block the host)."""
+
+  def __init__(self, works, keep):
+    self.works = works
+    self.keep = keep
+
+  def wait(self):
+    for w in self.works:
+      w.wait()
+    self.keep = None
+
+
+def exchange_async(sends, recvs):
+  """``exchange`` that runs beside the current stream: the messages start
+  after the work already queued on it (the sends' producers) and run
+  concurrently with what follows; returns a handle whose ``wait`` makes the
+  current stream wait for the received tensors (``wait_all``), or None when
+  the exchange already completed (gloo: host-staged, synchronous).  Same
+  matching rules and SPMD contract as ``exchange``."""
+  ctx = runtime.get()
+  if not ctx.distributed:
+    return None
+  if ctx.dist_backend == 'gloo':
+    exchange(sends, recvs)
+    return None
+  _guard('exchange')
+  if not sends and not recvs:
+    return None
+  import torch
+  sends = [(t.contiguous(), peer) for t, peer in sends]
+  if ctx.dist_backend == 'rccl':
+    cur = torch.cuda.current_stream()
+    side = ctx.comm_stream()
+    ready = torch.cuda.Event()
+    ready.record(cur)
+    side.wait_event(ready)
+    with torch.cuda.stream(side):
+      _exchange_rccl(sends, recvs)
+    done = torch.cuda.Event()
+    done.record(side)
+    return _Pending(done, (sends, recvs))
+  dist = _dist()
+  g = _grp()
+  ops = [dist.P2POp(dist.isend, t, peer, group=g) for t, peer in sends]
+  ops += [dist.P2POp(dist.irecv, t, peer, group=g) for t, peer in recvs]
+  return _Works(dist.batch_isend_irecv(ops), (sends, recvs))
+
+
+def _exchange_rccl(sends, recvs):
+  """spx_sendrecv of one batch on the current stream (libspx RCCL plane)."""
+  ctx = runtime.get()
+  for t, _ in recvs:
+    _contig(t, 'exchange recv')
+  ns, nr = len(sends), len(recvs)
+  VP, I64, I32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+  sb = (VP * max(ns, 1))(*[t.data_ptr() for t, _ in sends])
+  sn = (I64 * max(ns, 1))(*[t.numel() * t.element_size() for t, _ in sends])
+  sp = (I32 * max(ns, 1))(*[int(p) for _, p in sends])
+  rb = (VP * max(nr, 1))(*[t.data_ptr() for t, _ in recvs])
+  rn = (I64 * max(nr, 1))(*[t.numel() * t.element_size() for t, _ in recvs])
+  rp = (I32 * max(nr, 1))(*[int(p) for _, p in recvs])
+  _check(_lib().spx_sendrecv(ctx.rccl, ns, sb, sn, sp, nr, rb, rn, rp, _stream()), 'spx_sendrecv')
+
+
 def exchange(sends, recvs):
   """Point-to-point batch.  sends: [(tensor, dst_rank)], recvs: [(tensor, src_rank)].
 
@@ -331,18 +398,7 @@ def exchange(sends, recvs):
     return
   import torch
   if ctx.dist_backend == 'rccl':
-    sends = [(t.contiguous(), peer) for t, peer in sends]
-    for t, _ in recvs:
-      _contig(t, 'exchange recv')
-    ns, nr = len(sends), len(recvs)
-    VP, I64, I32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
-    sb = (VP * max(ns, 1))(*[t.data_ptr() for t, _ in sends])
-    sn = (I64 * max(ns, 1))(*[t.numel() * t.element_size() for t, _ in sends])
-    sp = (I32 * max(ns, 1))(*[int(p) for _, p in sends])
-    rb = (VP * max(nr, 1))(*[t.data_ptr() for t, _ in recvs])
-    rn = (I64 * max(nr, 1))(*[t.numel() * t.element_size() for t, _ in recvs])
-    rp = (I32 * max(nr, 1))(*[int(p) for _, p in recvs])
-    _check(_lib().spx_sendrecv(ctx.rccl, ns, sb, sn, sp, nr, rb, rn, rp, _stream()), 'spx_sendrecv')
+    _exchange_rccl([(t.contiguous(), peer) for t, peer in sends], recvs)
     return
   dist = _dist()
   post = []

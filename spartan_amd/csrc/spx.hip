@@ -617,14 +617,16 @@ extern "C" int spx_argreduce_combine(int op, int dtype, const void* vals, const 
 // fp32: 256x128x16, 8 waves (with the k-contiguous A staging: 141.4 TF = 89.9 %
 // of 157.3 at 32768^3 against 135.6 TF for the 256x256x16 16-wave tile,
 // profiles/r02_gemm_tune_ak.txt)
-// fp32: one accumulator set, flushed into C every 1024 K-tiles (gemm_kernels.h
-// GFL): chains of 8192 MFMA steps instead of K / 2 (two flushes at cfg4's
+// fp32: one accumulator set, flushed into C every 512 K-tiles (gemm_kernels.h
+// GFL): chains of 4096 MFMA steps instead of K / 2 (four flushes at cfg4's
 // K = 32768), at the one-chain form's registers and occupancy (round 3's
-// register two-level form, SEG, cost 6 %; GFL 128 / 256 / 512 / 1024: 139.1 /
-// 140.1 / 140.8 / 141.2 TF, profiles/r04_gemm_gfl.txt, r04_gemm_gfl2_sweep.txt;
-// test_dot_cfg4_full_size -- full rows and columns at K = 32768 under the
-// CPU-or-closer rule -- green at 1024)
-constexpr int SPX_GEMM_GFL = 1024;
+// register two-level form, SEG, cost 6 %).  Round 5, the cfg4 product against
+// fp64 at EVERY one of its 2^30 elements (tools/gemm_margin.py,
+// profiles/r05_gemm_gfl_margin.txt, one box): GFL 1024 141.0 TF, max rel err
+// 7.32e-6 (73 % of the 1e-5 budget); 512 140.4 TF, 3.71e-6; 256 140.2 TF,
+// 1.80e-6 -- 512 keeps 40 % of the budget in reserve for 0.4 TF
+// (test_dot_cfg4_full_size asserts <= 0.6e-5 over all elements).
+constexpr int SPX_GEMM_GFL = 512;
 typedef spx_mfma::Config<float, 256, 128, 16, 4, 2, 8, 0, SPX_GEMM_GFL> GemmF32Big;
 typedef spx_mfma::Config<float, 128, 128, 16, 2, 2, 8, 0, SPX_GEMM_GFL> GemmF32Small;
 
@@ -3531,6 +3533,45 @@ static i64 kp_nwin(i64 N) {
 // bytes of the fused step's block partials (k_kmeans_pp's fp32 windows)
 static i64 kfs_part_bytes(i64 N, i64 D, i64 K) { return kfs_grid(N) * kp_nwin(N) * K * D * 4; }
 
+// Optional timing of the fused step (spx_kmeans_timing): HIP events around
+// k_kmeans_pp and around the whole step, recorded on the caller's stream for
+// up to KT_CAP calls and read back (after the timed region) by
+// spx_kmeans_times -- bench.py's per-kernel roofline of the k-means leg.
+constexpr int KT_CAP = 256;
+static bool g_kt_on = false;
+static int g_kt_n = 0;
+static hipEvent_t g_kt_ev[KT_CAP][4];
+extern "C" int spx_kmeans_timing(int enable) {
+  if (enable && !g_kt_on) {
+    for (int i = 0; i < KT_CAP; ++i)
+      for (int k = 0; k < 4; ++k) HIP_TRY(hipEventCreate(&g_kt_ev[i][k]));
+    g_kt_on = true;
+  } else if (!enable && g_kt_on) {
+    for (int i = 0; i < KT_CAP; ++i)
+      for (int k = 0; k < 4; ++k) (void)hipEventDestroy(g_kt_ev[i][k]);
+    g_kt_on = false;
+  }
+  g_kt_n = 0;
+  return SPX_OK;
+}
+extern "C" int spx_kmeans_times(double* fused_ms, double* step_ms, int max) {
+  if (!g_kt_on) return set_err(SPX_EINVAL, "spx_kmeans_times: timing is off (spx_kmeans_timing(1))");
+  const int n = g_kt_n < max ? g_kt_n : max;
+  for (int i = 0; i < n; ++i) {
+    float a = 0.f, b = 0.f;
+    HIP_TRY(hipEventSynchronize(g_kt_ev[i][3]));
+    HIP_TRY(hipEventElapsedTime(&a, g_kt_ev[i][1], g_kt_ev[i][2]));
+    HIP_TRY(hipEventElapsedTime(&b, g_kt_ev[i][0], g_kt_ev[i][3]));
+    fused_ms[i] = a;
+    step_ms[i] = b;
+  }
+  g_kt_n = 0;
+  return n;
+}
+static void kt_record(int k, void* stream) {
+  if (g_kt_on && g_kt_n < KT_CAP) (void)hipEventRecord(g_kt_ev[g_kt_n][k], S(stream));
+}
+
 extern "C" int64_t spx_kmeans_step_workspace(int dtype, int64_t N, int64_t D, int64_t K) {
   const int64_t a = spx_kmeans_assign_workspace(dtype, N, D, K);
   const int64_t c = spx_kmeans_accumulate_workspace(dtype, N, D, K);
@@ -3577,14 +3618,17 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
   __bf16* CBl = CBh + (i64)32 * nct * D;
   float* cnf = (float*)w.cn;
   float* cnf2 = cnf + KF_BN;
+  kt_record(0, stream);
   HIP_TRY(hipMemsetAsync(w.counters, 0, 64, S(stream)));  // the counters and a null KmMove
   k_kmeans_prep_b3<<<1, 1024, 0, S(stream)>>>(D, K, 32 * nct, centers, CBh, CBl, cnf, w.cmax, mcoef, cnf2, w.muf);
   LAUNCH_CHECK("spx_kmeans_step(prep)");
   unsigned long long* dummy = (unsigned long long*)(((uintptr_t)(bcnt + nb + 1) + 63) & ~(uintptr_t)63);
   const i64 nwin = kp_nwin(N);
+  kt_record(1, stream);
   kp_launch_n(nct, (int)(D / 16), S(stream), (int)G, N, K, Pf, ldp, CBh, CBl, cnf2, w.cmax, w.muf, labels,
                w.und_mask, partF, (int)nwin, pcntF, dummy);
   LAUNCH_CHECK("spx_kmeans_step(fused screen + accumulate)");
+  kt_record(2, stream);
   // the screen's undecided rows, in row order (the gathered accumulation's order)
   k_ks_count<KFS_TPT><<<(unsigned)nb, 256, 0, S(stream)>>>(N, w.und_mask, bcnt);
   k_exscan_u32<<<1, 1024, 0, S(stream)>>>(bcnt, nb, w.counters + 3);
@@ -3656,6 +3700,8 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
   k_kmeans_reduce<unsigned long long><<<(unsigned)((K + 63) / 64), 256, 0, S(stream)>>>(
       K, G2, pcnt2, (unsigned long long*)counts, 2);
   LAUNCH_CHECK("spx_kmeans_step(reduce subtractions)");
+  kt_record(3, stream);
+  if (g_kt_on && g_kt_n < KT_CAP) ++g_kt_n;
   return SPX_OK;
 }
 

@@ -188,10 +188,10 @@ def run_dot(a, b, tile_hint=None):
       dst = 0
     requests.append((A.to_base(a_region), dst))
     plan.append((bex, dst))
-  got = distarray.gather_regions(a, requests)
   output = distarray.create(out_shape, dtype, reducer=np.add, tile_hint=tile_hint)
   if ctx.distributed and len(out_shape) == 2 and FLAGS.dot_overlap and _owner_slabs(output, ctx, M):
-    return _dot_overlapped(output, got, plan, b, B, K, M, N, dtype, C, col_blocks)
+    return _dot_overlapped(output, a, A, plan, b, B, K, M, N, dtype, C, col_blocks)
+  got = distarray.gather_regions(a, requests)
   for qi, (bex, dst) in enumerate(plan):
     if dst != ctx.rank:
       continue
@@ -240,39 +240,55 @@ def _owner_slabs(output, ctx, M):
   return _rank_slabs(output, ctx) and M % ctx.world_size == 0
 
 
-def _dot_overlapped(output, got, plan, b, B, K, M, N, dtype, C, col_blocks):
-  """K-split partials reduced chunk by chunk while the next chunk computes.
+def _dot_overlapped(output, a, A, plan, b, B, K, M, N, dtype, C, col_blocks):
+  """K-split partials reduced slab by slab while the next slab computes, the
+  A column strip gathered slab by slab ahead of its GEMM.
 
-  The output is one row slab per rank.  Every rank computes its partial of
-  slab j (its local K blocks, MFMA GEMM into C[slab j]) and immediately
-  starts an RCCL reduce of that slab to its owner j on the process group's
-  stream; the GEMM of slab j + 1 runs meanwhile on the compute stream.  The
-  bytes moved equal the reduce-scatter's, but the xGMI time hides behind the
-  GEMMs instead of following them."""
+  The output is one row slab per rank.  For every slab j (in the same order
+  on every rank) the rank needs rows j of its A column strip A[:, K_g]: the
+  piece that the owner of A's rows j holds.  All N slab gathers are posted
+  at once on the side stream (comm.exchange_async; a piece of whole rows is
+  received straight into its buffer), so slab j + 1's rows travel while slab
+  j's GEMM runs and the first GEMM waits only for its own piece -- the local
+  piece needs no transfer at all when A is row-strip tiled.  After the
+  partial of slab j is computed (MFMA GEMM into C[slab j]) an RCCL reduce of
+  it to its owner j starts on the side stream, under the GEMM of slab j + 1.
+  The bytes moved equal the gather + reduce-scatter's, but the xGMI time
+  hides behind the GEMMs (measured per-rank GEMMs, predicted N = 8
+  time).  Reference: dot.py:268-283 (map2 K-split, partials summed at the
+  target tile), map.py:326-328."""
   global OVERLAPPED_CALLS
   OVERLAPPED_CALLS += 1
   ctx = runtime.get()
   be = backend.get()
   slab = M // ctx.world_size
-  local = []
+  W = ctx.world_size
+  # slab j's request list: the rows of slab j of every K block's A strip
+  reqs = [[(A.to_base(ext.create((j * slab, bex.ul[0]), ((j + 1) * slab, bex.lr[0]), (M, K))), dst)
+           for bex, dst in plan] for j in range(W)]
+  pending = [distarray.gather_regions_async(a, reqs[j]) for j in range(W)]
+  local_b = []
   for qi, (bex, dst) in enumerate(plan):
     if dst != ctx.rank:
       continue
-    at = _as_dtype(got[qi].reshape(M, bex.shape[0]), dtype)
     if b.replicated:
       bt = b.fetch(ext.from_shape(b.shape)).reshape(K, N)
     else:
       bt = b.fetch(B.to_base(bex)).reshape(bex.shape)
-    local.append((bex, at, _as_dtype(bt, dtype)))
+    local_b.append((qi, bex, _as_dtype(bt, dtype)))
   handles = []
   disjoint = _blocks_disjoint(col_blocks)  # (else the caller made C zeros)
-  for j in range(ctx.world_size):
+  for j in range(W):
     r0, r1 = j * slab, (j + 1) * slab
+    got = pending[j].finish()
+    pending[j] = None
     started = set() if disjoint else _ALWAYS_STARTED
-    for bex, at, bt in local:
+    for qi, bex, bt in local_b:
+      at = _as_dtype(got[qi].reshape(slab, bex.shape[0]), dtype)
       key = (bex.ul[1], bex.lr[1])
-      be.gemm(at[r0:r1], bt, C[r0:r1, key[0]:key[1]], 1.0, 0.0 if key not in started else 1.0)
+      be.gemm(at, bt, C[r0:r1, key[0]:key[1]], 1.0, 0.0 if key not in started else 1.0)
       started.add(key)
+    del got
     for c0, c1 in col_blocks:
       if (c0, c1) not in started:
         C[r0:r1, c0:c1].zero_()

@@ -251,6 +251,31 @@ def test_dot_cfg4_full_size(ex, dtype, rtol):
       cpu = np.dot(arow, bcol)
       exact = np.dot(arow.astype(f64), bcol.astype(f64))
       check_fp(np.array([crow[c]]), np.array([cpu]), np.array([exact]), rtol)
+  # the margin (round-5 review): max |gpu - fp64| / |fp64| over EVERY element
+  # of C (2^30 of them: the rows and columns with the largest |A| / |B| sums
+  # included), against fp64 products of the same device values -- torch fp64
+  # GEMMs on the device in 2048-row blocks, a checker only.  Asserted at 60 %
+  # of the tolerance (40 % of the budget in reserve); printed for DESIGN 3.2.
+  import torch
+  (ta,), (tb,), (tc,) = ([t.data for t in X.local.values()] for X in (A, B, C))
+  b64 = tb.to(torch.float64)
+  margin, where = 0.0, None
+  edges = torch.tensor([1e-7, 3e-7, 1e-6, 2e-6, 3e-6, 4e-6, 6e-6], dtype=torch.float64, device=tc.device) * (rtol / 1e-5)
+  hist = torch.zeros(len(edges) + 1, dtype=torch.int64, device=tc.device)
+  for r0 in range(0, S, 2048):
+    want = ta[r0:r0 + 2048].to(torch.float64) @ b64
+    rel = (tc[r0:r0 + 2048].to(torch.float64) - want).abs_().div_(want.abs())
+    m = rel.max().item()
+    if m > margin:
+      i = int(rel.argmax())
+      margin, where = m, (r0 + i // S, i % S)
+    hist += torch.bincount(torch.bucketize(rel.flatten(), edges), minlength=len(edges) + 1)
+    del want, rel
+  del b64
+  print('cfg4 %s margin: max rel err %.4g at C%s over all %d elements, tolerance %g; elements per '
+        'rel-err bin (upper edges %s, last open): %s' % (np.dtype(dtype).name, margin, where, S * S, rtol,
+                                                        ['%.3g' % e for e in edges.tolist()], hist.tolist()))
+  assert margin <= 0.6 * rtol, 'cfg4 %s max rel err %.4g > 0.6 x %g' % (np.dtype(dtype).name, margin, rtol)
   # one FULL row and one FULL column of C against host dots over the whole of
   # B / A (the device values, bit-exact to the generator by
   # test_rand_bit_exact), streamed in 4096-row blocks: the dtype's own dot
@@ -1489,3 +1514,34 @@ def test_kmeans_step_far_undecided_outliers(ex):
   s = sums.cpu().numpy()
   err = np.abs(s - ws) / wa
   assert err.max() <= 1e-5, 'max |sum - fp64| / sum |x| = %.3g at %s' % (err.max(), np.unravel_index(err.argmax(), err.shape))
+
+
+def test_kmeans_step_timing_hook(ex):
+  """spx_kmeans_timing / spx_kmeans_times (bench.py's k-means kernel
+  roofline): one (kernel, step) pair per fused step in call order, the kernel
+  inside the step, nothing recorded while off, and the results unchanged."""
+  import torch
+  from spartan_amd import backend
+  be = backend.get()
+  N, D, K = 200_000, 128, 256
+  P = torch.empty((N, D), dtype=torch.float32, device='cuda')
+  be.fill(P, backend.FILL_UNIFORM, 0.0, 1.0, 5, (0, 0), (N, D))
+  Cd = P[:K].to(torch.float64).contiguous()
+  lab = torch.empty((N,), dtype=torch.int64, device='cuda')
+  sums = torch.empty((K, D), dtype=torch.float64, device='cuda')
+  cnt = torch.empty((K,), dtype=torch.int64, device='cuda')
+  be.kmeans_step(P, Cd, lab, sums, cnt)
+  s0, l0 = sums.clone(), lab.clone()
+  be.kmeans_timing(True)
+  try:
+    for _ in range(3):
+      be.kmeans_step(P, Cd, lab, sums, cnt)
+    t = be.kmeans_times()
+    assert len(t) == 3 and all(0.0 < a <= b for a, b in t), t
+    assert be.kmeans_times() == []   # read once
+  finally:
+    be.kmeans_timing(False)
+  be.kmeans_step(P, Cd, lab, sums, cnt)
+  assert torch.equal(sums, s0) and torch.equal(lab, l0)
+  with pytest.raises(RuntimeError):
+    be.kmeans_times()                # timing is off

@@ -30,6 +30,10 @@ for s in $STEPS; do
     tests)
       cd $R && step tests 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
         -p no:cacheprovider > $O/pytest.log 2>&1 ;;
+    testsp)
+      # the GPU suite with passed tests' output shown (the cfg4 margin lines)
+      cd $R && step testsp 900 python -u -m pytest tests -m gpu -v -rP --timeout 300 --timeout-method thread \
+        -p no:cacheprovider > $O/pytest.log 2>&1 ;;
     smoke)
       cd $R && step smoke 300 python3 -c 'import __graft_entry__ as g; g.smoke(); print("smoke ok")' > $O/smoke.log 2>&1 ;;
     lregtests)
