@@ -147,7 +147,7 @@ def main():
   achieved = bytes_launch / avg / 1e9 if red else None
 
   traffic = None
-  tname = 'r04_cfg2_pmc_traffic.json'
+  tname = 'r05_cfg2_pmc_traffic.json'
   tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', tname)
   if os.path.exists(tpath) and rows_local == 32768 and S == 32768:
     with open(tpath) as f:

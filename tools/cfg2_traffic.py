@@ -11,11 +11,16 @@ import json
 import sys
 
 
+HEADLINE = ('spx_reduce_cols_8da20c40', 'spx_reduce_rows_ed017d42')  # cfg2 axis 0 / axis 1 (codegen.named)
+
+
 def per_launch(d, counter):
   f = glob.glob(d + '/*counter_collection.csv')[0]
   acc = collections.OrderedDict()
   for r in csv.DictReader(open(f)):
-    if r['Counter_Name'] == counter and r['Kernel_Name'].startswith('spx_reduce'):
+    # the headline's two kernels only (the bench's cold-start, axis=None and
+    # map legs and its fp64 checks launch other spx_reduce kernels)
+    if r['Counter_Name'] == counter and r['Kernel_Name'] in HEADLINE:
       key = (r['Dispatch_Id'], r['Kernel_Name'])
       acc[key] = acc.get(key, 0.0) + float(r['Counter_Value']) * 1024.0
   return list(acc.values())

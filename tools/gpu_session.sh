@@ -97,7 +97,7 @@ for s in $STEPS; do
         for v in ${KAB:-base product}; do
           lib=$R/tools/bin/libspx_$v.so; [ $v = product ] && lib=$R/spartan_amd/libspx.so
           cd /tmp && step kab_${v}_$i 120 rocprofv3 --kernel-trace --stats -d $O/kab_${v}_$i -o p --output-format csv \
-            -- python3 $R/tools/km_step_once.py 100000000 5 step $lib > $O/kab_${v}_$i.log 2>&1
+            -- python3 $R/tools/km_step_once.py 100000000 5 ${KAB_MODE:-step} $lib > $O/kab_${v}_$i.log 2>&1
         done
       done ;;
     kclk)
@@ -150,6 +150,11 @@ for s in $STEPS; do
     trace2)
       cd /tmp && step trace2 300 rocprofv3 --kernel-trace --stats -d $O/trace2 -o p --output-format csv \
         -- python3 $R/bench.py --dot 0 --workloads 0 --cpu-baseline 0 --steps 20 --warmup 5 > $O/trace2.log 2>&1 ;;
+    benchtrace)
+      # the default bench (minus the CPU legs) under a kernel trace: its JSON
+      # line and the trace come from the SAME run (profiles/ roofline check)
+      cd /tmp && step benchtrace 600 rocprofv3 --kernel-trace --stats -d $O/benchtrace -o p --output-format csv \
+        -- python3 $R/bench.py --cpu-baseline 0 > $O/benchtrace.json 2> $O/benchtrace.err ;;
     traceall)
       cd /tmp && step traceall 600 rocprofv3 --kernel-trace --stats -d $O/traceall -o p --output-format csv \
         -- python3 $R/bench.py --cpu-baseline 0 --steps 5 --warmup 1 > $O/traceall.log 2>&1 ;;

@@ -18,7 +18,7 @@ def main():
         if 'k_kmeans_pp' in r['Name']:
           row = r
     log = open(sub + '.log').read() if os.path.exists(sub + '.log') else ''
-    m = re.search(r'step: ([0-9.]+) ms per iteration', log)
+    m = re.search(r'(?:step|first): ([0-9.]+) ms per iteration', log)
     print('%-22s kernel avg %7.3f min %7.3f ms  step %s ms' % (
         name, float(row.get('AverageNs', 'nan')) / 1e6, float(row.get('MinNs', 'nan')) / 1e6,
         m.group(1) if m else '?'))

@@ -43,6 +43,9 @@ subs = {
   # the ring loads non-temporal (global_load ... nt)
   'ntload': [('    for (int q = 0; q < NQ; ++q) r[q] = *(const kb_f4*)(p + 4 * qof(q));\n',
               '    for (int q = 0; q < NQ; ++q) r[q] = __builtin_nontemporal_load((const kb_f4*)(p + 4 * qof(q)));\n')],
+  # rows of rank >= NRU (3) not added: what the rare-round loop costs
+  'noloop3': [('    for (int k = NRU; k < U && __ballot(rnd >= k && rnd != 0xffff) != 0ull; ++k)\n',
+               '    for (int k = NRU; k < U && nit < 0 && __ballot(rnd >= k && rnd != 0xffff) != 0ull; ++k)\n')],
   'r_nobarrier': [NR, ('    __syncthreads();\n    if constexpr (c == 0)\n', '    if constexpr (c == 0)\n')],
   # the decision's rank / count atomics and their round trip (ranks all 0)
   'r_noatomic': [NR, ('    if (s == 0 && h == 0 && act) {\n      rk = __hip_atomic_fetch_add', '    if (s == 0 && h == 0 && act && nit < 0) {\n      rk = __hip_atomic_fetch_add')],
