@@ -2295,7 +2295,9 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
 
   // A operands: wave s screens centre tiles 2s and 2s + 1 (lane (j, h):
   // centre 32 ct + j, dims 16 ks + 8 h .. + 8 of k-step ks)
-  const bool scr0 = 2 * s < NCT, scr1 = 2 * s + 1 < NCT;
+  // (with 8 centre tiles every wave screens two: compile-time true, so the
+  // MFMA chain and the fold carry no per-pair branches)
+  const bool scr0 = NCT >= 8 || 2 * s < NCT, scr1 = NCT >= 8 || 2 * s + 1 < NCT;
   kh_f8 ca[2][KS];
 #pragma unroll
   for (int tl = 0; tl < 2; ++tl) {
@@ -2435,7 +2437,7 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     // (2) fold, first tile (its latency cover)
     float lo0 = -INFINITY, sec0 = -INFINITY, lo1 = -INFINITY, sec1 = -INFINITY;
     int il0 = 0, il1 = 0;
-    if (fv && scr0) fold16(acc0, 2 * s, lo0, sec0, il0);
+    if (scr0) fold16(acc0, 2 * s, lo0, sec0, il0);  // (unused when !fv: exv is written only if fv)
     __builtin_amdgcn_sched_barrier(0);
     // (3) decide: top-2 over the 4 waves' candidates, the certified rule.
     // d: the centre the row is added to -- its label when decided, and,
@@ -2479,7 +2481,7 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
       rk = __hip_atomic_fetch_add(rcnt + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       __hip_atomic_fetch_add(cnts + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    if (fv && scr1) fold16(acc1, 2 * s + 1, lo1, sec1, il1);
+    if (scr1) fold16(acc1, 2 * s + 1, lo1, sec1, il1);
     __builtin_amdgcn_sched_barrier(0);
     if (s == 0 && h == 0 && act) __hip_atomic_store(rcnt + d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     // (5) merge the fold's tiles and halves, the candidates out (mu's reads
@@ -2523,7 +2525,6 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     // both waves of a SIMD are ready (-0.3 ms per cfg3 pass; the vector role
     // first: +0.2 ms, profiles/r04_kp_ablate_v4.txt)
     __builtin_amdgcn_s_setprio(1);
-    const bool mf = tt < nit;
     const int ua = tt - KP_LAG;
     const bool av = ua >= 0 && ua < nit;
     const i64 una = bk + (i64)(av ? ua : 0) * G;
@@ -2545,10 +2546,11 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     };
     const kb_bf8 cc0 = ccop(h == 0 && scr0, 2 * s);
     const kb_bf8 cc1 = ccop(h == 0 && scr1, 2 * s + 1);
-    if (mf) {
-      acc0 = (kb_acc){};
-      acc1 = (kb_acc){};
-    }
+    // the MFMAs run in every slot, also in the few drain slots past the
+    // block's last unit (stale operands, results never folded into exv):
+    // no per-pair branches in the chain
+    acc0 = (kb_acc){};
+    acc1 = (kb_acc){};
     const int dcode = av ? (int)(short)(dr & 0xffff) : -1;
     const int d = dcode >= 0 ? dcode : dcode <= -2 ? -2 - dcode : -1;  // the centre the row is added to
     const int rnd = av ? (int)((unsigned int)dr >> 16) : 0xffff;
@@ -2590,8 +2592,8 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     auto mk = [&](auto kc) __attribute__((always_inline)) {
       constexpr int ks = decltype(kc)::value;
       if constexpr (ks + PF < KS) bq[(ks + PF) % NB] = *(const kh_f8*)(bp + 32 * (ks + PF));
-      if (mf && scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[0][ks], bq[ks % NB], acc0, 0, 0, 0);
-      if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[1][ks], bq[ks % NB], acc1, 0, 0, 0);
+      if (scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[0][ks], bq[ks % NB], acc0, 0, 0, 0);
+      if (scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ca[1][ks], bq[ks % NB], acc1, 0, 0, 0);
       if constexpr (ks == WR0) { if (rnd == 0) wr(); }
       if constexpr (ks == RD1) { if (rnd == 1) rd(); }
       if constexpr (ks == WR1) { if (rnd == 1) wr(); }
@@ -2610,8 +2612,8 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
       }
     load(r, tt + KP_AHEAD);
     __builtin_amdgcn_sched_barrier(0);
-    if (mf && scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cc0, ones, acc0, 0, 0, 0);
-    if (mf && scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cc1, ones, acc1, 0, 0, 0);
+    if (scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cc0, ones, acc0, 0, 0, 0);
+    if (scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cc1, ones, acc1, 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
 
