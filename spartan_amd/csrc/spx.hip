@@ -2247,7 +2247,7 @@ static_assert(KP_FW % KP_UNR == 0 && KP_UNR == 2 * KP_NR && KP_AHEAD + KP_LAG ==
               "flush points fall on the unrolled body's first slot; the ring cycles once per body");
 static size_t kp_lds_bytes(int D) {
   return (size_t)256 * D * 4 + 256 * 4 + (size_t)2 * KP_U * kfs_rs(D) + (size_t)2 * KP_U * KP_XS +
-         (size_t)4 * KP_U * KP_XS + (size_t)4 * KP_U * 4 + 256 * 4 + (size_t)8 * 32 * 8 + (size_t)D * 4;
+         (size_t)4 * KP_U * KP_XS + (size_t)4 * KP_U * 4 + 256 * 4 + (size_t)8 * 2 * 16 * 4 + (size_t)D * 4;
 }
 
 template <int KS, int NCT>
@@ -2273,8 +2273,8 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
   unsigned char* p2p = exv + (size_t)2 * U * KP_XS;      // [4][U][KP_XS]: 8 |x'|^2 column partials (by unit mod 4)
   int* dres = (int*)(p2p + (size_t)4 * U * KP_XS);       // [4][U]: label (low 16 bits, -1: undecided) | add round << 16
   unsigned int* rcnt = (unsigned int*)(dres + 4 * U);    // [256] rows per centre so far in the unit (rank counters)
-  unsigned long long* ccl = (unsigned long long*)(rcnt + 256);  // [8 tiles][32] -cc/2 as 3 bf16 pieces + a zero
-  float* mus = (float*)(ccl + 8 * 32);                   // [D] the centring vector mu
+  float* cci = (float*)(rcnt + 256);                     // [8 tiles][2 halves][16]: -cc/2 of a lane's accumulator centres
+  float* mus = cci + 8 * 2 * 16;                         // [D] the centring vector mu
   // (j, h): the MFMA / fold / decision lanes (row j = lane & 31, k-half or
   // centre half h = lane >> 5).  (jr, hr): the raw-column lanes (row jr =
   // lane >> 1, column half hr = lane & 1) of the loads, the staging and the
@@ -2310,22 +2310,16 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
         const i64 d = 16 * ks + 8 * h + e;
         ca[tl][ks][e] = (_Float16)((float)CBh[c * D + d] + (float)CBl[c * D + d]);
       }
-    const float v = -0.5f * cnf2[c];
-    const __bf16 b1 = (__bf16)v;
-    const float v1 = v - (float)b1;
-    const __bf16 b2 = (__bf16)v1;
-    const __bf16 b3 = (__bf16)(v1 - (float)b2);
-    const __bf16 z = (__bf16)0.f;
-    // the MFMA operand of the -cc/2 step: lane (j, 0) holds centre j's three
-    // pieces, lane (j, 1) zeros -- kept in LDS (16 B per centre), read at
-    // the step
-    if (h == 0 && ct < NCT) {
-      typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
-      ccl[ct * 32 + j] = __builtin_bit_cast(unsigned long long, (bf4){b1, b2, b3, z});
+    // the chain's initial accumulator (round 5; was a bf16 MFMA pair adding
+    // -cc/2 as three pieces after the chain): register q of lane (j, h) is
+    // centre 32 ct + (q & 3) + 8 (q >> 2) + 4 h, so the 16 values depend on
+    // (ct, h) only -- lanes j < 16 write them once, the chain's lanes read
+    // them back as four broadcast ds_read_b128 per tile
+    if (j < 16) {
+      const i64 m = 32 * (i64)ct + (j & 3) + 8 * (j >> 2) + 4 * h;
+      cci[(ct * 2 + h) * 16 + j] = ct < NCT ? -0.5f * cnf2[m] : 0.f;
     }
   }
-  const __bf16 one = (__bf16)1.f;
-  const kb_bf8 ones = (kb_bf8){one, one, one, one, one, one, one, one};
 
   // the certified bound of k_kmeans_filter_as MODE 1 (same arithmetic)
   const double cmax = cmax_p[0], mcoef = cmax_p[1], mun = cmax_p[2], dcmax = cmax_p[3];
@@ -2334,6 +2328,10 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
   const double eS = (u32 * cmax + 4.8828125e-04 * cmax + 1.001 * dcmax +
                      2.0 * (chain + 3.0) * u32 * 1.001 * (cmax + dcmax)) * 1.01;
   double xk1 = 64.0 * u32 * cmax, xk0 = 32.0 * u32 * (cmax * cmax + 2.0 * mun * cmax);
+  // -cc/2 enters the chain as its initial accumulator: every one of the
+  // chain's roundings also sees |cc/2| <= cmax^2 / 2 (x 2 for the MFMA's
+  // directed rounding, x 2 for the best and the second value)
+  xk0 += 2.0 * (chain + 3.0) * u32 * 1.001 * 1.01 * cmax * cmax;
   xk0 += sqrt((double)D) * 1.1920928955078125e-07 * (cmax + dcmax) + (double)D * 3.552713678800501e-15;
   xk1 += 14.0 * 1.1920928955078125e-07 * cmax;
   xk0 += 7.0 * 1.1920928955078125e-07 * (cmax * cmax + 2.0 * mun * cmax);
@@ -2418,6 +2416,11 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     il = 32 * ct + (int)((qb & 3) + 8 * (qb >> 2)) + 4 * h;
   };
 
+  auto cc_init = [&]() __attribute__((always_inline)) {
+    acc0 = *(const kb_acc*)(cci + (4 * s + h) * 16);
+    acc1 = *(const kb_acc*)(cci + (4 * s + 2 + h) * 16);
+  };
+
   // vector role of slot t: the decision of unit t - 2 and its add rounds
   // (dres[(t - 2) & 3]), the fold of unit t - 1 (exv[(t - 1) & 1]), the
   // staging of unit t + 1.  Every wave of the group computes the decision
@@ -2482,6 +2485,8 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
       __hip_atomic_fetch_add(cnts + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (scr1) fold16(acc1, 2 * s + 1, lo1, sec1, il1);
+    // folded: the accumulators take the next chain's initial -cc/2
+    cc_init();
     __builtin_amdgcn_sched_barrier(0);
     if (s == 0 && h == 0 && act) __hip_atomic_store(rcnt + d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     // (5) merge the fold's tiles and halves, the candidates out (mu's reads
@@ -2539,18 +2544,9 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     kh_f8 bq[NB];
 #pragma unroll
     for (int p = 0; p < PF; ++p) bq[p] = *(const kh_f8*)(bp + 32 * p);
-    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-    auto ccop = [&](bool on, int ct) __attribute__((always_inline)) {  // (pieces, 0, 0 0 0 0) or zeros
-      const unsigned long long v = on ? ccl[ct * 32 + j] : 0ull;
-      return __builtin_bit_cast(kb_bf8, (u4v){(unsigned int)v, (unsigned int)(v >> 32), 0u, 0u});
-    };
-    const kb_bf8 cc0 = ccop(h == 0 && scr0, 2 * s);
-    const kb_bf8 cc1 = ccop(h == 0 && scr1, 2 * s + 1);
     // the MFMAs run in every slot, also in the few drain slots past the
     // block's last unit (stale operands, results never folded into exv):
-    // no per-pair branches in the chain
-    acc0 = (kb_acc){};
-    acc1 = (kb_acc){};
+    // no per-pair branches in the chain; acc0 / acc1 hold -cc/2 (cc_init)
     const int dcode = av ? (int)(short)(dr & 0xffff) : -1;
     const int d = dcode >= 0 ? dcode : dcode <= -2 ? -2 - dcode : -1;  // the centre the row is added to
     const int rnd = av ? (int)((unsigned int)dr >> 16) : 0xffff;
@@ -2611,9 +2607,6 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
         wr();
       }
     load(r, tt + KP_AHEAD);
-    __builtin_amdgcn_sched_barrier(0);
-    if (scr0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cc0, ones, acc0, 0, 0, 0);
-    if (scr1) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cc1, ones, acc1, 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -2669,7 +2662,8 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
   // the set-up loads (centres, mu, bound inputs) complete here, so the loop's
   // waits count only the ring's loads and the slots' stores
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  __syncthreads();  // sums, rcnt, ccl
+  __syncthreads();  // sums, rcnt, cci
+  cc_init();
   if (grp == 0)
     body(std::integral_constant<int, 0>{});
   else
