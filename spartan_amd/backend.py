@@ -247,10 +247,18 @@ def compile_code_object(src):
 _NCU = []
 NT_STORE_BYTES = 64 << 20  # map outputs at least this large: non-temporal stores
 ROWS_GRID_PER_CU = 2  # rows reductions: 1.824 ms vs 1.836 uncapped at cfg2 axis 1 (profiles/r02_cfg2_grid.txt)
-# fused row-dot column reductions (cfg5's gradient): blocks per CU and rows
-# unrolled per lane group (profiles/r04_lreg_sweep*.txt; tools/lreg_sweep.py)
-ROWDOT_BLOCKS_PER_CU = 16
+# fused row-dot column reductions (cfg5's gradient): blocks per CU, rows
+# unrolled per lane group, and the row order.  Round 5: the blocks take
+# interleaved super-chunks of U x 16 rows (block p: chunks p, p + P, ...;
+# codegen.gen_reduce interleave) instead of one contiguous chunk each, so the
+# grid streams one stretch of X at a time -- and then ONE block per CU is
+# best: 3.600 ms per lreg iteration against 3.811 for the round-4 form (16
+# contiguous chunks per CU, U 8) on one box; interleaved with 2 / 4 / 8 / 16
+# blocks per CU 3.69-3.88, U 4 / 6 / 10 / 12 at one block 5.11 / 3.97 / 3.62
+# / 3.71 (tools/lreg_il.py, profiles/r05_lreg_interleave.txt)
+ROWDOT_BLOCKS_PER_CU = 1
 ROWDOT_UNROLL = 8
+ROWDOT_INTERLEAVE = True
 
 
 def _num_cus():
@@ -526,8 +534,8 @@ class HipBackend:
       # 1024 1.87, 2048 1.87, 4096 1.90); one narrow column tile (cfg5's 64
       # columns) with eight (2048: 4.06 ms per lreg iteration, 512: 4.15)
       # -- profiles/r02_cfg2_grid.txt; a fused row dot (cfg5's gradient, one
-      # 64-column tile) with sixteen and rows unrolled 8 deep (3.866 ms per
-      # lreg iteration against 3.959 at eight and 4; profiles/r04_lreg_sweep.txt)
+      # 64-column tile) with ROWDOT_BLOCKS_PER_CU (one, its rows interleaved
+      # over the blocks: see ROWDOT_INTERLEAVE)
       rowdot = bool(codegen.rowdots(root))
       tb = (2 if CT > 1 else ROWDOT_BLOCKS_PER_CU if rowdot else 8) * _num_cus()
       if base < tb:
@@ -572,11 +580,12 @@ class HipBackend:
     klpr, kfull = None, False
     if kind == 'cols' and codegen.rowdots(root):
       klpr, kfull = lpr, bool(vec_ok and CT == 1 and I == lpr * per)
-    sig = ('reduce', root.sig(), tuple(ins), tuple(classes), kind, op, V, U, rowinv, klpr, kfull)
+    kint = bool(klpr and ROWDOT_INTERLEAVE)
+    sig = ('reduce', root.sig(), tuple(ins), tuple(classes), kind, op, V, U, rowinv, klpr, kfull, kint)
     fn = self._sig_fns.get(sig)
     if fn is None:
-      src, kname = codegen.named(codegen.gen_reduce(root, ins, classes, kind, op, V, U, rowinv, klpr, kfull),
-                                 'spx_reduce', kind)
+      src, kname = codegen.named(codegen.gen_reduce(root, ins, classes, kind, op, V, U, rowinv, klpr, kfull,
+                                                    kint), 'spx_reduce', kind)
       fn = self._sig_fns[sig] = self.kernel(src, kname)
     self.launch(fn, nblk, args)
     if not direct:

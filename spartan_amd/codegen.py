@@ -639,7 +639,7 @@ def _acc_update(op, j, val, idx_expr):
   return 'acc%d = comb(acc%d, %s);' % (j, j, val)
 
 
-def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=(), lpr=None, full=False):
+def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=(), lpr=None, full=False, interleave=False):
   """Fused map+reduce.  kind 'rows' (reduce over contiguous R of (O, R), one
   or more blocks per segment), 'rowsp' (the same for short R: several
   segments per wave, LPR lanes each, butterfly combine) or 'cols' (reduce over
@@ -944,6 +944,21 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=(), lpr
                 for j, v in enumerate(srcs)]
           b.append('  }')
       b.append('  const i64 STEP = 4 * RPW;')
+      lv = interleave and op == 'sum'
+      if interleave:
+        # block p takes the U-step super-chunks p, p + P, p + 2P, ...: at any
+        # moment the grid streams one contiguous stretch of X instead of P
+        # streams far apart (one chunk per block).  A block then covers R / P
+        # rows, so (sums) each super-chunk's U rows go into a fresh
+        # accumulator that is folded into a middle one, and every 32 chunks
+        # the middle one into the block's total: fp32 chains of U + 32 +
+        # R / (32 P U 16) additions per lane instead of R / (16 P)
+        if lv:
+          b.append('  %s %s;' % (act, ', '.join('mid%d = (%s)0, top%d = (%s)0' % (j, act, j, act)
+                                                for j in range(V))))
+          b.append('  int nsc = 0;')
+        b.append('  for (i64 sb = p * (%d * STEP); sb < R; sb += P * (%d * STEP)) {' % (U, U))
+        b.append('  const i64 r0 = sb; i64 r1 = sb + %d * STEP; if (r1 > R) r1 = R;' % U)
       b.append('  i64 r = r0 + w * RPW + sub;')
       if U > 1:
         b.append('  for (; r + %d * STEP < r1; r += %d * STEP) {' % (U - 1, U))
@@ -965,6 +980,19 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=(), lpr
       ld, cp = one_row(V, 'r', '', masked)
       b += ['    ' + x for x in ld + cp]
       b.append('  }')
+      if interleave:
+        if lv:
+          for j in range(V):
+            b.append('  mid%d = mid%d + acc%d; acc%d = (%s)0;' % (j, j, j, j, act))
+          b.append('  if (++nsc == 32) {')
+          for j in range(V):
+            b.append('    top%d = top%d + mid%d; mid%d = (%s)0;' % (j, j, j, j, act))
+          b.append('    nsc = 0;')
+          b.append('  }')
+        b.append('  }')
+        if lv:
+          for j in range(V):
+            b.append('  acc%d = top%d + mid%d;' % (j, j, j))
       b.append('}')
       return b
 

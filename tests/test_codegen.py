@@ -117,3 +117,21 @@ def test_rowdot_narrow_row_input_compiles(rdt):
   src = codegen.gen_reduce(root, ins, ['c', 'b', 'c', 'b'], 'cols', 'sum', V, 8, (2,), lpr=16, full=True)
   assert 'yb1' in src and 'yb3' not in src
   _compile(src)
+
+
+def test_rowdot_interleaved_rows_compile():
+  """The cfg5 kernel's interleaved row order (round 5): block p walks the
+  U-step super-chunks p, p + P, ... (one loop around the unrolled and the
+  tail loops), for both dtypes; the contiguous form has no such loop."""
+  from spartan_amd.codegen import RowDot
+  for dt in (F32, F64):
+    x, yv, w = In(0, dt), In(1, dt), In(2, dt)
+    root = Op('multiply', [x, Op('subtract', [RowDot(x, w), yv])])
+    ins = [(0, dt), (1, dt), (2, dt)]
+    V = codegen.vec_width([dt])
+    src = codegen.gen_reduce(root, ins, ['c', 'b', 'c'], 'cols', 'sum', V, 8, (2,), lpr=16, full=True,
+                             interleave=True)
+    assert src.count('for (i64 sb = p * (8 * STEP); sb < R; sb += P * (8 * STEP))') == 2
+    _compile(src)
+    assert 'for (i64 sb' not in codegen.gen_reduce(root, ins, ['c', 'b', 'c'], 'cols', 'sum', V, 8, (2,),
+                                                   lpr=16, full=True)
