@@ -259,6 +259,13 @@ ROWS_GRID_PER_CU = 2  # rows reductions: 1.824 ms vs 1.836 uncapped at cfg2 axis
 ROWDOT_BLOCKS_PER_CU = 1
 ROWDOT_UNROLL = 8
 ROWDOT_INTERLEAVE = True
+# wide column sums (several column tiles: cfg2 axis 0): resident blocks per
+# CU and whether their row segments are interleaved super-chunks.  The lreg
+# kernel's interleaving does NOT carry over: cfg2 axis 0 ran 1.80 ms
+# contiguous at 2 blocks per CU against 1.95-2.00 interleaved at 2 / 4 and
+# 2.8-3.1 at one block (tools/cfg2_il.py, profiles/r05_cfg2_interleave.txt)
+COLS_BLOCKS_PER_CU = 2
+COLS_INTERLEAVE = False
 
 
 def _num_cus():
@@ -537,7 +544,7 @@ class HipBackend:
       # 64-column tile) with ROWDOT_BLOCKS_PER_CU (one, its rows interleaved
       # over the blocks: see ROWDOT_INTERLEAVE)
       rowdot = bool(codegen.rowdots(root))
-      tb = (2 if CT > 1 else ROWDOT_BLOCKS_PER_CU if rowdot else 8) * _num_cus()
+      tb = (COLS_BLOCKS_PER_CU if CT > 1 else ROWDOT_BLOCKS_PER_CU if rowdot else 8) * _num_cus()
       if base < tb:
         P = max(1, min(-(-tb // base), -(-R // (rows_per_step * 4))))
       chunk = -(-R // P)
@@ -580,7 +587,7 @@ class HipBackend:
     klpr, kfull = None, False
     if kind == 'cols' and codegen.rowdots(root):
       klpr, kfull = lpr, bool(vec_ok and CT == 1 and I == lpr * per)
-    kint = bool(klpr and ROWDOT_INTERLEAVE)
+    kint = bool((klpr and ROWDOT_INTERLEAVE) or (kind == 'cols' and CT > 1 and op == 'sum' and COLS_INTERLEAVE))
     sig = ('reduce', root.sig(), tuple(ins), tuple(classes), kind, op, V, U, rowinv, klpr, kfull, kint)
     fn = self._sig_fns.get(sig)
     if fn is None:
