@@ -2485,8 +2485,6 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
       __hip_atomic_fetch_add(cnts + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (scr1) fold16(acc1, 2 * s + 1, lo1, sec1, il1);
-    // folded: the accumulators take the next chain's initial -cc/2
-    cc_init();
     __builtin_amdgcn_sched_barrier(0);
     if (s == 0 && h == 0 && act) __hip_atomic_store(rcnt + d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     // (5) merge the fold's tiles and halves, the candidates out (mu's reads
@@ -2537,6 +2535,10 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     const bool rlive = av && grow < N;
     const int dr = dres[(ua & 3) * U + jr];  // the add lanes' rows
     const int dlv = dres[(ua & 3) * U + j];  // the label lanes' rows
+    // the chain's initial accumulators (-cc/2), read first: the matrix role
+    // has the slack for their latency, the vector role (the slot's critical
+    // path, tools/kp_roles.py) does not
+    cc_init();
     const unsigned char* bp = xh + ((size_t)(tt & 1) * U + j) * RS + 16 * h;
     // B fragments three k-steps ahead: under load an LDS read takes longer
     // than one MFMA pair, and a read issued one step ahead stalled every pair
