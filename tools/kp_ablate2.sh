@@ -46,6 +46,12 @@ subs = {
   # rows of rank >= NRU (3) not added: what the rare-round loop costs
   'noloop3': [('    for (int k = NRU; k < U && __ballot(rnd >= k && rnd != 0xffff) != 0ull; ++k)\n',
                '    for (int k = NRU; k < U && nit < 0 && __ballot(rnd >= k && rnd != 0xffff) != 0ull; ++k)\n')],
+  # wave priority: none, or on the vector role instead of the matrix role
+  'noprio': [('    __builtin_amdgcn_s_setprio(1);\n    const int ua = tt - KP_LAG;', '    const int ua = tt - KP_LAG;')],
+  'prio_vec': [('    __builtin_amdgcn_s_setprio(1);\n    const int ua = tt - KP_LAG;', '    const int ua = tt - KP_LAG;'),
+               (VR, VR + '    __builtin_amdgcn_s_setprio(1);\n'),
+               ('    if (s == 0 && h == 0) dres[(u2 & 3) * U + j] = (dl & 0xffff) | (rnd << 16);\n  };',
+                '    if (s == 0 && h == 0) dres[(u2 & 3) * U + j] = (dl & 0xffff) | (rnd << 16);\n    __builtin_amdgcn_s_setprio(0);\n  };')],
   'r_nobarrier': [NR, ('    __syncthreads();\n    if constexpr (c == 0)\n', '    if constexpr (c == 0)\n')],
   # the decision's rank / count atomics and their round trip (ranks all 0)
   'r_noatomic': [NR, ('    if (s == 0 && h == 0 && act) {\n      rk = __hip_atomic_fetch_add', '    if (s == 0 && h == 0 && act && nit < 0) {\n      rk = __hip_atomic_fetch_add')],
