@@ -245,6 +245,7 @@ def compile_code_object(src):
 
 
 _NCU = []
+MAP_UNROLL = 1  # vectors per lane of a dense map (grid = n / (256 V MAP_UNROLL))
 NT_STORE_BYTES = 64 << 20  # map outputs at least this large: non-temporal stores
 ROWS_GRID_PER_CU = 2  # rows reductions: 1.824 ms vs 1.836 uncapped at cfg2 axis 1 (profiles/r02_cfg2_grid.txt)
 # fused row-dot column reductions (cfg5's gradient): blocks per CU, rows
@@ -403,17 +404,18 @@ class HipBackend:
     # streamed outputs: non-temporal stores (x*y+exp(z) map at 2^30 fp32:
     # 2.75 -> 2.57 ms, profiles/r02_stream_ceiling_maps.txt)
     nt = n * out.element_size() >= NT_STORE_BYTES
-    sig = ('map', root.sig(), tuple(ins), tuple(classes), ndim, V, dense, nt)
+    mu = MAP_UNROLL if (dense and args.flags & 1) else 1
+    sig = ('map', root.sig(), tuple(ins), tuple(classes), ndim, V, dense, nt, mu)
     fn = self._sig_fns.get(sig)
     if fn is None:
-      src, kname = codegen.named(codegen.gen_map(root, ins, classes, ndim, V, dense, nt), 'spx_map',
+      src, kname = codegen.named(codegen.gen_map(root, ins, classes, ndim, V, dense, nt, mu), 'spx_map',
                                  'dense' if dense else 'nd')
       fn = self._sig_fns[sig] = self.kernel(src, kname)
     per = V if args.flags & 1 else 1
-    # one vector per lane and no grid-stride loop: x + 1 / x * y at 2^30 fp32
-    # 1.75 / 2.58 ms with a 4096-block grid-stride loop, 1.34 / 2.01 ms with
-    # the full grid (6.4 TB/s read+write; profiles/r02_map_grid.txt)
-    grid = max(1, -(-n // (256 * per)))
+    # MAP_UNROLL vectors per lane and no grid-stride loop: x + 1 / x * y at
+    # 2^30 fp32 1.75 / 2.58 ms with a 4096-block grid-stride loop, 1.34 / 2.01
+    # ms with the full grid (6.4 TB/s read+write; profiles/r02_map_grid.txt)
+    grid = max(1, -(-n // (256 * per * mu)))
     self.launch(fn, grid, args)
 
   # --------------------------------------------------------------- reduce

@@ -488,11 +488,13 @@ def named(src, base, kind):
 
 
 # ---------------------------------------------------------------- map
-def gen_map(root, inputs, classes, ndim, vec, dense, nt_store=False):
+def gen_map(root, inputs, classes, ndim, vec, dense, nt_store=False, unroll=1):
   """Elementwise kernel.  inputs: [(slot, dtype)], classes: per-input 'c'/'b'/'g'.
 
   dense=True: every input is contiguous with the output's shape (flat index).
   Otherwise the N-d path: offsets from the iteration index via dim[] / str[][].
+  unroll: grid steps per lane (dense vector path), all loads first; the
+  launch's grid is n / (256 vec unroll) (backend.MAP_UNROLL).
   """
   if rowdots(root):
     raise NotImplementedError('a fused row dot needs the column-reduce skeleton')
@@ -534,10 +536,9 @@ def gen_map(root, inputs, classes, ndim, vec, dense, nt_store=False):
   L.append('  if (a.flags & 1) {')
   L.append('    const i64 step = (i64)a.grid * 256 * %d;' % vec)
   L.append('    i64 e = ((i64)bidx() * 256 + tid()) * %d;' % vec)
-  # dense maps with one or two streamed inputs: U grid steps per iteration,
-  # all loads first (one 16-byte load per lane and step does not keep enough
-  # bytes in flight: x + 1 at 2^30 fp32 ran 4.5 TB/s read+write)
-  U = rows_unroll(inputs, ['c'] * len(inputs)) if dense and vec > 1 else 1
+  # dense maps: U grid steps per lane, all loads first (with the full grid,
+  # U = 1, every lane has one vector: profiles/r02_map_grid.txt)
+  U = unroll if dense and vec > 1 else 1
   if U > 1:
     L.append('    for (; e + %d * step < n; e += %d * step) {' % (U - 1, U))
     lines = []
