@@ -1625,14 +1625,17 @@ __device__ __forceinline__ float ks_max3(float a, float b, float c) {
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
-// (bits(a) & ~7) | ct.  Plain C, not inline asm: its operand comes straight
-// from an MFMA accumulator, and only compiler-generated instructions get the
-// MFMA -> VALU read wait states from the hazard recognizer (an asm
-// v_and_or_b32 there read stale accumulators: ~5 % wrong labels, caught by
-// the exact-kernel comparison).  An asm form placed three MFMAs after the
-// write measured no faster (tools/ks_variants.sh).
+// (bits(a) & ~7) | ct, ct < 8 (a centre tile; uniform).  Plain C, not inline
+// asm: its operand comes straight from an MFMA accumulator, and only
+// compiler-generated instructions get the MFMA -> VALU read wait states from
+// the hazard recognizer (an asm v_and_or_b32 there read stale accumulators:
+// ~5 % wrong labels, caught by the exact-kernel comparison).  The empty asm
+// hides ct's range from the compiler: with ct known < 8 it proved the or
+// disjoint and emitted v_and + v_add (two VALU per value) instead of one
+// v_and_or_b32.
 __device__ __forceinline__ float ks_tag(float a, unsigned int ct) {
-  return __builtin_bit_cast(float, (__builtin_bit_cast(unsigned int, a) & ~7u) | (ct & 7u));
+  asm("" : "+s"(ct));
+  return __builtin_bit_cast(float, (__builtin_bit_cast(unsigned int, a) & ~7u) | ct);
 }
 
 // Top-2 (largest) VALUES across the 32 lanes of each half (register halving
