@@ -2426,9 +2426,11 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
 
   // vector role of slot t: the decision of unit t - 2 and its add rounds
   // (dres[(t - 2) & 3]), the fold of unit t - 1 (exv[(t - 1) & 1]), the
-  // staging of unit t + 1.  Every wave of the group computes the decision
-  // (the same bits; wave 0 writes it): its LDS round trips run in the shadow
-  // of the fold's vector work, interleaved by hand (sched barriers).
+  // staging of unit t + 1.  Wave 0 of the group computes the decision and
+  // writes it (round 4: every wave computed the same bits; wave 0 alone is
+  // -0.05-0.1 ms, the kernel being power-limited): its LDS round trips run
+  // in the shadow of the fold's vector work, interleaved by hand (sched
+  // barriers).
   auto vector_role = [&](int tt, const kb_f4 (&rs)[NQ]) __attribute__((always_inline)) {
     const int u2 = tt - 2, uf = tt - 1, us = tt + 1;
     const bool dv = u2 >= 0 && u2 < nit, fv = uf >= 0 && uf < nit;
@@ -2436,10 +2438,15 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     const bool rlive = dv && grow < N;
     const unsigned char* er = exv + ((size_t)(u2 & 1) * U + j) * KP_XS;
     const unsigned char* pr = p2p + ((size_t)(u2 & 3) * U + j) * KP_XS;
-    // (1) the decision's loads
-    const kb_f4 e4 = *(const kb_f4*)(er + 16 * h);
-    const kfs_i2 i2 = *(const kfs_i2*)(er + 32 + 8 * h);
-    const kb_f4 p4 = *(const kb_f4*)(pr + 16 * h);
+    // (1) the decision's loads (wave 0 only: the other waves' decisions were
+    // the same bits, computed for nothing)
+    kb_f4 e4 = (kb_f4){0.f, 0.f, 0.f, 0.f}, p4 = (kb_f4){0.f, 0.f, 0.f, 0.f};
+    kfs_i2 i2 = (kfs_i2){0, 0};
+    if (s == 0) {
+      e4 = *(const kb_f4*)(er + 16 * h);
+      i2 = *(const kfs_i2*)(er + 32 + 8 * h);
+      p4 = *(const kb_f4*)(pr + 16 * h);
+    }
     // (2) fold, first tile (its latency cover)
     float lo0 = -INFINITY, sec0 = -INFINITY, lo1 = -INFINITY, sec1 = -INFINITY;
     int il0 = 0, il1 = 0;
@@ -2452,8 +2459,8 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     // by a correction pass, spx_kmeans_step).  dl: the label code stored
     // for the row: the label, -2 - d (provisional) or -1 (not added:
     // non-finite, or a ghost row).
-    int d, dl;
-    {
+    int d = -1, dl = -1;
+    if (s == 0) {
       const float b1 = ks_max(e4[0], e4[2]), b2 = ks_med3(e4[0], e4[2], ks_max(e4[1], e4[3]));
       const int ib = e4[0] >= e4[2] ? i2[0] : i2[1];
       const float pp = (p4[0] + p4[1]) + (p4[2] + p4[3]);
@@ -2576,19 +2583,21 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     };
     if (rnd == 0) rd();
     // labels (-1 for an undecided row: the list passes write it) and the
-    // unit's undecided-row mask; every store issued.  Lanes j and j + 32
-    // write the same label to the same word, and all 64 lanes the same mask
-    // word: the dummy word takes only ghost rows / units (a few per block).
-    // (With the idle lanes of every store aimed at ONE dummy word, all CUs'
-    // stores met on one L2 line; the vmcnt waits that count those stores
-    // cost ~3.7 ms per cfg3 pass -- profiles/r04_kp_ablate_v4.txt.)
+    // unit's undecided-row mask, each word stored ONCE: row j's label by lane
+    // j of wave j / 8, the mask by lane 0 of wave 0 (round 5: every wave's 64
+    // lanes stored every word, 8 label and 256 mask stores per word: -0.25 ms
+    // without them, profiles/r05_kp_redundant_ab.txt -- the kernel is power-
+    // limited).  The dummy word takes only ghost rows / units (a few per
+    // block).  (With the idle lanes of every store aimed at ONE dummy word,
+    // all CUs' stores met on one L2 line; the vmcnt waits that count those
+    // stores cost ~3.7 ms per cfg3 pass -- profiles/r04_kp_ablate_v4.txt.)
     auto stores = [&]() __attribute__((always_inline)) {
       const int dlab = av ? (int)(short)(dlv & 0xffff) : -1;
       i64* la = rlive ? labels + grow : (i64*)dummy;
-      *la = (i64)dlab;
+      if ((j >> 3) == s && h == 0) *la = (i64)dlab;
       const unsigned long long m = __ballot(dlab < 0 && rlive) & 0xffffffffull;
       unsigned long long* ma = av ? und_mask + una : dummy + 1;
-      *ma = m;
+      if (s == 0 && lane == 0) *ma = m;
     };
     auto mk = [&](auto kc) __attribute__((always_inline)) {
       constexpr int ks = decltype(kc)::value;
