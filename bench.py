@@ -190,6 +190,8 @@ def main():
   result['cfg2_map'] = bench_cfg2_extra('map', X, Y, Z, x, y, z, R, S, rows_local, be, expr, comm, sync)
   del x, y, z, X, Y, Z, last
   torch.cuda.empty_cache()
+  result['vendor_reduce'] = vendor_reduce(achieved)
+  torch.cuda.empty_cache()
 
   def leg(fn, *a):
     # a failing secondary leg is reported in the line, not allowed to take
@@ -291,6 +293,34 @@ def check_cfg2(last, x, y, z, R, S):
     xc, yc, zc = (distarray.glom_region(t, reg).astype(np.float64).ravel() for t in (x, y, z))
     ok &= _rel_ok(g0[j], np.sum(xc * yc + np.exp(zc)), 1e-5)
   return bool(ok)
+
+
+def vendor_reduce(achieved, n=1 << 30, runs=10):
+  """The same box's vendor reduction for comparison: ATen's torch.sum over one
+  2^30 fp32 tensor (4 GiB), HIP events on torch's stream, median of ``runs``.
+  ``cfg2_over_vendor`` = the cfg2 kernel's rate / this one (a comparison
+  point, not a ceiling: the read-stream ceiling of these boxes is 7.0-7.4
+  TB/s, profiles/r02_stream_ceiling_before.txt)."""
+  import torch
+  t = torch.empty(n, dtype=torch.float32, device='cuda').uniform_()
+  for _ in range(2):
+    t.sum()
+  torch.cuda.synchronize()
+  ms = []
+  for _ in range(runs):
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    t.sum()
+    b.record()
+    b.synchronize()
+    ms.append(a.elapsed_time(b))
+  del t
+  torch.cuda.empty_cache()
+  med = float(np.median(ms))
+  gbs = 4.0 * n / (med * 1e-3) / 1e9
+  return {'kernel': 'torch.sum over one 2^30 fp32 tensor (ATen reduce)', 'ms': round(med, 4), 'GBps': round(gbs, 1),
+          'frac': round(gbs / HBM_PEAK_GBS, 4),
+          'cfg2_over_vendor': round(achieved / gbs, 4) if achieved else None}
 
 
 def _ranks_seen():
