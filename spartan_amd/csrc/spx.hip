@@ -2197,15 +2197,15 @@ static void ks_launch_n(int nct, hipStream_t s, i64 N, i64 D, const float* P, i6
 // pipe busy while its partner does vector / LDS work (MI355X_MICROARCH.md
 // "Two waves per SIMD"):
 //   matrix role (group t & 1): the screen of unit t -- wave s holds centre
-//     tiles 2s, 2s + 1 (64 centres) as the fp16 MFMA A operand plus their
-//     -cc/2 pieces; two chains of 8 v_mfma_f32_32x32x16_f16 + 1 bf16 MFMA
-//     (-cc/2) over unit t's fp16 x' (LDS) give S - cc/2 = -a''/2 for 64
-//     centres x 32 rows.  Woven between those MFMAs: the read-add-writes of
+//     tiles 2s, 2s + 1 (64 centres) as the fp16 MFMA A operand; two chains
+//     of 8 v_mfma_f32_32x32x16_f16 over unit t's fp16 x' (LDS), started from
+//     -cc/2 (an LDS table in accumulator order), give S - cc/2 = -a''/2 for
+//     64 centres x 32 rows.  Woven between those MFMAs: the read-add-writes of
 //     unit t - 4's decided rows (this group's unit whose decision the other
 //     group made in slot t - 2) into the LDS sums; then that unit's labels
 //     and undecided bits, and the loads of unit t + 4;
 //   vector role (the other group): the decision of unit t - 2 (the matrix
-//     group's unit, folded in slot t - 1) with the add rounds of its rows,
+//     group's unit, folded in slot t - 1; wave 0) with the add rounds of its rows,
 //     written to LDS for its adds in slot t + 2; the fold of unit t - 1's
 //     accumulators (this group's matrix role of slot t - 1) to per-row top-2
 //     candidates; the staging of unit t + 1 (x' = fl(x - mu), fp16(x') to
@@ -2225,16 +2225,15 @@ static void ks_launch_n(int nct, hipStream_t s, i64 N, i64 D, const float* P, i6
 // the loads landed in and waves never share an address.  Two rows of one
 // centre in one unit would race in a plain read-add-write, so the adds go in
 // rounds: a row's round is its rank among the unit's rows of its centre,
-// from one LDS atomic increment per decided row on a counter table (the
-// decision's wave; the lanes of one instruction that hit one counter are
+// from one LDS atomic increment per decided row on a counter table (wave
+// 0, the decision's; the lanes of one instruction that hit one counter are
 // ordered the same way every time), and the round loop runs to the unit's
 // largest rank (< 32 by construction: no data-dependent bound to guard).
 // The order of every add is fixed: the sums are deterministic.  Every KP_FW
 // units the fp32 sums go by plain stores to the block's partial slot for
 // that window and are cleared; the slots are summed in fp64 in a fixed order
-// after the kernel.  Global stores are issued unconditionally (ghost rows
-// write a dummy word), so the count of loads in flight that the compiler
-// tracks is the same in every slot.
+// after the kernel.  Each label / mask word is stored once, by one lane
+// (ghost rows write a dummy word).
 typedef float kfs_f2 __attribute__((ext_vector_type(2)));
 typedef int kfs_i2 __attribute__((ext_vector_type(2)));
 __host__ __device__ constexpr int kfs_rs(int D) { return 2 * D + 16; }  // fp16 row stride: +16 B keeps ds_read_b128 conflict-free
