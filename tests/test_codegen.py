@@ -135,3 +135,14 @@ def test_rowdot_interleaved_rows_compile():
     _compile(src)
     assert 'for (i64 sb' not in codegen.gen_reduce(root, ins, ['c', 'b', 'c'], 'cols', 'sum', V, 8, (2,),
                                                    lpr=16, full=True)
+
+
+@pytest.mark.parametrize('unroll', [1, 2, 4])
+def test_dense_map_unroll_compiles(unroll):
+  """backend.MAP_UNROLL: U vectors per lane (all loads first) for the dense
+  vector path; U = 1 has no unrolled loop at all (the full-grid default)."""
+  root = Op('add', [Op('multiply', [In(0, F32), In(1, F32)]), Op('exp', [In(2, F32)])])
+  ins = [(0, F32), (1, F32), (2, F32)]
+  src = codegen.gen_map(root, ins, ['c'] * 3, 1, 4, True, True, unroll)
+  assert ('e + %d * step < n' % (unroll - 1) in src) == (unroll > 1)
+  _compile(src)
