@@ -2249,7 +2249,8 @@ static_assert(KP_FW % KP_UNR == 0 && KP_UNR == 2 * KP_NR && KP_AHEAD + KP_LAG ==
               "flush points fall on the unrolled body's first slot; the ring cycles once per body");
 static size_t kp_lds_bytes(int D) {
   return (size_t)256 * D * 4 + 256 * 4 + (size_t)2 * KP_U * kfs_rs(D) + (size_t)2 * KP_U * KP_XS +
-         (size_t)4 * KP_U * KP_XS + (size_t)4 * KP_U * 4 + 256 * 4 + (size_t)8 * 2 * 16 * 4 + (size_t)D * 4;
+         (size_t)4 * KP_U * KP_XS + (size_t)4 * KP_U * 4 + 256 * 4 + (size_t)8 * 2 * 16 * 4 + (size_t)D * 4 +
+         (size_t)4 * KP_U * 4;
 }
 
 template <int KS, int NCT>
@@ -2277,6 +2278,7 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
   unsigned int* rcnt = (unsigned int*)(dres + 4 * U);    // [256] rows per centre so far in the unit (rank counters)
   float* cci = (float*)(rcnt + 256);                     // [8 tiles][2 halves][16]: -cc/2 of a lane's accumulator centres
   float* mus = cci + 8 * 2 * 16;                         // [D] the centring vector mu
+  float* ebuf = mus + D;                                 // [4][U]: a row's bound e (NaN: no decision), by unit mod 4
   // (j, h): the MFMA / fold / decision lanes (row j = lane & 31, k-half or
   // centre half h = lane >> 5).  (jr, hr): the raw-column lanes (row jr =
   // lane >> 1, column half hr = lane & 1) of the loads, the staging and the
@@ -2436,21 +2438,42 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     const i64 grow = (bk + (i64)(dv ? u2 : 0) * G) * U + j;
     const bool rlive = dv && grow < N;
     const unsigned char* er = exv + ((size_t)(u2 & 1) * U + j) * KP_XS;
-    const unsigned char* pr = p2p + ((size_t)(u2 & 3) * U + j) * KP_XS;
     // (1) the decision's loads (wave 0 only: the other waves' decisions were
-    // the same bits, computed for nothing)
-    kb_f4 e4 = (kb_f4){0.f, 0.f, 0.f, 0.f}, p4 = (kb_f4){0.f, 0.f, 0.f, 0.f};
+    // the same bits, computed for nothing); the rows' bounds e come ready
+    // from wave 1 of the previous slot (step (2b))
+    kb_f4 e4 = (kb_f4){0.f, 0.f, 0.f, 0.f};
     kfs_i2 i2 = (kfs_i2){0, 0};
+    float er_e = 0.f;
     if (s == 0) {
       e4 = *(const kb_f4*)(er + 16 * h);
       i2 = *(const kfs_i2*)(er + 32 + 8 * h);
-      p4 = *(const kb_f4*)(pr + 16 * h);
+      er_e = ebuf[(u2 & 3) * U + j];
     }
     // (2) fold, first tile (its latency cover)
     float lo0 = -INFINITY, sec0 = -INFINITY, lo1 = -INFINITY, sec1 = -INFINITY;
     int il0 = 0, il1 = 0;
     if (scr0) fold16(acc0, 2 * s, lo0, sec0, il0);  // (unused when !fv: exv is written only if fv)
     __builtin_amdgcn_sched_barrier(0);
+    // (2b) wave 1 (off the critical path: it makes no decision) prepares the
+    // bound of the unit decided in the NEXT slot, t - 1 (staged in slot t - 2,
+    // its |x'|^2 partials complete): the sum of the 8 column partials, |p|,
+    // e(|p|) and the finiteness / range checks, exactly as the decision did
+    // them (the same order: bit-identical decisions), NaN for a row the
+    // screen cannot decide.  (Round 5: the decision wave is the slot's
+    // critical path, ~400 cycles longer than the other waves' vector roles,
+    // tools/kp_roles.py.)
+    if (s == 1) {
+      const int ue = tt - 1;
+      const kb_f4 p4 = *(const kb_f4*)(p2p + ((size_t)(ue & 3) * U + j) * KP_XS + 16 * h);
+      const float pp = (p4[0] + p4[1]) + (p4[2] + p4[3]);
+      float pl, ph;
+      sw32(pp, pl, ph);
+      const float p2f = pl + ph;  // the same order in both lanes of the row
+      const float pn = __builtin_amdgcn_sqrtf(__builtin_fmaf(p2f, 1.001f, 1e-37f)) * 1.0001f;
+      const float e = __builtin_fmaf(__builtin_fmaf(kq[2], pn, kq[1]), pn, kq[0]) * 1.0001f;
+      const bool ok = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim;
+      if (h == 0) ebuf[(ue & 3) * U + j] = ok ? e : __builtin_nanf("");
+    }
     // (3) decide: top-2 over the 4 waves' candidates, the certified rule.
     // d: the centre the row is added to -- its label when decided, and,
     // PROVISIONALLY, the screen's best for a finite undecided row (the list
@@ -2462,18 +2485,14 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
     if (s == 0) {
       const float b1 = ks_max(e4[0], e4[2]), b2 = ks_med3(e4[0], e4[2], ks_max(e4[1], e4[3]));
       const int ib = e4[0] >= e4[2] ? i2[0] : i2[1];
-      const float pp = (p4[0] + p4[1]) + (p4[2] + p4[3]);
-      float b1l, b1h, b2l, b2h, fl, fh, pl, ph;
+      float b1l, b1h, b2l, b2h, fl, fh;
       sw32(b1, b1l, b1h);
       sw32(b2, b2l, b2h);
       sw32(__builtin_bit_cast(float, ib), fl, fh);
-      sw32(pp, pl, ph);
       const float B1 = ks_max(b1l, b1h), B2 = ks_med3(b1l, b1h, ks_max(b2l, b2h));
       const int IB = b1l >= b1h ? __builtin_bit_cast(int, fl) : __builtin_bit_cast(int, fh);
-      const float p2f = pl + ph;  // the same order in both lanes of the row
-      const float pn = __builtin_amdgcn_sqrtf(__builtin_fmaf(p2f, 1.001f, 1e-37f)) * 1.0001f;
-      const float e = __builtin_fmaf(__builtin_fmaf(kq[2], pn, kq[1]), pn, kq[0]) * 1.0001f;
-      const bool fin = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim && isfinite(B1) && isfinite(B2);
+      const float e = er_e;  // NaN: not finite, out of range, or cok false (2b)
+      const bool fin = isfinite(e) && isfinite(B1) && isfinite(B2);
       const bool dec = fin && B1 - B2 > 1.0001f * e;
       const bool add = rlive && fin && IB < (int)K;
       d = add ? IB : -1;
