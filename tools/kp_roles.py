@@ -49,6 +49,9 @@ def main():
     tot = a[:, w0:w1, 2].mean() / slots
     print('  %s: matrix role %6.0f  vector role %6.0f  slot (wall) %6.0f  => barrier wait %6.0f' % (
         name, m, v, tot, tot - (m + v) / 2))
+  for w in range(8):
+    print('    wave %d (SIMD %d): matrix role %6.0f  vector role %6.0f' % (
+        w, w & 3, a[:, w, 0].mean() / (slots / 2), a[:, w, 1].mean() / (slots / 2)))
 
 
 if __name__ == '__main__':
