@@ -5,7 +5,9 @@
 # steps: tests bench trace2 lregpmc (default: all, in that order).  A step
 # that ends in a fault, abort, signal or time limit stops the session (no
 # further GPU work in this call); an ordinary test failure (pytest exit 1)
-# does not.
+# does not.  The steps that load dev builds from tools/bin/ (kab, kclk,
+# ablate, gemm*) need that directory uploaded: .gpurunignore lists it (the
+# round-end runs never read it), so drop that line for such a session.
 R=$GRAFT_REPO_ROOT
 T=${1:-sess}
 shift
