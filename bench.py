@@ -91,7 +91,12 @@ def main():
   import spartan_amd
   from spartan_amd import backend, comm, expr, runtime
 
-  ctx = spartan_amd.initialize()
+  try:
+    ctx = spartan_amd.initialize()
+  except runtime.DataPlaneError as e:
+    # the data plane's start-up self-test names the failing collective
+    sys.stderr.write('bench.py: rank %s: %s\n' % (os.environ.get('RANK', '0'), e))
+    sys.exit(4)
   be = backend.get()
   assert isinstance(be, backend.HipBackend)
   S = args.size
@@ -160,6 +165,7 @@ def main():
       'n_ranks_seen': _ranks_seen(),
       'dist_backend': ctx.dist_backend,
       'dataplane_selftest': getattr(ctx, 'selftest', None),
+      'pg_timeout_s': getattr(ctx, 'pg_timeout', None),
       'steps': args.steps,
       'warmup': args.warmup,
       'ms_per_step': round(elapsed / args.steps * 1e3, 4),
@@ -481,11 +487,53 @@ def bench_dot(S, ctx, be, expr, comm, sync, runs=10, warm=2):
       km = float(np.sum(gemm_ms)) / runs
       out[name]['kernel_ms'] = round(km, 3)
       out[name]['kernel_mfma_frac'] = round(flops / (km * 1e-3) / 1e12 / peak, 4)
+    if ctx.world_size == 1 and os.environ.get('SPARTAN_BENCH_VENDOR_GEMM', '1') != '0':
+      try:
+        out[name]['vendor'] = vendor_gemm(a, b, S, peak, out[name].get('kernel_ms'))
+      except Exception as e:  # noqa: BLE001  (a comparison point: reported, not fatal)
+        out[name]['vendor'] = {'error': '%s: %s' % (type(e).__name__, str(e)[:200])}
     del a, b, A, B
     torch.cuda.empty_cache()
   out['config'] = ('dot(A, B), A, B ~ U[0,1) (%d, %d), K-split over ranks; median of %d runs after %d warm-ups'
                    % (S, S, runs, warm))
   return out
+
+
+def vendor_gemm(a, b, S, peak, ours_ms, runs=5, warm=2):
+  """The same box's vendor GEMM on the same resident operands: torch.matmul
+  (hipBLASLt / rocBLAS through ATen; TF32-style reduced precision off, so
+  fp32 is computed in fp32), HIP events on torch's stream, median of
+  ``runs`` after ``warm`` warm-ups.  ``ours_over_vendor`` = the vendor's
+  kernel time / spx_gemm's (> 1: ours is faster)."""
+  import torch
+  ta = next(iter(a.local.values())).data
+  tb = next(iter(b.local.values())).data
+  assert tuple(ta.shape) == (S, S) and tuple(tb.shape) == (S, S)
+  prev = torch.backends.cuda.matmul.allow_tf32
+  torch.backends.cuda.matmul.allow_tf32 = False
+  try:
+    c = torch.empty((S, S), dtype=ta.dtype, device=ta.device)
+    for _ in range(warm):
+      torch.matmul(ta, tb, out=c)
+    torch.cuda.synchronize()
+    ms = []
+    for _ in range(runs):
+      e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+      e0.record()
+      torch.matmul(ta, tb, out=c)
+      e1.record()
+      e1.synchronize()
+      ms.append(e0.elapsed_time(e1))
+    del c
+  finally:
+    torch.backends.cuda.matmul.allow_tf32 = prev
+    torch.cuda.empty_cache()
+  med = float(np.median(ms))
+  tf = 2.0 * S ** 3 / (med * 1e-3) / 1e12
+  return {'kernel': 'torch.matmul (ATen -> hipBLASLt / rocBLAS), allow_tf32=False', 'ms': round(med, 3),
+          'ms_min_max': [round(min(ms), 3), round(max(ms), 3)], 'tflops': round(tf, 1),
+          'mfma_frac': round(tf / peak, 4),
+          'ours_over_vendor': round(med / ours_ms, 4) if ours_ms else None}
 
 
 def check_dot(c, A, B, S, dt, expr):

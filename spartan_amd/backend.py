@@ -433,7 +433,10 @@ class HipBackend:
     pkey = (root.sig(), op, tuple((s, inputs[s].dtype, tuple(inputs[s].shape), inputs[s].stride(),
                                    inputs[s].data_ptr() % 16) for s in slots),
             tuple(in_shape), axis, tuple(out_shape), np.dtype(out_dtype).str,
-            None if idx_geom is None else repr(sorted(idx_geom.items())))
+            None if idx_geom is None else repr(sorted(idx_geom.items())),
+            # the module's grid / layout knobs shape the plan too
+            (ROWS_GRID_PER_CU, COLS_BLOCKS_PER_CU, COLS_INTERLEAVE, ROWDOT_BLOCKS_PER_CU, ROWDOT_UNROLL,
+             ROWDOT_INTERLEAVE))
     plan = self._reduce_plans.get(pkey)
     if plan is not None:
       return self._replay_reduce(plan, root, inputs, slots, out_shape, out_dtype)
@@ -567,13 +570,22 @@ class HipBackend:
         args.aux[6] = len(tshape)
         for d in range(len(tshape)):
           args.tshape[d], args.tul[d], args.ashape[d] = tshape[d], tul[d], ashape[d]
+    # a fused row dot's lane group width (and whether the vector path covers
+    # the columns exactly) is compiled in: its per-row lane sum is then
+    # straight-line DPP (codegen.gen_reduce)
+    klpr, kfull = None, False
+    if kind == 'cols' and codegen.rowdots(root):
+      klpr, kfull = lpr, bool(vec_ok and CT == 1 and I == lpr * per)
+    kint = bool((klpr and ROWDOT_INTERLEAVE) or (kind == 'cols' and CT > 1 and op == 'sum' and COLS_INTERLEAVE))
+    # partials' dtype: fp64 for an interleaved fp32 sum (codegen.partial_dtype)
+    pdt = codegen.partial_dtype(op, adt, kint) if kind == 'cols' else adt
     if arg:
       direct = P == 1
       part_v = res_v if direct else torch.empty((P * n_out,), dtype=torch_dtype(adt), device=dev)
       part_i = result if direct else torch.empty((P * n_out,), dtype=torch.int64, device=dev)
     else:
-      direct = (P == 1 and adt == np.dtype(out_dtype))
-      part_v = result if direct else torch.empty((P * n_out,), dtype=torch_dtype(adt), device=dev)
+      direct = (P == 1 and pdt == np.dtype(out_dtype))
+      part_v = result if direct else torch.empty((P * n_out,), dtype=torch_dtype(pdt), device=dev)
       part_i = None
     args.out0 = part_v.data_ptr()
     args.out1 = part_i.data_ptr() if arg else 0
@@ -583,13 +595,6 @@ class HipBackend:
       if codegen.rowdots(root):
         U = ROWDOT_UNROLL
       rowinv = tuple(s for k, s in enumerate(slots) if vstr[k][1] == 0)
-    # a fused row dot's lane group width (and whether the vector path covers
-    # the columns exactly) is compiled in: its per-row lane sum is then
-    # straight-line DPP (codegen.gen_reduce)
-    klpr, kfull = None, False
-    if kind == 'cols' and codegen.rowdots(root):
-      klpr, kfull = lpr, bool(vec_ok and CT == 1 and I == lpr * per)
-    kint = bool((klpr and ROWDOT_INTERLEAVE) or (kind == 'cols' and CT > 1 and op == 'sum' and COLS_INTERLEAVE))
     sig = ('reduce', root.sig(), tuple(ins), tuple(classes), kind, op, V, U, rowinv, klpr, kfull, kint)
     fn = self._sig_fns.get(sig)
     if fn is None:
@@ -599,13 +604,13 @@ class HipBackend:
     self.launch(fn, nblk, args)
     if not direct:
       _check(self.lib.spx_reduce_finalize(
-          OP_CODE[op], spx_dtype(adt), spx_dtype(np.int64 if arg else out_dtype),
+          OP_CODE[op], spx_dtype(pdt), spx_dtype(np.int64 if arg else out_dtype),
           ctypes.c_void_p(part_v.data_ptr()), ctypes.c_void_p(part_i.data_ptr() if arg else 0), P, n_out,
           ctypes.c_void_p(result.data_ptr()), ctypes.c_void_p(res_v.data_ptr() if arg else 0),
           self.stream()), 'spx_reduce_finalize')
     if len(self._reduce_plans) >= 512:
       self._reduce_plans.clear()
-    self._reduce_plans[pkey] = (fn, nblk, bytes(args), arg, direct, adt, P, n_out, dev, OP_CODE[op])
+    self._reduce_plans[pkey] = (fn, nblk, bytes(args), arg, direct, pdt, P, n_out, dev, OP_CODE[op])
     return (res_v, result) if arg else result
 
   def _replay_reduce(self, plan, root, inputs, slots, out_shape, out_dtype):

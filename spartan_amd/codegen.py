@@ -587,6 +587,15 @@ def acc_dtype(op, dt):
   return dt
 
 
+def partial_dtype(op, adt, interleave):
+  """dtype of a column reduction's per-block partials: fp64 for an
+  interleaved fp32 sum (its lane totals are fp64, codegen 'cols'), else the
+  accumulator dtype."""
+  if interleave and op == 'sum' and np.dtype(adt) == np.float32:
+    return np.dtype(np.float64)
+  return np.dtype(adt)
+
+
 def _ident(op, dt):
   ct = ctype(dt)
   if op == 'sum':
@@ -849,6 +858,9 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=(), lpr
     L.append('}')
   else:
     U = unroll or cols_unroll(inputs, classes, vec)
+    lv = interleave and op == 'sum'
+    pact = ctype(partial_dtype(op, adt, interleave))
+    kahan = lv and pact == 'double' and act == 'double'
 
     def one_row(V, rv, sfx, masked, bcu=None):
       """Loads + (row dots) + accumulator updates of row ``rv`` into names
@@ -945,18 +957,21 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=(), lpr
                 for j, v in enumerate(srcs)]
           b.append('  }')
       b.append('  const i64 STEP = 4 * RPW;')
-      lv = interleave and op == 'sum'
       if interleave:
         # block p takes the U-step super-chunks p, p + P, p + 2P, ...: at any
         # moment the grid streams one contiguous stretch of X instead of P
         # streams far apart (one chunk per block).  A block then covers R / P
         # rows, so (sums) each super-chunk's U rows go into a fresh
-        # accumulator that is folded into a middle one, and every 32 chunks
-        # the middle one into the block's total: fp32 chains of U + 32 +
-        # R / (32 P U 16) additions per lane instead of R / (16 P)
+        # accumulator (in the input's precision: U additions) that is folded
+        # into a middle one, and every 32 chunks the middle one into the
+        # block's total.  Middle and total are fp64 (round 6; fp32 inputs:
+        # only the U-row chunk sums round to fp32, everything above them --
+        # lane total, LDS combine, partials, finalize -- is fp64), and for
+        # fp64 inputs the total is Kahan-compensated (topc)
         if lv:
-          b.append('  %s %s;' % (act, ', '.join('mid%d = (%s)0, top%d = (%s)0' % (j, act, j, act)
-                                                for j in range(V))))
+          b.append('  %s %s;' % (pact, ', '.join('mid%d = 0.0, top%d = 0.0' % (j, j) for j in range(V))))
+          if kahan:
+            b.append('  double %s;' % ', '.join('topc%d = 0.0' % j for j in range(V)))
           b.append('  int nsc = 0;')
         b.append('  for (i64 sb = p * (%d * STEP); sb < R; sb += P * (%d * STEP)) {' % (U, U))
         b.append('  const i64 r0 = sb; i64 r1 = sb + %d * STEP; if (r1 > R) r1 = R;' % U)
@@ -984,16 +999,23 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=(), lpr
       if interleave:
         if lv:
           for j in range(V):
-            b.append('  mid%d = mid%d + acc%d; acc%d = (%s)0;' % (j, j, j, j, act))
+            b.append('  mid%d = mid%d + (%s)acc%d; acc%d = (%s)0;' % (j, j, pact, j, j, act))
           b.append('  if (++nsc == 32) {')
           for j in range(V):
-            b.append('    top%d = top%d + mid%d; mid%d = (%s)0;' % (j, j, j, j, act))
+            if kahan:
+              b.append('    { const double y_ = mid%d - topc%d, t_ = top%d + y_; topc%d = (t_ - top%d) - y_; '
+                       'top%d = t_; } mid%d = 0.0;' % (j, j, j, j, j, j, j))
+            else:
+              b.append('    top%d = top%d + mid%d; mid%d = 0.0;' % (j, j, j, j))
           b.append('    nsc = 0;')
           b.append('  }')
         b.append('  }')
         if lv:
           for j in range(V):
-            b.append('  acc%d = top%d + mid%d;' % (j, j, j))
+            if kahan:
+              b.append('  fin%d = top%d + (mid%d - topc%d);' % (j, j, j, j))
+            else:
+              b.append('  fin%d = top%d + mid%d;' % (j, j, j))
       b.append('}')
       return b
 
@@ -1017,6 +1039,8 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=(), lpr
       L.append('  %s acc%d = %s;' % (act, j, _ident(op, adt)))
       if arg:
         L.append('  i64 acci%d = 0x7fffffffffffffffLL;' % j)
+      if lv:
+        L.append('  %s fin%d = 0.0;' % (pact, j))
     L.append('  if (a.flags & 1) {')
     L += ['    ' + x for x in body(vec)]
     L.append('  } else {')
@@ -1024,29 +1048,32 @@ def gen_reduce(root, inputs, classes, kind, op, vec, unroll=None, rowinv=(), lpr
     L.append('  }')
     if arg:
       L += ['  ' + x for x in to_global()]
-    # LDS combine over the 4*RPW row groups sharing a column, in row-group order
-    L.append('  SHARED %s sv[256 * %d];' % (act, vec))
+    # LDS combine over the 4*RPW row groups sharing a column, in row-group
+    # order (in the partials' type: fp64 for an interleaved fp32 sum)
+    L.append('  SHARED %s sv[256 * %d];' % (pact, vec))
     if arg:
       L.append('  SHARED i64 si[256 * %d];' % vec)
     L.append('  const i64 grp = w * RPW + sub;')
     L.append('  const i64 W = LPR * V;')
     for j in range(vec):
-      L.append('  if (%d < V) { sv[grp * W + cl * V + %d] = acc%d;%s }'
-               % (j, j, j, (' si[grp * W + cl * V + %d] = acci%d;' % (j, j)) if arg else ''))
+      L.append('  if (%d < V) { sv[grp * W + cl * V + %d] = %s%d;%s }'
+               % (j, j, 'fin' if lv else 'acc', j, (' si[grp * W + cl * V + %d] = acci%d;' % (j, j)) if arg else ''))
     L.append('  bsync();')
     L.append('  if ((i64)t < W) {')
-    L.append('    %s b = sv[t];' % act)
+    L.append('    %s b = sv[t];' % pact)
     if arg:
       L.append('    i64 bi = si[t];')
     L.append('    for (i64 g = 1; g < 4 * RPW; ++g) {')
     if arg:
       L.append('      if (better(sv[g * W + t], si[g * W + t], b, bi)) { b = sv[g * W + t]; bi = si[g * W + t]; }')
+    elif lv:
+      L.append('      b = b + sv[g * W + t];')
     else:
       L.append('      b = comb(b, sv[g * W + t]);')
     L.append('    }')
     L.append('    const i64 gc = ct * W + t;')
     L.append('    if (gc < I) {')
-    L.append('      ((GLOBAL %s*)a.out0)[(p * O + o) * I + gc] = b;' % act)
+    L.append('      ((GLOBAL %s*)a.out0)[(p * O + o) * I + gc] = b;' % pact)
     if arg:
       L.append('      ((GLOBAL i64*)a.out1)[(p * O + o) * I + gc] = bi;')
     L.append('    }')

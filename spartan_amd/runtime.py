@@ -34,8 +34,9 @@ class Context:
     self.rccl = rccl                   # libspx RCCL communicator handle when dist_backend == 'rccl'
     self._comm_stream = None
     self.pg = None          # torch process group of the data plane when dist_backend == 'nccl' (None: default)
-    self.selftest = None    # data-plane self-test verdict at start-up (multi-rank RCCL only)
+    self.selftest = None    # data-plane self-test verdict at start-up (every multi-rank data plane)
     self.ctl = None         # gloo group of the control plane when the default group is nccl (None: default)
+    self.pg_timeout = None  # seconds: the process groups' collective timeout (world > 1)
     self.num_workers = int(FLAGS.num_workers or world_size)
     if self.num_workers < 1:
       raise ValueError('num_workers must be >= 1')
@@ -82,6 +83,22 @@ def data_plane(device_type, env=None):
   if backend == 'rccl' and (env.get('SPARTAN_COMM') == 'torch' or device_type != 'cuda'):
     backend = 'nccl' if device_type == 'cuda' else 'gloo'
   return backend
+
+
+class DataPlaneError(RuntimeError):
+  """The multi-rank data plane failed its start-up self-test (the message
+  names the first failing collective)."""
+
+
+def pg_timeout_s(env=None):
+  """Timeout (s) of the torch.distributed process groups: a collective that
+  never completes aborts the job after this long instead of torch's default
+  (``SPARTAN_NCCL_TIMEOUT``, default 300)."""
+  env = os.environ if env is None else env
+  t = float(env.get('SPARTAN_NCCL_TIMEOUT', '300'))
+  if not t > 0:
+    raise ValueError('SPARTAN_NCCL_TIMEOUT must be > 0, not %r' % env.get('SPARTAN_NCCL_TIMEOUT'))
+  return t
 
 
 def _rccl_init_bounded(comm, rank, world, uid, device, timeout):
@@ -133,6 +150,7 @@ def initialize(argv=None, device=None):
   ``device`` overrides the device (tests run the host logic on 'cpu' with a
   test backend and gloo)."""
   global _ctx
+  import datetime
   import torch
   if argv is not None:
     FLAGS.parse(list(argv))
@@ -149,19 +167,20 @@ def initialize(argv=None, device=None):
   rccl = None
   init_err = None
   ctl = None
+  pg_timeout = pg_timeout_s()
   if world > 1:
     import torch.distributed as dist
     backend = data_plane(device.type)
     pg = 'nccl' if backend == 'nccl' else 'gloo'   # torch.distributed: control plane (or the torch RCCL path)
     if not dist.is_initialized():
       os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-      kw = {}
+      kw = {'timeout': datetime.timedelta(seconds=pg_timeout)}
       if device.type == 'cuda' and pg == 'nccl':
         kw['device_id'] = device
       dist.init_process_group(backend=pg, rank=rank, world_size=world, **kw)
     if dist.get_backend() == 'nccl':
       # the SPMD guard and host maxima never share the data plane's communicator
-      ctl = dist.new_group(backend='gloo')
+      ctl = dist.new_group(backend='gloo', timeout=datetime.timedelta(seconds=pg_timeout))
     if backend == 'rccl':
       from . import comm
       obj = [None]
@@ -178,6 +197,19 @@ def initialize(argv=None, device=None):
         init_err = 'rank 0 could not make an RCCL unique id (%s)' % obj[0]
   _ctx = Context(rank, world, local_rank, device, backend, rccl)
   _ctx.ctl = ctl
+  if world > 1:
+    _ctx.pg_timeout = pg_timeout
+  if world > 1 and backend != 'rccl' and os.environ.get('SPARTAN_SELFTEST', '1') != '0':
+    # the default data plane (torch's RCCL group; gloo in the CPU tests) is
+    # checked the same way before any tile moves: every collective once,
+    # bounded, the verdict agreed over ranks -- a failure names the
+    # collective and stops the run here instead of in the first tile
+    # exchange (which would sit until the process group's timeout)
+    from . import comm
+    err = comm.selftest()
+    _ctx.selftest = err or 'ok'
+    if err:
+      raise DataPlaneError('spartan_amd: the %s data plane failed its start-up self-test: %s' % (backend, err))
   if backend == 'rccl':
     from . import comm
     # every rank learns whether any rank's communicator failed to come up

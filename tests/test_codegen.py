@@ -132,6 +132,13 @@ def test_rowdot_interleaved_rows_compile():
     src = codegen.gen_reduce(root, ins, ['c', 'b', 'c'], 'cols', 'sum', V, 8, (2,), lpr=16, full=True,
                              interleave=True)
     assert src.count('for (i64 sb = p * (8 * STEP); sb < R; sb += P * (8 * STEP))') == 2
+    # round 6: the chunk sums fold into fp64 middle / total accumulators, the
+    # LDS combine and the partials are fp64; fp64 inputs Kahan the total
+    assert 'double mid0 = 0.0, top0 = 0.0' in src
+    assert 'SHARED double sv[' in src and '((GLOBAL double*)a.out0)' in src
+    assert ('topc0' in src) == (dt == F64)
+    assert codegen.partial_dtype('sum', dt, True) == F64
+    assert codegen.partial_dtype('sum', dt, False) == dt
     _compile(src)
     assert 'for (i64 sb' not in codegen.gen_reduce(root, ins, ['c', 'b', 'c'], 'cols', 'sum', V, 8, (2,),
                                                    lpr=16, full=True)

@@ -42,8 +42,10 @@ def _body(rank, world, port, W, q):
     sys.path.insert(0, os.path.dirname(HERE))
     sys.path.insert(0, HERE)
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), SPARTAN_SPMD_GUARD='strict')
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), SPARTAN_SPMD_GUARD='strict',
+                      SPARTAN_NCCL_TIMEOUT='240')
     import torch
+    import torch.distributed as dist
     from spartan_amd import backend, runtime, expr, comm
     from spartan_amd.config import FLAGS
     from fake_backend import FakeBackend
@@ -54,7 +56,13 @@ def _body(rank, world, port, W, q):
     runtime.initialize(device='cpu')
     ctx = runtime.get()
     assert ctx.world_size == world and ctx.dist_backend == 'gloo'
-    # the data-plane self-test the runtime runs on a multi-rank RCCL start
+    # round 6: the default data plane is self-tested at start-up (every
+    # collective once, verdict agreed over ranks) and its process group has
+    # a bounded timeout (SPARTAN_NCCL_TIMEOUT) instead of torch's default
+    assert ctx.selftest == 'ok', ctx.selftest
+    assert ctx.pg_timeout == 240.0
+    pg = dist.distributed_c10d._get_default_group()
+    assert pg._get_backend(torch.device('cpu')).options._timeout.total_seconds() == 240.0
     assert comm.selftest() is None
 
     # placement: only the local tiles hold data
@@ -203,6 +211,53 @@ def _diverge_body(rank, world, port, q):
   except Exception:  # pragma: no cover
     import traceback
     q.put((rank, traceback.format_exc()))
+
+
+def _selftest_fail_body(rank, world, port, q):
+  """A data plane whose start-up self-test fails (here: comm.selftest
+  reports a broken send/recv on every rank) stops initialize on every rank
+  with DataPlaneError naming the collective."""
+  try:
+    sys.path.insert(0, os.path.dirname(HERE))
+    sys.path.insert(0, HERE)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from spartan_amd import backend, runtime, comm
+    from fake_backend import FakeBackend
+    backend.set_backend(FakeBackend())
+    comm.selftest = lambda timeout=None: 'send/recv: wrong result on rank 1'
+    try:
+      runtime.initialize(device='cpu')
+      q.put((rank, 'no error'))
+    except runtime.DataPlaneError as e:
+      q.put((rank, 'raised' if 'send/recv' in str(e) and 'gloo' in str(e) else repr(e)))
+  except Exception:  # pragma: no cover
+    import traceback
+    q.put((rank, traceback.format_exc()))
+
+
+def test_default_data_plane_selftest_failure_raises():
+  import multiprocessing as mp
+  ctx = mp.get_context('spawn')
+  q = ctx.Queue()
+  port = _free_port()
+  procs = [ctx.Process(target=_selftest_fail_body, args=(r, 2, port, q)) for r in range(2)]
+  for p in procs:
+    p.start()
+  res = dict(q.get(timeout=120) for _ in procs)
+  for p in procs:
+    p.join(timeout=30)
+    if p.is_alive():
+      p.kill()
+  assert res == {0: 'raised', 1: 'raised'}, res
+
+
+def test_pg_timeout_env():
+  from spartan_amd import runtime
+  assert runtime.pg_timeout_s({}) == 300.0
+  assert runtime.pg_timeout_s({'SPARTAN_NCCL_TIMEOUT': '45'}) == 45.0
+  with pytest.raises(ValueError):
+    runtime.pg_timeout_s({'SPARTAN_NCCL_TIMEOUT': '0'})
 
 
 def test_spmd_guard_divergence_raises():
