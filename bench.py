@@ -622,16 +622,18 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
   from spartan_amd import backend
   be = backend.get()
   be.kmeans_timing(True)  # HIP events around the one-pass kernel of each step (no host sync inside)
-  sync()
-  comm.barrier()
-  t0 = time.perf_counter()
-  info = {}
-  c, labels = workloads.kmeans_fit(X, K, iters, info=info)
-  sync()
-  comm.barrier()
-  el = comm.max_over_ranks(time.perf_counter() - t0) / iters
-  kt = be.kmeans_times()
-  be.kmeans_timing(False)
+  try:
+    sync()
+    comm.barrier()
+    t0 = time.perf_counter()
+    info = {}
+    c, labels = workloads.kmeans_fit(X, K, iters, info=info)
+    sync()
+    comm.barrier()
+    el = comm.max_over_ranks(time.perf_counter() - t0) / iters
+    kt = be.kmeans_times()
+  finally:
+    be.kmeans_timing(False)
   checked = check_kmeans(X, labels, info['assign_centers'], comm)
   checked_sums = check_kmeans_sums(X, labels, info['sums'], info['counts'], comm)
   n = npts * ctx.world_size

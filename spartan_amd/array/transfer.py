@@ -134,7 +134,11 @@ def upload(arr, device, dtype=None):
   return out
 
 
-TINY = 4096        # host arrays up to this size go through a pinned ring (an iterative driver's w)
+# host arrays up to this size go through a pinned ring: an iterative
+# driver's w (256 B at cfg5) or k-means centres (256 KiB at cfg3), uploaded
+# every iteration -- an async copy instead of a pageable one that blocks the
+# host (round 6: 4 KiB -> 1 MiB for the centres)
+TINY = 1 << 20
 _TINY_RING = 8
 _tiny = {}
 

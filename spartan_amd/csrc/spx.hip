@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <type_traits>
 #include <utility>
@@ -2342,15 +2343,19 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
   float kq[3];
   kc_coef(eS, cmax, mun, mcoef, D, kq, xk1, xk0);
   const bool cok = cmax * cmax < 1e36 && mun * cmax < 1e36 && cmax < 3.0e4 && dcmax == dcmax;
-  // rows with |x'| >= pn_lim are left undecided and not added (label code
-  // -1): the list passes label them exactly and the gathered accumulation
-  // adds them in fp64.  Besides the fp32 range limit, pn_lim keeps far
-  // outliers (|x'| > 4 (cmax + |mu|)) out of the fp32 window sums: a
-  // provisionally added row that moved afterwards would leave the fp32
-  // rounding of its own add in p's chain (the test with far
-  // undecided outliers).  A far row that the screen could decide takes the
-  // list passes instead -- exact either way, and such rows are rare.
-  const float pn_lim = (float)fmin(cmax > 0.0 ? 1e36 / cmax : 1e36, 4.0 * (cmax + mun) + 1e-30);
+  // rows with |x'| >= pn_lim (the fp32 range limit) are left undecided and
+  // not added (label code -1): the list passes label them exactly and the
+  // gathered accumulation adds them in fp64.  A FAR row (|x'| >= pn_far =
+  // 4 (cmax + |mu|)) that the screen cannot decide is not added
+  // provisionally either: if its label moved afterwards, the fp32 rounding
+  // of its own add would stay in p's window chain (the test with
+  // far undecided outliers).  A far row the screen DOES decide is added as
+  // any other -- its label is final, so nothing moves (round 6, ADVICE r05:
+  // the far cut on every row left most rows of zero-mean data, where |x'|
+  // is the data's scale and cmax + |mu| may be far smaller, to the list
+  // passes).  Wave 1 hands the far flag to the decision as the sign of e.
+  const float pn_lim = (float)(cmax > 0.0 ? 1e36 / cmax : 1e36);
+  const float pn_far = (float)(4.0 * (cmax + mun) + 1e-30);
 
   const int G = gridDim.x, bk = blockIdx.x;
   // block bk takes units bk, bk + G, ...: in every slot the grid reads one
@@ -2472,7 +2477,7 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
       const float pn = __builtin_amdgcn_sqrtf(__builtin_fmaf(p2f, 1.001f, 1e-37f)) * 1.0001f;
       const float e = __builtin_fmaf(__builtin_fmaf(kq[2], pn, kq[1]), pn, kq[0]) * 1.0001f;
       const bool ok = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim;
-      if (h == 0) ebuf[(ue & 3) * U + j] = ok ? e : __builtin_nanf("");
+      if (h == 0) ebuf[(ue & 3) * U + j] = ok ? (pn < pn_far ? e : -e) : __builtin_nanf("");
     }
     // (3) decide: top-2 over the 4 waves' candidates, the certified rule.
     // d: the centre the row is added to -- its label when decided, and,
@@ -2491,10 +2496,11 @@ __global__ __launch_bounds__(KP_WAVES * 64, 1) void k_kmeans_pp(
       sw32(__builtin_bit_cast(float, ib), fl, fh);
       const float B1 = ks_max(b1l, b1h), B2 = ks_med3(b1l, b1h, ks_max(b2l, b2h));
       const int IB = b1l >= b1h ? __builtin_bit_cast(int, fl) : __builtin_bit_cast(int, fh);
-      const float e = er_e;  // NaN: not finite, out of range, or cok false (2b)
+      const float e = __builtin_fabsf(er_e);  // NaN: not finite, out of range, or cok false (2b)
+      const bool far = er_e < 0.f;            // |x'| >= pn_far: added only when decided
       const bool fin = isfinite(e) && isfinite(B1) && isfinite(B2);
       const bool dec = fin && B1 - B2 > 1.0001f * e;
-      const bool add = rlive && fin && IB < (int)K;
+      const bool add = rlive && fin && IB < (int)K && (dec || !far);
       d = add ? IB : -1;
       dl = !add ? -1 : dec ? IB : -2 - IB;
     }
@@ -3566,24 +3572,54 @@ static i64 kfs_part_bytes(i64 N, i64 D, i64 K) { return kfs_grid(N) * kp_nwin(N)
 // up to KT_CAP calls and read back (after the timed region) by
 // spx_kmeans_times -- bench.py's per-kernel roofline of the k-means leg.
 constexpr int KT_CAP = 256;
+// the state is process-global: one mutex serialises enable / read-back /
+// record, the events belong to the device that was current at enable time
+// (a step on another device records nothing and is counted in g_kt_skipped,
+// reported by spx_kmeans_times as an error), and a failed event creation
+// destroys the events already made
+static std::mutex g_kt_mu;
 static bool g_kt_on = false;
-static int g_kt_n = 0;
+static int g_kt_n = 0, g_kt_dev = -1, g_kt_skipped = 0;
 static hipEvent_t g_kt_ev[KT_CAP][4];
+static void kt_destroy(int upto) {
+  for (int i = 0; i < upto; ++i)
+    for (int k = 0; k < 4; ++k) (void)hipEventDestroy(g_kt_ev[i][k]);
+}
 extern "C" int spx_kmeans_timing(int enable) {
+  std::lock_guard<std::mutex> lk(g_kt_mu);
   if (enable && !g_kt_on) {
+    int dev = -1;
+    HIP_TRY(hipGetDevice(&dev));
     for (int i = 0; i < KT_CAP; ++i)
-      for (int k = 0; k < 4; ++k) HIP_TRY(hipEventCreate(&g_kt_ev[i][k]));
+      for (int k = 0; k < 4; ++k) {
+        const hipError_t e = hipEventCreate(&g_kt_ev[i][k]);
+        if (e != hipSuccess) {
+          for (int kk = 0; kk < k; ++kk) (void)hipEventDestroy(g_kt_ev[i][kk]);
+          kt_destroy(i);
+          return set_err(SPX_EHIP, "spx_kmeans_timing: hipEventCreate: %s", hipGetErrorString(e));
+        }
+      }
     g_kt_on = true;
+    g_kt_dev = dev;
   } else if (!enable && g_kt_on) {
-    for (int i = 0; i < KT_CAP; ++i)
-      for (int k = 0; k < 4; ++k) (void)hipEventDestroy(g_kt_ev[i][k]);
+    kt_destroy(KT_CAP);
     g_kt_on = false;
+    g_kt_dev = -1;
   }
   g_kt_n = 0;
+  g_kt_skipped = 0;
   return SPX_OK;
 }
 extern "C" int spx_kmeans_times(double* fused_ms, double* step_ms, int max) {
+  std::lock_guard<std::mutex> lk(g_kt_mu);
   if (!g_kt_on) return set_err(SPX_EINVAL, "spx_kmeans_times: timing is off (spx_kmeans_timing(1))");
+  if (g_kt_skipped) {
+    const int sk = g_kt_skipped;
+    g_kt_n = 0;
+    g_kt_skipped = 0;
+    return set_err(SPX_EINVAL, "spx_kmeans_times: %d step(s) ran on another device than the one timing was "
+                   "enabled on (%d) and were not timed", sk, g_kt_dev);
+  }
   const int n = g_kt_n < max ? g_kt_n : max;
   for (int i = 0; i < n; ++i) {
     float a = 0.f, b = 0.f;
@@ -3596,8 +3632,17 @@ extern "C" int spx_kmeans_times(double* fused_ms, double* step_ms, int max) {
   g_kt_n = 0;
   return n;
 }
+// k = 0 opens a step's record (on the enabling device only), 3 closes it
 static void kt_record(int k, void* stream) {
-  if (g_kt_on && g_kt_n < KT_CAP) (void)hipEventRecord(g_kt_ev[g_kt_n][k], S(stream));
+  std::lock_guard<std::mutex> lk(g_kt_mu);
+  if (!g_kt_on || g_kt_n >= KT_CAP) return;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev != g_kt_dev) {
+    if (k == 0) ++g_kt_skipped;
+    return;
+  }
+  (void)hipEventRecord(g_kt_ev[g_kt_n][k], S(stream));
+  if (k == 3) ++g_kt_n;
 }
 
 extern "C" int64_t spx_kmeans_step_workspace(int dtype, int64_t N, int64_t D, int64_t K) {
@@ -3729,7 +3774,6 @@ extern "C" int spx_kmeans_step(int dtype, int64_t N, int64_t D, int64_t K, const
       K, G2, pcnt2, (unsigned long long*)counts, 2);
   LAUNCH_CHECK("spx_kmeans_step(reduce subtractions)");
   kt_record(3, stream);
-  if (g_kt_on && g_kt_n < KT_CAP) ++g_kt_n;
   return SPX_OK;
 }
 

@@ -83,9 +83,19 @@ def _row_blocks(X, ncols):
 
 
 def _deliver_full(target, full):
-  """Copy a full-size tensor, identical on every rank, into target's local tiles."""
+  """Copy a full-size tensor, identical on every rank, into target's local
+  tiles; a local tile that IS the whole array and was never written adopts
+  the tensor instead (no copy: the join made it for this target alone)."""
   from ..expr.engine import _copy_out
   be = backend.get()
+  if len(target.local) == 1:
+    (d, t), = target.local.items()
+    if (not t.written and tuple(d.ul) == (0,) * len(target.shape) and tuple(d.shape) == tuple(target.shape)
+        and tuple(full.shape) == tuple(d.shape) and full.dtype == backend.torch_dtype(target.dtype)
+        and full.is_contiguous()):
+      t.data = full
+      t.written = [d]
+      return
   for d, t in target.local.items():
     _copy_out(be, t, full, d)
 
@@ -197,9 +207,10 @@ def _assign_fused(arrays, fn_kw, target, dist_dtype):
   blocks, got = _row_blocks(X, D)
   fused = _step_domain(X, K)
   _STEP.clear()
-  if fused:
-    sums = torch.zeros((K, D), dtype=torch.float64, device=ctx.device)
-    counts = torch.zeros((K,), dtype=torch.int64, device=ctx.device)
+  if fused:  # the first local block's step writes them (zero_first), the others add
+    sums = torch.empty((K, D), dtype=torch.float64, device=ctx.device)
+    counts = torch.empty((K,), dtype=torch.int64, device=ctx.device)
+    first = True
   updates = []
   for qi, (src, region) in enumerate(blocks):
     tex = ext.create((region.ul[0],), (region.lr[0],), target.shape)
@@ -210,12 +221,16 @@ def _assign_fused(arrays, fn_kw, target, dist_dtype):
         pts = be.contiguous(pts)
       lab = torch.empty((tex.shape[0],), dtype=torch.int64, device=ctx.device)
       if fused:
-        be.kmeans_step(pts, c, lab, sums, counts, zero_first=False, dist_dtype=dist_dtype)
+        be.kmeans_step(pts, c, lab, sums, counts, zero_first=first, dist_dtype=dist_dtype)
+        first = False
       else:
         be.kmeans_assign(pts, c, lab, dist_dtype=dist_dtype)
     updates.append((qi, tex, src, lab))
   _scatter_updates(target, updates)
   if fused:
+    if first:  # no local row block on this rank
+      sums.zero_()
+      counts.zero_()
     _STEP.update(labels=target, X=X, K=K, sums=sums, counts=counts)
 
 

@@ -240,17 +240,25 @@ def _owner_slabs(output, ctx, M):
   return _rank_slabs(output, ctx) and M % ctx.world_size == 0
 
 
+# slab gathers in flight ahead of the GEMM that consumes them (_dot_overlapped)
+GATHER_AHEAD = 2
+
+
 def _dot_overlapped(output, a, A, plan, b, B, K, M, N, dtype, C, col_blocks):
   """K-split partials reduced slab by slab while the next slab computes, the
   A column strip gathered slab by slab ahead of its GEMM.
 
   The output is one row slab per rank.  For every slab j (in the same order
   on every rank) the rank needs rows j of its A column strip A[:, K_g]: the
-  piece that the owner of A's rows j holds.  All N slab gathers are posted
-  at once on the side stream (comm.exchange_async; a piece of whole rows is
-  received straight into its buffer), so slab j + 1's rows travel while slab
-  j's GEMM runs and the first GEMM waits only for its own piece -- the local
-  piece needs no transfer at all when A is row-strip tiled.  After the
+  piece that the owner of A's rows j holds.  The slab gathers run
+  GATHER_AHEAD slabs ahead of the GEMMs on the side stream
+  (comm.exchange_async; a piece of whole rows is received straight into its
+  buffer): slabs 0 .. GATHER_AHEAD - 1 are posted first, and the gather of
+  slab j + GATHER_AHEAD right after the reduce of slab j, so slab j + 1's
+  rows travel while slab j's GEMM runs and -- on one communication stream,
+  where collectives run in posting order -- the reduce of slab j is not
+  queued behind the gathers of every later slab (round-6 advisor).  The
+  local piece needs no transfer at all when A is row-strip tiled.  After the
   partial of slab j is computed (MFMA GEMM into C[slab j]) an RCCL reduce of
   it to its owner j starts on the side stream, under the GEMM of slab j + 1.
   The bytes moved equal the gather + reduce-scatter's, but the xGMI time
@@ -266,7 +274,9 @@ def _dot_overlapped(output, a, A, plan, b, B, K, M, N, dtype, C, col_blocks):
   # slab j's request list: the rows of slab j of every K block's A strip
   reqs = [[(A.to_base(ext.create((j * slab, bex.ul[0]), ((j + 1) * slab, bex.lr[0]), (M, K))), dst)
            for bex, dst in plan] for j in range(W)]
-  pending = [distarray.gather_regions_async(a, reqs[j]) for j in range(W)]
+  pending = [None] * W
+  for j in range(min(GATHER_AHEAD, W)):
+    pending[j] = distarray.gather_regions_async(a, reqs[j])
   local_b = []
   for qi, (bex, dst) in enumerate(plan):
     if dst != ctx.rank:
@@ -293,6 +303,8 @@ def _dot_overlapped(output, a, A, plan, b, B, K, M, N, dtype, C, col_blocks):
       if (c0, c1) not in started:
         C[r0:r1, c0:c1].zero_()
     handles.append(comm.reduce_async(C[r0:r1], j, 'sum'))
+    if j + GATHER_AHEAD < W:
+      pending[j + GATHER_AHEAD] = distarray.gather_regions_async(a, reqs[j + GATHER_AHEAD])
   comm.wait_all(handles)
   (d, t), = output.local.items()
   t.data = C[ctx.rank * slab:(ctx.rank + 1) * slab].clone()  # free the full-size partial buffer

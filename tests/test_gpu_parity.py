@@ -1624,6 +1624,47 @@ def test_kmeans_step_far_undecided_outliers(ex):
   assert err.max() <= 1e-5, 'max |sum - fp64| / sum |x| = %.3g at %s' % (err.max(), np.unravel_index(err.argmax(), err.shape))
 
 
+@pytest.mark.parametrize('K', [1, 8, 256])
+def test_kmeans_step_zero_mean_gaussian(ex, K):
+  """zero-mean isotropic Gaussian rows (D = 128, |x'| ~ 11 while
+  the centres' spread cmax and |mu| are far smaller for K = 1 / mean-like
+  centres): the far-row cut 4 (cmax + |mu|) applies only to rows the screen
+  cannot decide, so a decided far row is still added in the one pass --
+  the screen's undecided fraction stays small; labels exact, counts exact,
+  sums within 1e-5 of the fp64 sum |x|."""
+  import torch
+  from spartan_amd import backend
+  be = backend.get()
+  g = np.random.default_rng(606 + K)
+  N, D = 200_000, 128
+  pts = g.standard_normal((N, D)).astype(np.float32)
+  if K == 1:
+    C = np.zeros((1, D))
+  else:  # centres near the mean (second-iteration-like): means of random halves of the data
+    C = np.stack([pts[g.choice(N, N // 4, replace=False)].astype(np.float64).mean(0) * 8 for _ in range(K)])
+  P = torch.as_tensor(pts).cuda()
+  Cd = torch.as_tensor(C).cuda()
+  lab = torch.empty((N,), dtype=torch.int64, device='cuda')
+  sums = torch.empty((K, D), dtype=torch.float64, device='cuda')
+  cnt = torch.empty((K,), dtype=torch.int64, device='cuda')
+  be.kmeans_step(P, Cd, lab, sums, cnt)
+  und = be.kmeans_counters(D)[3]
+  print('zero-mean Gaussian K=%d: %d of %d rows undecided by the screen' % (K, und, N))
+  assert und <= (0.01 if K == 1 else 0.3) * N
+  exact = torch.empty_like(lab)
+  be.kmeans_assign(P, Cd, exact, exact_only=True)
+  assert torch.equal(lab, exact)
+  L = lab.cpu().numpy()
+  np.testing.assert_array_equal(cnt.cpu().numpy(), np.bincount(L, minlength=K))
+  p64 = pts.astype(np.float64)
+  ws = np.zeros((K, D))
+  wa = np.zeros((K, D))
+  np.add.at(ws, L, p64)
+  np.add.at(wa, L, np.abs(p64))
+  err = np.abs(sums.cpu().numpy() - ws) / wa
+  assert err.max() <= 1e-5, err.max()
+
+
 def test_kmeans_step_timing_hook(ex):
   """spx_kmeans_timing / spx_kmeans_times (bench.py's k-means kernel
   roofline): one (kernel, step) pair per fused step in call order, the kernel

@@ -1,8 +1,8 @@
 // Dev tool: time GEMM configurations of spartan_amd/csrc/gemm_kernels.h (the
 // product kernels) in one process, interleaved rounds (cdna_hip_programming.md
 // 5.4 rule 24), each checked against the first configuration of its dtype.
-//   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -o tools/bin/gemm_tune tools/gemm_tune.hip
-//   ./tools/bin/gemm_tune <size> <rounds> <f32|f64|both>
+//   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -o tools/devbin/gemm_tune tools/gemm_tune.hip
+//   ./tools/devbin/gemm_tune <size> <rounds> <f32|f64|both>
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -99,6 +99,27 @@ int main(int argc, char** argv) {
   i64 S = argc > 1 ? atoll(argv[1]) : 8192;
   int rounds = argc > 2 ? atoi(argv[2]) : 2;
   std::string which = argc > 3 ? argv[3] : "both";
+  if (which == "big") {  // round 6: one wave per SIMD with 128 x 128 (or 128 x 64) wave tiles, against the product
+    run<float>(S, rounds,
+               {VG(float, 256, 128, 16, 4, 2, 8, 512), VG(float, 256, 256, 16, 2, 2, 8, 512),
+                VG(float, 256, 256, 32, 2, 2, 8, 256), VG(float, 256, 128, 16, 2, 1, 8, 512),
+                VG(float, 128, 256, 16, 1, 2, 8, 512), VG(float, 256, 256, 16, 2, 4, 8, 512),
+                VG(float, 256, 128, 32, 2, 2, 8, 256)},
+               157.3);
+    run<double>(S, rounds,
+                {V(double, 128, 128, 16, 4, 4, 0), V(double, 128, 128, 16, 2, 2, 0), V(double, 128, 128, 16, 2, 2, 8),
+                 V(double, 256, 128, 16, 2, 2, 8), V(double, 128, 128, 32, 2, 2, 8), V(double, 256, 256, 16, 2, 2, 8),
+                 V(double, 128, 256, 16, 2, 2, 8)},
+                78.6);
+    return 0;
+  }
+  if (which == "big2") {  // 128 x 128 wave tiles without the in-kernel flush (a K-chunked launch instead)
+    run<float>(S, rounds,
+               {VG(float, 256, 128, 16, 4, 2, 8, 512), V(float, 256, 256, 16, 2, 2, 8), V(float, 256, 256, 32, 2, 2, 8),
+                V(float, 256, 256, 16, 2, 2, 4), V(float, 256, 256, 16, 2, 2, 16), V(float, 256, 256, 16, 2, 2, 0)},
+               157.3);
+    return 0;
+  }
   if (which == "gfl") {  // one accumulator set, flushed into C every GFL K-tiles, against SEG and one chain
     run<float>(S, rounds,
                {V(float, 256, 128, 16, 4, 2, 8), VS(float, 256, 128, 16, 4, 2, 8, 16), VG(float, 256, 128, 16, 4, 2, 8, 128),
