@@ -300,6 +300,427 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
   flush_c(flushed);
 }
 
+// fp32, one wave per SIMD: a 256 x 256 block tile, 4 waves (2 x 2), each
+// wave 128 x 128 = 4 x 4 v_mfma_f32_32x32x2_f32 tiles (256 accumulator
+// registers), K-tiles of 16.  Three LDS stages: tile t + 2 is written in the
+// middle of tile t's MFMAs (its global loads were issued in the middle of
+// tile t - 1), and tile t + 1's A fragments and first B fragments are read
+// into registers before the one barrier that ends tile t -- so after the
+// barrier the wave's next MFMA has its operands and nothing waits on LDS or
+// HBM at the tile boundary (the two-stage kernel above loses the LDS
+// write, the barrier and the fragment reads' latency there, ~15 % at one
+// wave per SIMD).  Hazards (buffer b = t mod 3):
+//   * tile t + 2 goes into buffer (t + 2) % 3 = (t - 1) % 3, last read in
+//     tile t - 1 (B reads) and tile t - 2 (its A fragment prefetch): both
+//     before the barrier that ended tile t - 1;
+//   * tile t + 1 (buffer (t + 1) % 3) was written in tile t - 1 by every
+//     wave: visible after the barrier that ended tile t - 1.
+// Requires M % 256 == N % 256 == K % 16 == 0, lda % 4 == ldb % 4 == 0 and
+// 16-byte aligned A, B (p3_ok).  The accumulator chain spans K: callers cap
+// K per launch (spx_gemm runs K in chunks with beta = 1 after the first).
+constexpr int P3_AST = 20;                            // A row stride (floats): k-contiguous, +4 pad
+constexpr int P3_SA = 256 * P3_AST, P3_SB = 16 * 256;  // floats per stage
+constexpr int P3_LDS = 3 * (P3_SA + P3_SB) * 4;       // bytes
+template <int GM, int ABL = 0, int FL = 0>
+__global__ __launch_bounds__(256, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, const float* __restrict__ A, i64 lda,
+                                                    const float* __restrict__ B, i64 ldb, float* __restrict__ C,
+                                                    i64 ldc, float alpha, float beta, int tiles_n, int ntiles) {
+  typedef float V __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) float p3_lds[];
+  int tm, tn;
+  tile_of(blockIdx.x, ntiles, tiles_n, GM, tm, tn);
+  const i64 row0 = (i64)tm * 256, col0 = (i64)tn * 256;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int li = lane & 31, kb = 8 * (lane >> 5);
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x16){};
+  // staging: A rows (t >> 2) + 64 i, k quad t & 3; B rows (t >> 6) + 4 i, column quad t & 63
+  V ra[4], rb[4];
+  const float* ag = A + (row0 + (t >> 2)) * lda + 4 * (t & 3);
+  const float* bg = B + (i64)(t >> 6) * ldb + col0 + 4 * (t & 63);
+  auto load = [&](i64 k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ra[i] = *(const V*)(ag + (i64)64 * i * lda + k0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rb[i] = *(const V*)(bg + (k0 + 4 * i) * ldb);
+  };
+  auto abuf = [&](int s) __attribute__((always_inline)) { return p3_lds + s * (P3_SA + P3_SB); };
+  auto store = [&](int s) __attribute__((always_inline)) {
+    float* a = abuf(s) + (t >> 2) * P3_AST + 4 * (t & 3);
+    float* b = abuf(s) + P3_SA + (t >> 6) * 256 + 4 * (t & 63);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *(V*)(a + 64 * i * P3_AST) = ra[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *(V*)(b + 4 * i * 256) = rb[i];
+  };
+  // a lane's A values of a whole K-tile (k = kb .. kb + 7 of rows wm 128 + 32 i + li)
+  auto read_a = [&](int s, float (&av)[4][8]) __attribute__((always_inline)) {
+    const float* a = abuf(s) + (wm * 128 + li) * P3_AST + kb;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const V v0 = *(const V*)(a + 32 * i * P3_AST), v1 = *(const V*)(a + 32 * i * P3_AST + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        av[i][e] = v0[e];
+        av[i][4 + e] = v1[e];
+      }
+    }
+  };
+  auto read_b = [&](int s, int kk, float (&b)[4]) __attribute__((always_inline)) {
+    const float* p = abuf(s) + P3_SA + (kb + kk) * 256 + wn * 128 + li;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = p[32 * j];
+  };
+  // K runs in chunks of FL K-tiles (FL > 0; one chunk otherwise), each with
+  // its own pipeline fill; between chunks the accumulators go into C (see
+  // flush below) -- there no pipeline state is live, so the flush needs no
+  // registers the K loop holds
+  const int nkt = (int)(K / 16);
+  int kb0 = 0, nk = nkt;
+  float avA[4][8], avB[4][8], bn[4];
+  // one K-tile: MFMAs from av (this tile's A fragments), B read a step
+  // ahead; woven between each step's four MFMA groups: one piece of tile
+  // kt + 2's LDS stage (its global loads were issued a tile earlier, piece
+  // by piece), the global load of the same piece of tile kt + 3 into the
+  // staging register it just freed, and one ds_read_b128 of tile kt + 1's A
+  // fragments -- one memory instruction between MFMA groups instead of
+  // bursts of eight (a burst held the wave's in-order issue, and with one
+  // wave per SIMD the matrix pipe, for ~9 % of the kernel: tools/gemm_tune
+  // p3abl).  Sched barriers pin the weave.
+  auto store_piece = [&](int sb, int q) __attribute__((always_inline)) {
+    if (q < 4)
+      *(V*)(abuf(sb) + (t >> 2) * P3_AST + 4 * (t & 3) + 64 * q * P3_AST) = ra[q];
+    else
+      *(V*)(abuf(sb) + P3_SA + (t >> 6) * 256 + 4 * (t & 63) + 4 * (q - 4) * 256) = rb[q - 4];
+  };
+  auto load_piece = [&](i64 k0, int q) __attribute__((always_inline)) {
+    if (q < 4)
+      ra[q] = *(const V*)(ag + (i64)64 * q * lda + k0);
+    else
+      rb[q - 4] = *(const V*)(bg + (k0 + 4 * (q - 4)) * ldb);
+  };
+  auto read_a_piece = [&](int sb, float (&av)[4][8], int q) __attribute__((always_inline)) {
+    const int i = q >> 1, hf = q & 1;
+    const V v = *(const V*)(abuf(sb) + (wm * 128 + li) * P3_AST + kb + 32 * i * P3_AST + 4 * hf);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) av[i][4 * hf + e] = v[e];
+  };
+  auto tile = [&](int kt, int s, float (&av)[4][8], float (&avn)[4][8]) __attribute__((always_inline)) {
+    const int s1 = s == 2 ? 0 : s + 1, s2 = s1 == 2 ? 0 : s1 + 1;
+    // unconditional (no branch around a memory instruction: hipcc then waits
+    // vmcnt(0) at every store): past the last tile the stage writes a
+    // buffer nobody reads again, the loads re-read the last tile
+    constexpr bool st = ABL < 1, ld = ABL < 1, ra_ = ABL < 3;
+    const i64 k3 = (i64)(kb0 + (kt + 3 < nk ? kt + 3 : nk - 1)) * 16;
+    float b[2][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[0][j] = bn[j];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      if (kk + 1 < 8) read_b(s, kk + 1, b[(kk + 1) & 1]);
+      if (kk == 7) read_b(s1, 0, bn);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][kk], b[kk & 1][j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (i == 0 && st) store_piece(s2, kk);
+        if (i == 1 && ld) load_piece(k3, kk);
+        if (i == 2 && ra_) read_a_piece(s1, avn, kk);
+      }
+    }
+    if (ABL < 2) __syncthreads();
+  };
+  // FL > 0: every FL K-tiles the accumulators go into C and restart from
+  // zero (chains of 8 FL MFMA steps; the generic kernel's GFL): the first
+  // flush stores (beta 0) or adds, later ones add by no-return fp32 atomics
+  // (one wave owns each element, so its adds land in program order:
+  // deterministic).  The caller passes beta 0 or 1 when FL > 0.
+  const bool use_beta = beta != 0.f;
+  bool flushed = false;
+  auto flush = [&](bool again) __attribute__((always_inline)) {
+    int fl = lane;
+    i64 ldf = ldc;
+    // the addresses are invariant across chunks: opaque operands keep the
+    // compiler from hoisting all 256 of them (512 registers) out of the loop
+    asm volatile("" : "+v"(fl));
+    asm volatile("" : "+s"(ldf));
+    float* const cb = C + (row0 + wm * 128 + Mfma<float>::crow(fl, 0)) * ldf + col0 + wn * 128 + (fl & 31);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float* const pc = cb + (i64)(i * 32 + Mfma<float>::crow(0, r)) * ldf + j * 32;
+          const float v = alpha * acc[i][j][r];
+          if (again || use_beta)
+            unsafeAtomicAdd(pc, v);
+          else
+            *pc = v;
+        }
+        acc[i][j] = (f32x16){};
+        __builtin_amdgcn_sched_barrier(0);  // one accumulator tile's 16 values in VGPRs at a time
+      }
+  };
+  constexpr int CH = FL > 0 ? FL : (1 << 30);
+  for (kb0 = 0; kb0 < nkt; kb0 += CH) {
+    nk = nkt - kb0 < CH ? nkt - kb0 : CH;
+    load((i64)kb0 * 16);
+    store(0);
+    if (nk > 1) {
+      load((i64)(kb0 + 1) * 16);
+      store(1);
+    }
+    __syncthreads();
+    read_a(0, avA);
+    read_b(0, 0, bn);
+    load((i64)(kb0 + (nk > 2 ? 2 : nk - 1)) * 16);
+    int s = 0;
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+      tile(kt, s, avA, avB);
+      s = s == 2 ? 0 : s + 1;
+      tile(kt + 1, s, avB, avA);
+      s = s == 2 ? 0 : s + 1;
+    }
+    if (kt < nk) tile(kt, s, avA, avB);
+    if constexpr (FL > 0) {
+      if (kb0 + CH < nkt) {  // block-uniform
+        flush(flushed);
+        flushed = true;
+      }
+    }
+  }
+  if (FL > 0 && flushed) {
+    flush(true);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const i64 gr = row0 + wm * 128 + i * 32 + Mfma<float>::crow(lane, r);
+        const i64 gc = col0 + wn * 128 + j * 32 + li;
+        float v = alpha * acc[i][j][r];
+        if (use_beta) v += beta * C[gr * ldc + gc];
+        C[gr * ldc + gc] = v;
+      }
+}
+
+// fp64, the same three-stage one-wave-per-SIMD structure: a 128 x 128 block
+// tile, 4 waves (2 x 2), each 64 x 64 = 4 x 4 v_mfma_f64_16x16x4_f64 tiles,
+// K-tiles of BK.  The K-tile is split between the four lane groups g = l >> 4
+// (step kk takes k = g BK / 4 + kk from group g, for A and B alike), so a
+// lane's A values for the whole K-tile are BK / 4 consecutive doubles of its
+// row (ds_read_b128) and a B value is one ds_read_b64.  Strides: A rows
+// BK + 2 (BK = 16) or BK + 2 doubles (the b128 reads of 16 rows spread
+// over the banks), B rows 128 + 4 doubles (the four lane groups' rows two
+// by two on different bank halves).
+template <int BK>
+struct P3d {
+  static constexpr int AST = BK + 2, BST = 132, SA = 128 * AST, SB = BK * BST, LDS = 3 * (SA + SB) * 8, KQ = BK / 4;
+};
+template <int GM, int BK>
+__global__ __launch_bounds__(256, 1) void gemm_f64_p3(i64 M, i64 N, i64 K, const double* __restrict__ A, i64 lda,
+                                                    const double* __restrict__ B, i64 ldb, double* __restrict__ C,
+                                                    i64 ldc, double alpha, double beta, int tiles_n, int ntiles) {
+  typedef P3d<BK> P;
+  typedef double V __attribute__((ext_vector_type(2)));
+  extern __shared__ __attribute__((aligned(16))) double p3d_lds[];
+  int tm, tn;
+  tile_of(blockIdx.x, ntiles, tiles_n, GM, tm, tn);
+  const i64 row0 = (i64)tm * 128, col0 = (i64)tn * 128;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int li = lane & 15, g = lane >> 4, kb = P::KQ * g;
+  f64x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f64x4){0, 0, 0, 0};
+  // staging, 16-byte pieces: A 128 rows x BK / 2 pieces, B BK rows x 64 pieces
+  constexpr int APR = BK / 2, NLA = 128 * APR / 256, NLB = BK * 64 / 256;
+  V ra[NLA], rb[NLB];
+  auto load = [&](i64 k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NLA; ++i) {
+      const int idx = t + 256 * i, r = idx / APR, q = idx % APR;
+      ra[i] = *(const V*)(A + (row0 + r) * lda + k0 + 2 * q);
+    }
+#pragma unroll
+    for (int i = 0; i < NLB; ++i) {
+      const int idx = t + 256 * i, r = idx >> 6, q = idx & 63;
+      rb[i] = *(const V*)(B + (k0 + r) * ldb + col0 + 2 * q);
+    }
+  };
+  auto abuf = [&](int s) __attribute__((always_inline)) { return p3d_lds + s * (P::SA + P::SB); };
+  auto store = [&](int s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NLA; ++i) {
+      const int idx = t + 256 * i, r = idx / APR, q = idx % APR;
+      *(V*)(abuf(s) + r * P::AST + 2 * q) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NLB; ++i) {
+      const int idx = t + 256 * i, r = idx >> 6, q = idx & 63;
+      *(V*)(abuf(s) + P::SA + r * P::BST + 2 * q) = rb[i];
+    }
+  };
+  auto read_a = [&](int s, double (&av)[4][P::KQ]) __attribute__((always_inline)) {
+    const double* a = abuf(s) + (wm * 64 + li) * P::AST + kb;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < P::KQ; q += 2) {
+        const V v = *(const V*)(a + 16 * i * P::AST + q);
+        av[i][q] = v[0];
+        av[i][q + 1] = v[1];
+      }
+  };
+  auto read_b = [&](int s, int kk, double (&b)[4]) __attribute__((always_inline)) {
+    const double* p = abuf(s) + P::SA + (kb + kk) * P::BST + wn * 64 + li;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = p[16 * j];
+  };
+  const int nk = (int)(K / BK);
+  double avA[4][P::KQ], avB[4][P::KQ], bn[4];
+  load(0);
+  store(0);
+  if (nk > 1) {
+    load(BK);
+    store(1);
+  }
+  __syncthreads();
+  read_a(0, avA);
+  read_b(0, 0, bn);
+  load((i64)(nk > 2 ? 2 : nk - 1) * BK);
+  constexpr int KQ = P::KQ;
+  static_assert(BK == 16 && NLA == 4 && NLB == 4, "the weave below places 8 staging pieces over 4 k-steps");
+  // the fp32 kernel's weave (see there): per k-step, between its four MFMA
+  // groups, two pieces of tile kt + 2's stage, the loads of the same pieces
+  // of tile kt + 3 and two of tile kt + 1's A fragment reads
+  auto store_piece = [&](int sb, int q) __attribute__((always_inline)) {
+    const int idx = t + 256 * (q & 3);
+    if (q < 4)
+      *(V*)(abuf(sb) + (idx / APR) * P::AST + 2 * (idx % APR)) = ra[q];
+    else
+      *(V*)(abuf(sb) + P::SA + (idx >> 6) * P::BST + 2 * (idx & 63)) = rb[q - 4];
+  };
+  auto load_piece = [&](i64 k0, int q) __attribute__((always_inline)) {
+    const int idx = t + 256 * (q & 3);
+    if (q < 4)
+      ra[q] = *(const V*)(A + (row0 + idx / APR) * lda + k0 + 2 * (idx % APR));
+    else
+      rb[q - 4] = *(const V*)(B + (k0 + (idx >> 6)) * ldb + col0 + 2 * (idx & 63));
+  };
+  auto read_a_piece = [&](int sb, double (&av)[4][KQ], int q) __attribute__((always_inline)) {
+    const int i = q >> 1, hf = q & 1;
+    const V v = *(const V*)(abuf(sb) + (wm * 64 + li) * P::AST + kb + 16 * i * P::AST + 2 * hf);
+    av[i][2 * hf] = v[0];
+    av[i][2 * hf + 1] = v[1];
+  };
+  auto tile = [&](int kt, int s, double (&av)[4][KQ], double (&avn)[4][KQ]) __attribute__((always_inline)) {
+    const int s1 = s == 2 ? 0 : s + 1, s2 = s1 == 2 ? 0 : s1 + 1;
+    const i64 k3 = (i64)(kt + 3 < nk ? kt + 3 : nk - 1) * BK;
+    double b[2][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[0][j] = bn[j];
+#pragma unroll
+    for (int kk = 0; kk < KQ; ++kk) {
+      if (kk + 1 < KQ) read_b(s, kk + 1, b[(kk + 1) & 1]);
+      if (kk == KQ - 1) read_b(s1, 0, bn);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i][kk], b[kk & 1][j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        const int q = 2 * kk + (i >> 1);
+        if ((i & 1) == 0) store_piece(s2, q);
+        if ((i & 1) == 1) {
+          load_piece(k3, q);
+          read_a_piece(s1, avn, q);
+        }
+      }
+    }
+    __syncthreads();
+  };
+  int s = 0;
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    tile(kt, s, avA, avB);
+    s = s == 2 ? 0 : s + 1;
+    tile(kt + 1, s, avB, avA);
+    s = s == 2 ? 0 : s + 1;
+  }
+  if (kt < nk) tile(kt, s, avA, avB);
+  const bool use_beta = beta != 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const i64 gr = row0 + wm * 64 + i * 16 + Mfma<double>::crow(lane, r);
+        const i64 gc = col0 + wn * 64 + j * 16 + li;
+        double v = alpha * acc[i][j][r];
+        if (use_beta) v += beta * C[gr * ldc + gc];
+        C[gr * ldc + gc] = v;
+      }
+}
+
+template <int BK>
+__host__ inline bool p3d_ok(i64 M, i64 N, i64 K, const void* A, i64 lda, const void* B, i64 ldb) {
+  return M % 128 == 0 && N % 128 == 0 && K % BK == 0 && K > 0 && lda % 2 == 0 && ldb % 2 == 0 &&
+         (uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0;
+}
+
+template <int GM, int BK>
+__host__ inline hipError_t p3d_launch(i64 M, i64 N, i64 K, const double* A, i64 lda, const double* B, i64 ldb,
+                                      double* C, i64 ldc, double alpha, double beta, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_f64_p3<GM, BK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       P3d<BK>::LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const i64 tn = N / 128, nt = (M / 128) * tn;
+  gemm_f64_p3<GM, BK><<<(unsigned)nt, 256, P3d<BK>::LDS, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, (int)tn,
+                                                             (int)nt);
+  return hipGetLastError();
+}
+
+__host__ inline bool p3_ok(i64 M, i64 N, i64 K, const void* A, i64 lda, const void* B, i64 ldb) {
+  return M % 256 == 0 && N % 256 == 0 && K % 16 == 0 && K > 0 && lda % 4 == 0 && ldb % 4 == 0 &&
+         (uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0;
+}
+
+template <int GM, int ABL = 0, int FL = 0>
+__host__ inline hipError_t p3_launch(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i64 ldb,
+                                     float* C, i64 ldc, float alpha, float beta, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_f32_p3<GM, ABL, FL>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, P3_LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const i64 tn = N / 256, nt = (M / 256) * tn;
+  gemm_f32_p3<GM, ABL, FL><<<(unsigned)nt, 256, P3_LDS, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, (int)tn, (int)nt);
+  return hipGetLastError();
+}
+
 template <typename T, int BM, int BN, int BK, int WM, int WN, int GM, int SEG = 0, int GFL = 0>
 struct Config {
   static constexpr int bm = BM, bn = BN, bk = BK, threads = 64 * WM * WN;

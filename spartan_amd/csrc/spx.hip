@@ -640,6 +640,32 @@ __global__ __launch_bounds__(256) void k_scale_rows(i64 M, i64 N, float* C, i64 
 }
 typedef spx_mfma::Config<double, 128, 128, 16, 4, 4, 0> GemmF64;
 
+// Round 6: the three-stage one-wave-per-SIMD kernels (gemm_kernels.h
+// gemm_f32_p3 / gemm_f64_p3) for large aligned products.  fp32: chains of
+// SPX_GEMM_GFL K-tiles flushed into C inside the kernel, as the two-stage
+// kernel's GFL (the same chains: the cfg4 product is bit-identical to it);
+// fp64 (experimental, SPX_GEMM_P3=2): K in launches of SPX_GEMM_KCHUNK.
+// SPX_GEMM_P3=0 in the environment selects the two-stage kernels (A/B; read
+// once).
+constexpr i64 SPX_GEMM_KCHUNK = 8192;
+static int gemm_p3_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SPX_GEMM_P3");
+    v = e ? atoi(e) : 1;
+  }
+  return v;
+}
+template <typename T, typename F>
+static hipError_t gemm_kchunks(i64 K, const T* a, const T* b, i64 ldb, T beta, F launch) {
+  for (i64 k0 = 0; k0 < K; k0 += SPX_GEMM_KCHUNK) {
+    const i64 kc = K - k0 < SPX_GEMM_KCHUNK ? K - k0 : SPX_GEMM_KCHUNK;
+    const hipError_t e = launch(kc, a + k0, b + k0 * ldb, k0 ? (T)1 : beta);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 // integer GEMM (exact, wrap-around like NumPy's int matmul): 16x16 output
 // tile per 256-thread block, K staged through LDS.  Used for integer dot
 // products (the reference's tests multiply arange ints); not a hot path.
@@ -701,7 +727,12 @@ extern "C" int spx_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* 
       beta = 1.0;
     }
     i64 big_tiles = ((M + 255) / 256) * ((N + 255) / 256);
-    if (big_tiles >= 512) {
+    if (big_tiles >= 512 && big_tiles <= 0x7fffffffLL && gemm_p3_on() && spx_mfma::p3_ok(M, N, K, A, lda, B, ldb)) {
+      // one launch, K in chunks of SPX_GEMM_GFL K-tiles inside the kernel
+      // (beta is 0 or 1 here, as the flush needs)
+      e = spx_mfma::p3_launch<8, 0, SPX_GEMM_GFL>(M, N, K, a, lda, b, ldb, (float*)C, ldc, (float)alpha,
+                                                   (float)beta, S(stream));
+    } else if (big_tiles >= 512) {
       if (big_tiles > 0x7fffffffLL) return set_err(SPX_EINVAL, "spx_gemm: too many tiles");
       e = GemmF32Big::launch(M, N, K, a, lda, b, ldb, (float*)C, ldc, (float)alpha, (float)beta,
                              GemmF32Big::is_aligned(M, N, K, A, lda, B, ldb), S(stream));
@@ -713,6 +744,12 @@ extern "C" int spx_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* 
   } else {
     i64 tiles = ((M + 127) / 128) * ((N + 127) / 128);
     if (tiles > 0x7fffffffLL) return set_err(SPX_EINVAL, "spx_gemm: too many tiles");
+    if (tiles >= 1024 && gemm_p3_on() > 1 && spx_mfma::p3d_ok<16>(M, N, K, A, lda, B, ldb)) {
+      const double *a = (const double*)A, *b = (const double*)B;
+      e = gemm_kchunks<double>(K, a, b, ldb, beta, [&](i64 kc, const double* ak, const double* bk, double bt) {
+        return spx_mfma::p3d_launch<8, 16>(M, N, kc, ak, lda, bk, ldb, (double*)C, ldc, alpha, bt, S(stream));
+      });
+    } else
     e = GemmF64::launch(M, N, K, (const double*)A, lda, (const double*)B, ldb, (double*)C, ldc, alpha, beta,
                         GemmF64::is_aligned(M, N, K, A, lda, B, ldb), S(stream));
     if (e != hipSuccess) return set_err(SPX_EHIP, "spx_gemm(f64) launch failed: %s", hipGetErrorString(e));

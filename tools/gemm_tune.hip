@@ -49,6 +49,55 @@ __global__ void init(T* p, i64 n, unsigned seed) {
   }
 }
 
+// max over all elements of |C - R| / max(|R|, 1e-30), as ordered int bits (non-negative floats)
+template <typename T>
+__global__ void maxrel(const T* C, const T* R, i64 n, unsigned int* out) {
+  float m = 0.f;
+  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
+    const double r = (double)R[i], d = fabs((double)C[i] - r) / fmax(fabs(r), 1e-30);
+    m = fmaxf(m, d == d ? (float)d : 3e38f);
+  }
+  atomicMax(out, __float_as_uint(m));
+}
+
+hipError_t p3_8(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i64 ldb, float* C, i64 ldc, float alpha,
+                float beta, bool, hipStream_t s) {
+  return spx_mfma::p3_launch<8>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, s);
+}
+hipError_t p3_4(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i64 ldb, float* C, i64 ldc, float alpha,
+                float beta, bool, hipStream_t s) {
+  return spx_mfma::p3_launch<4>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, s);
+}
+hipError_t p3_16(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i64 ldb, float* C, i64 ldc, float alpha,
+                 float beta, bool, hipStream_t s) {
+  return spx_mfma::p3_launch<16>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, s);
+}
+hipError_t p3_fl(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i64 ldb, float* C, i64 ldc,
+                 float alpha, float beta, bool, hipStream_t s) {
+  return spx_mfma::p3_launch<8, 0, 512>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, s);
+}
+// the K-chunked form spx_gemm runs: chains of at most 8192 k, beta = 1 after the first chunk
+hipError_t p3_8c(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i64 ldb, float* C, i64 ldc,
+                 float alpha, float beta, bool, hipStream_t s) {
+  for (i64 k0 = 0; k0 < K; k0 += 8192) {
+    const i64 kc = K - k0 < 8192 ? K - k0 : 8192;
+    hipError_t e = spx_mfma::p3_launch<8>(M, N, kc, A + k0, lda, B + k0 * ldb, ldb, C, ldc, alpha, k0 ? 1.f : beta, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t p3d_16(i64 M, i64 N, i64 K, const double* A, i64 lda, const double* B, i64 ldb, double* C, i64 ldc,
+                  double alpha, double beta, bool, hipStream_t s) {
+  return spx_mfma::p3d_launch<8, 16>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, s);
+}
+
+template <int ABL>
+hipError_t p3a(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i64 ldb, float* C, i64 ldc, float alpha,
+               float beta, bool, hipStream_t s) {
+  return spx_mfma::p3_launch<8, ABL>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, s);
+}
+
 template <typename T>
 void run(i64 S, int rounds, std::vector<Variant<T>> vs, double peak) {
   T *A, *B, *C, *R;
@@ -82,6 +131,21 @@ void run(i64 S, int rounds, std::vector<Variant<T>> vs, double peak) {
       for (int i = 0; i < 64; ++i) err = fmax(err, fabs((double)got[i] - (double)ref[i]) / fabs((double)ref[i]));
       if (err > (sizeof(T) == 8 ? 1e-12 : 1e-5)) printf("  MISMATCH %s rel %g\n", vs[v].name.c_str(), err);
     }
+  {  // every element of every variant against the first
+    unsigned int* dm;
+    CK(hipMalloc(&dm, 4));
+    for (size_t v = 1; v < vs.size(); ++v) {
+      CK(hipMemset(dm, 0, 4));
+      CK(vs[v].launch(S, S, S, A, S, B, S, C, S, (T)1, (T)0, true, 0));
+      maxrel<T><<<1024, 256>>>(C, R, (i64)n, dm);
+      unsigned int hm;
+      CK(hipMemcpy(&hm, dm, 4, hipMemcpyDeviceToHost));
+      float fm;
+      memcpy(&fm, &hm, 4);
+      printf("  %-24s max rel diff vs %s over all %zu elements: %.3g\n", vs[v].name.c_str(), vs[0].name.c_str(), n, fm);
+    }
+    CK(hipFree(dm));
+  }
   double fl = 2.0 * S * S * S;
   for (size_t v = 0; v < vs.size(); ++v) {
     float best = 1e30f;
@@ -110,6 +174,27 @@ int main(int argc, char** argv) {
                 {V(double, 128, 128, 16, 4, 4, 0), V(double, 128, 128, 16, 2, 2, 0), V(double, 128, 128, 16, 2, 2, 8),
                  V(double, 256, 128, 16, 2, 2, 8), V(double, 128, 128, 32, 2, 2, 8), V(double, 256, 256, 16, 2, 2, 8),
                  V(double, 128, 256, 16, 2, 2, 8)},
+                78.6);
+    return 0;
+  }
+  if (which == "p3") {  // the three-stage one-wave-per-SIMD kernel against the product
+    run<float>(S, rounds,
+               {VG(float, 256, 128, 16, 4, 2, 8, 512), Variant<float>{"p3 g8", p3_8}, Variant<float>{"p3 g4", p3_4},
+                Variant<float>{"p3 g16", p3_16}, Variant<float>{"p3 g8 kchunk8192", p3_8c},
+                Variant<float>{"p3 g8 fl512", p3_fl}},
+               157.3);
+    return 0;
+  }
+  if (which == "p3abl") {  // ablations of the p3 kernel (results wrong by design for 1-3)
+    run<float>(S, rounds,
+               {Variant<float>{"p3", p3a<0>}, Variant<float>{"p3 abl1 no-ldst", p3a<1>},
+                Variant<float>{"p3 abl2 +no-bar", p3a<2>}, Variant<float>{"p3 abl3 +no-aread", p3a<3>}},
+               157.3);
+    return 0;
+  }
+  if (which == "p3d") {  // fp64 three-stage one-wave-per-SIMD kernels against the product
+    run<double>(S, rounds,
+                {V(double, 128, 128, 16, 4, 4, 0), Variant<double>{"p3d bk16 g8", p3d_16}},
                 78.6);
     return 0;
   }
