@@ -321,7 +321,7 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
 constexpr int P3_AST = 20;                            // A row stride (floats): k-contiguous, +4 pad
 constexpr int P3_SA = 256 * P3_AST, P3_SB = 16 * 256;  // floats per stage
 constexpr int P3_LDS = 3 * (P3_SA + P3_SB) * 4;       // bytes
-template <int GM, int ABL = 0, int FL = 0>
+template <int GM, int ABL = 0, int FL = 0, int BT = 0>
 __global__ __launch_bounds__(256, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, const float* __restrict__ A, i64 lda,
                                                     const float* __restrict__ B, i64 ldb, float* __restrict__ C,
                                                     i64 ldc, float alpha, float beta, int tiles_n, int ntiles) {
@@ -370,18 +370,29 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, const
       }
     }
   };
+  // BT = 0: MFMA tile j's lane li is output column wn 128 + 32 j + li (four
+  // b32 reads per step); BT = 1: column wn 128 + 4 li + j, so a lane's four
+  // B values of a step are one ds_read_b128 and its four tiles' values of a
+  // row one 16-byte store in the epilogue
   auto read_b = [&](int s, int kk, float (&b)[4]) __attribute__((always_inline)) {
-    const float* p = abuf(s) + P3_SA + (kb + kk) * 256 + wn * 128 + li;
+    if constexpr (BT) {
+      const V v = *(const V*)(abuf(s) + P3_SA + (kb + kk) * 256 + wn * 128 + 4 * li);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = p[32 * j];
+      for (int j = 0; j < 4; ++j) b[j] = v[j];
+    } else {
+      const float* p = abuf(s) + P3_SA + (kb + kk) * 256 + wn * 128 + li;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = p[32 * j];
+    }
   };
+  auto ccol = [&](int j, int l) __attribute__((always_inline)) { return BT ? 4 * l + j : 32 * j + l; };
   // K runs in chunks of FL K-tiles (FL > 0; one chunk otherwise), each with
   // its own pipeline fill; between chunks the accumulators go into C (see
   // flush below) -- there no pipeline state is live, so the flush needs no
   // registers the K loop holds
   const int nkt = (int)(K / 16);
   int kb0 = 0, nk = nkt;
-  float avA[4][8], avB[4][8], bn[4];
+  float avA[4][8], avB[4][8], bn[2][4];
   // one K-tile: MFMAs from av (this tile's A fragments), B read a step
   // ahead; woven between each step's four MFMA groups: one piece of tile
   // kt + 2's LDS stage (its global loads were issued a tile earlier, piece
@@ -416,19 +427,27 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, const
     // buffer nobody reads again, the loads re-read the last tile
     constexpr bool st = ABL < 1, ld = ABL < 1, ra_ = ABL < 3;
     const i64 k3 = (i64)(kb0 + (kt + 3 < nk ? kt + 3 : nk - 1)) * 16;
-    float b[2][4];
+    // B two steps ahead (a ring of three): step kk reads step kk + 2's
+    // values, steps 6 / 7 the next tile's steps 0 / 1 (bn[0] / bn[1])
+    float b[3][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[0][j] = bn[j];
+    for (int j = 0; j < 4; ++j) {
+      b[0][j] = bn[0][j];
+      b[1][j] = bn[1][j];
+    }
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
-      if (kk + 1 < 8) read_b(s, kk + 1, b[(kk + 1) & 1]);
-      if (kk == 7) read_b(s1, 0, bn);
+      if (ABL < 4 && kk + 2 < 8) read_b(s, kk + 2, b[(kk + 2) % 3]);
+      if (ABL >= 4 && kk + 2 < 8)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[(kk + 2) % 3][j] = bn[0][j];
+      if (kk >= 6) read_b(s1, kk - 6, bn[kk - 6]);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][kk], b[kk & 1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][kk], b[kk % 3][j], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
         if (i == 0 && st) store_piece(s2, kk);
         if (i == 1 && ld) load_piece(k3, kk);
@@ -451,14 +470,14 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, const
     // compiler from hoisting all 256 of them (512 registers) out of the loop
     asm volatile("" : "+v"(fl));
     asm volatile("" : "+s"(ldf));
-    float* const cb = C + (row0 + wm * 128 + Mfma<float>::crow(fl, 0)) * ldf + col0 + wn * 128 + (fl & 31);
+    float* const cb = C + (row0 + wm * 128 + Mfma<float>::crow(fl, 0)) * ldf + col0 + wn * 128 + ccol(0, fl & 31);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float* const pc = cb + (i64)(i * 32 + Mfma<float>::crow(0, r)) * ldf + j * 32;
+          float* const pc = cb + (i64)(i * 32 + Mfma<float>::crow(0, r)) * ldf + ccol(j, 0);
           const float v = alpha * acc[i][j][r];
           if (again || use_beta)
             unsafeAtomicAdd(pc, v);
@@ -480,7 +499,8 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, const
     }
     __syncthreads();
     read_a(0, avA);
-    read_b(0, 0, bn);
+    read_b(0, 0, bn[0]);
+    read_b(0, 1, bn[1]);
     load((i64)(kb0 + (nk > 2 ? 2 : nk - 1)) * 16);
     int s = 0;
     int kt = 0;
@@ -509,7 +529,7 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, const
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const i64 gr = row0 + wm * 128 + i * 32 + Mfma<float>::crow(lane, r);
-        const i64 gc = col0 + wn * 128 + j * 32 + li;
+        const i64 gc = col0 + wn * 128 + ccol(j, li);
         float v = alpha * acc[i][j][r];
         if (use_beta) v += beta * C[gr * ldc + gc];
         C[gr * ldc + gc] = v;
@@ -706,18 +726,18 @@ __host__ inline bool p3_ok(i64 M, i64 N, i64 K, const void* A, i64 lda, const vo
          (uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0;
 }
 
-template <int GM, int ABL = 0, int FL = 0>
+template <int GM, int ABL = 0, int FL = 0, int BT = 0>
 __host__ inline hipError_t p3_launch(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i64 ldb,
                                      float* C, i64 ldc, float alpha, float beta, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_f32_p3<GM, ABL, FL>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_f32_p3<GM, ABL, FL, BT>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, P3_LDS);
     if (e != hipSuccess) return e;
     attr = true;
   }
   const i64 tn = N / 256, nt = (M / 256) * tn;
-  gemm_f32_p3<GM, ABL, FL><<<(unsigned)nt, 256, P3_LDS, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, (int)tn, (int)nt);
+  gemm_f32_p3<GM, ABL, FL, BT><<<(unsigned)nt, 256, P3_LDS, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, (int)tn, (int)nt);
   return hipGetLastError();
 }
 

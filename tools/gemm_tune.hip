@@ -76,6 +76,14 @@ hipError_t p3_fl(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i
                  float alpha, float beta, bool, hipStream_t s) {
   return spx_mfma::p3_launch<8, 0, 512>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, s);
 }
+hipError_t p3_flbt(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i64 ldb, float* C, i64 ldc,
+                   float alpha, float beta, bool, hipStream_t s) {
+  return spx_mfma::p3_launch<8, 0, 512, 1>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, s);
+}
+hipError_t p3_bt(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i64 ldb, float* C, i64 ldc,
+                 float alpha, float beta, bool, hipStream_t s) {
+  return spx_mfma::p3_launch<8, 0, 0, 1>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, s);
+}
 // the K-chunked form spx_gemm runs: chains of at most 8192 k, beta = 1 after the first chunk
 hipError_t p3_8c(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i64 ldb, float* C, i64 ldc,
                  float alpha, float beta, bool, hipStream_t s) {
@@ -185,10 +193,18 @@ int main(int argc, char** argv) {
                157.3);
     return 0;
   }
+  if (which == "p3bt") {  // B as one ds_read_b128 per step (interleaved columns)
+    run<float>(S, rounds,
+               {VG(float, 256, 128, 16, 4, 2, 8, 512), Variant<float>{"p3 fl512", p3_fl},
+                Variant<float>{"p3 fl512 bt", p3_flbt}, Variant<float>{"p3", p3_8}, Variant<float>{"p3 bt", p3_bt}},
+               157.3);
+    return 0;
+  }
   if (which == "p3abl") {  // ablations of the p3 kernel (results wrong by design for 1-3)
     run<float>(S, rounds,
                {Variant<float>{"p3", p3a<0>}, Variant<float>{"p3 abl1 no-ldst", p3a<1>},
-                Variant<float>{"p3 abl2 +no-bar", p3a<2>}, Variant<float>{"p3 abl3 +no-aread", p3a<3>}},
+                Variant<float>{"p3 abl2 +no-bar", p3a<2>}, Variant<float>{"p3 abl3 +no-aread", p3a<3>},
+                Variant<float>{"p3 abl4 +no-bread", p3a<4>}},
                157.3);
     return 0;
   }
