@@ -54,10 +54,12 @@ def main():
   if 'kmeans' in d and d['kmeans'].get('kernel_ms'):
     m, _ = avg(lambda n: 'k_kmeans_pp' in n)
     row('kmeans fused', d['kmeans']['kernel_hbm_frac'], 'k_kmeans_pp', m, 4.0 * 1e8 * 128, 'GB/s')
-  for t, tag in (('f32', 'gemm<float'), ('f64', 'gemm<double')):
+  # (round 6: the fp32 product runs gemm_f32_p3, the three-stage kernel)
+  for t, tags in (('f32', ('gemm<float', 'gemm_f32_p3')), ('f64', ('gemm<double', 'gemm_f64_p3'))):
     v = d.get('dot', {}).get(t)
+    tag = '/'.join(tags)
     if v and v.get('kernel_mfma_frac'):
-      m, _ = avg(lambda n: tag in n and 'spx_mfma' in n)
+      m, _ = avg(lambda n: any(g in n for g in tags) and 'spx_mfma' in n)
       row('dot ' + t, v['kernel_mfma_frac'], tag, m, 2.0 * 32768 ** 3, t)
   print('\n'.join(rows))
 
