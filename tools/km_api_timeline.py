@@ -46,7 +46,9 @@ def main():
                            (km, '_replicated_f64', '_replicated_f64'), (km, '_row_blocks', '_row_blocks'),
                            (km, '_assign_fused', '_assign_fused'), (km, '_center_join', '_center_join'),
                            (km, '_count_join', '_count_join'), (ejoin, '_scatter_updates', '_scatter_updates'),
-                           (transfer, 'download', 'download'), (transfer, 'upload', 'upload')):
+                           (transfer, 'download', 'download'), (transfer, 'upload', 'upload'),
+                           (km, '_step_domain', '_step_domain'), (km, '_take_step', '_take_step'),
+                           (km, '_deliver_full', '_deliver_full'), (torch, 'empty', 'torch.empty')):
     wrap(obj, name, label)
   # the registered join functions were bound at import: re-register the wrapped ones
   ejoin.register_join(km.kmeans_count_mapper, km._count_join)
