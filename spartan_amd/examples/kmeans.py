@@ -106,24 +106,6 @@ def _row_blocks(X, ncols):
   return blocks, got
 
 
-# a label buffer allocated while the previous fused step runs (the caching
-# allocator's 0.06 ms for an 800 MB block otherwise sits between the host's
-# glom and the next step's launch): (shape, device) -> tensor
-_SPARE = {}
-
-
-def _labels_buffer(n, device):
-  import torch
-  t = _SPARE.pop((n, str(device)), None)
-  return t if t is not None else torch.empty((n,), dtype=torch.int64, device=device)
-
-
-def _stock_labels(n, device):
-  import torch
-  _SPARE.clear()
-  _SPARE[(n, str(device))] = torch.empty((n,), dtype=torch.int64, device=device)
-
-
 def _deliver_full(target, full):
   """Copy a full-size tensor, identical on every rank, into target's local
   tiles; a local tile that IS the whole array and was never written adopts
@@ -261,17 +243,13 @@ def _assign_fused(arrays, fn_kw, target, dist_dtype):
       pts = got[qi]
       if pts.stride(-1) != 1:
         pts = be.contiguous(pts)
-      lab = _labels_buffer(tex.shape[0], ctx.device)
+      lab = torch.empty((tex.shape[0],), dtype=torch.int64, device=ctx.device)
       if fused:
         be.kmeans_step(pts, c, lab, sums, counts, zero_first=first, dist_dtype=dist_dtype)
         first = False
       else:
         be.kmeans_assign(pts, c, lab, dist_dtype=dist_dtype)
     updates.append((qi, tex, src, lab))
-  # the next call's label buffer, allocated while this step runs
-  mine = [u for u in updates if u[3] is not None]
-  if len(mine) == 1:
-    _stock_labels(mine[0][3].shape[0], ctx.device)
   _scatter_updates(target, updates)
   if fused:
     if first:  # no local row block on this rank
