@@ -300,138 +300,127 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
   flush_c(flushed);
 }
 
-// fp32, one wave per SIMD: a 256 x 256 block tile, 4 waves (2 x 2), each
-// wave 128 x 128 = 4 x 4 v_mfma_f32_32x32x2_f32 tiles (256 accumulator
-// registers), K-tiles of 16.  Three LDS stages: tile t + 2 is written in the
-// middle of tile t's MFMAs (its global loads were issued in the middle of
-// tile t - 1), and tile t + 1's A fragments and first B fragments are read
-// into registers before the one barrier that ends tile t -- so after the
-// barrier the wave's next MFMA has its operands and nothing waits on LDS or
-// HBM at the tile boundary (the two-stage kernel above loses the LDS
-// write, the barrier and the fragment reads' latency there, ~15 % at one
-// wave per SIMD).  Hazards (buffer b = t mod 3):
+// fp32, a 256 x 256 block tile over 2 x WN waves -- WN = 2: one wave per
+// SIMD, each 128 x 128 = 4 x 4 v_mfma_f32_32x32x2_f32 tiles (256 accumulator
+// registers); WN = 4: two waves per SIMD, each 128 x 64 -- K-tiles of 16.
+// Three LDS stages: tile t + 2 is staged during tile t's MFMAs (its global
+// loads were issued during tile t - 1), and tile t + 1's A fragments and
+// first B fragments are read into registers before the one barrier that ends
+// tile t, so after the barrier the wave's next MFMA has its operands.
+// Hazards (buffer b = t mod 3):
 //   * tile t + 2 goes into buffer (t + 2) % 3 = (t - 1) % 3, last read in
 //     tile t - 1 (B reads) and tile t - 2 (its A fragment prefetch): both
 //     before the barrier that ended tile t - 1;
 //   * tile t + 1 (buffer (t + 1) % 3) was written in tile t - 1 by every
 //     wave: visible after the barrier that ended tile t - 1.
 // Requires M % 256 == N % 256 == K % 16 == 0, lda % 4 == ldb % 4 == 0 and
-// 16-byte aligned A, B (p3_ok).  The accumulator chain spans K: callers cap
-// K per launch (spx_gemm runs K in chunks with beta = 1 after the first).
+// 16-byte aligned A, B (p3_ok).  FL > 0: the accumulators go into C every FL
+// K-tiles (in-kernel chunks, see flush); else one chain spans K.
 constexpr int P3_AST = 20;                            // A row stride (floats): k-contiguous, +4 pad
 constexpr int P3_SA = 256 * P3_AST, P3_SB = 16 * 256;  // floats per stage
 constexpr int P3_LDS = 3 * (P3_SA + P3_SB) * 4;       // bytes
-template <int GM, int ABL = 0, int FL = 0, int BT = 0>
-__global__ __launch_bounds__(256, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, const float* __restrict__ A, i64 lda,
-                                                    const float* __restrict__ B, i64 ldb, float* __restrict__ C,
-                                                    i64 ldc, float alpha, float beta, int tiles_n, int ntiles) {
+template <int GM, int ABL = 0, int FL = 0, int BT = 0, int WN = 2, int SCH = 1>
+__global__ __launch_bounds__(128 * WN, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, const float* __restrict__ A, i64 lda,
+                                                         const float* __restrict__ B, i64 ldb, float* __restrict__ C,
+                                                         i64 ldc, float alpha, float beta, int tiles_n, int ntiles) {
   typedef float V __attribute__((ext_vector_type(4)));
+  constexpr int NT = 128 * WN, WTN = 256 / WN, TN = WTN / 32;
+  constexpr int NPA = 1024 / NT, NPB = 1024 / NT, NP = NPA + NPB;  // 16-byte staging pieces per thread
+  static_assert(WN == 2 || WN == 4, "2 x 2 or 2 x 4 waves");
+  typedef float VB __attribute__((ext_vector_type(TN)));
   extern __shared__ __attribute__((aligned(16))) float p3_lds[];
   int tm, tn;
   tile_of(blockIdx.x, ntiles, tiles_n, GM, tm, tn);
   const i64 row0 = (i64)tm * 256, col0 = (i64)tn * 256;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int wm = w >> 1, wn = w & 1;
+  const int wm = w / WN, wn = w % WN;
   const int li = lane & 31, kb = 8 * (lane >> 5);
-  f32x16 acc[4][4];
+  f32x16 acc[4][TN];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x16){};
-  // staging: A rows (t >> 2) + 64 i, k quad t & 3; B rows (t >> 6) + 4 i, column quad t & 63
-  V ra[4], rb[4];
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){};
+  // staging: A piece i = rows (t >> 2) + NT / 4 i, k quad t & 3; B piece i =
+  // rows (t >> 6) + NT / 64 i, column quad t & 63
+  V ra[NPA], rb[NPB];
   const float* ag = A + (row0 + (t >> 2)) * lda + 4 * (t & 3);
   const float* bg = B + (i64)(t >> 6) * ldb + col0 + 4 * (t & 63);
+  auto abuf = [&](int s) __attribute__((always_inline)) { return p3_lds + s * (P3_SA + P3_SB); };
+  auto load_piece = [&](i64 k0, int q) __attribute__((always_inline)) {
+    if (q < NPA)
+      ra[q] = *(const V*)(ag + (i64)(NT / 4) * q * lda + k0);
+    else
+      rb[q - NPA] = *(const V*)(bg + (k0 + (NT / 64) * (q - NPA)) * ldb);
+  };
+  auto store_piece = [&](int sb, int q) __attribute__((always_inline)) {
+    if (q < NPA)
+      *(V*)(abuf(sb) + ((t >> 2) + (NT / 4) * q) * P3_AST + 4 * (t & 3)) = ra[q];
+    else
+      *(V*)(abuf(sb) + P3_SA + ((t >> 6) + (NT / 64) * (q - NPA)) * 256 + 4 * (t & 63)) = rb[q - NPA];
+  };
   auto load = [&](i64 k0) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ra[i] = *(const V*)(ag + (i64)64 * i * lda + k0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) rb[i] = *(const V*)(bg + (k0 + 4 * i) * ldb);
+    for (int q = 0; q < NP; ++q) load_piece(k0, q);
   };
-  auto abuf = [&](int s) __attribute__((always_inline)) { return p3_lds + s * (P3_SA + P3_SB); };
-  auto store = [&](int s) __attribute__((always_inline)) {
-    float* a = abuf(s) + (t >> 2) * P3_AST + 4 * (t & 3);
-    float* b = abuf(s) + P3_SA + (t >> 6) * 256 + 4 * (t & 63);
+  auto store = [&](int sb) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *(V*)(a + 64 * i * P3_AST) = ra[i];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) *(V*)(b + 4 * i * 256) = rb[i];
+    for (int q = 0; q < NP; ++q) store_piece(sb, q);
   };
-  // a lane's A values of a whole K-tile (k = kb .. kb + 7 of rows wm 128 + 32 i + li)
-  auto read_a = [&](int s, float (&av)[4][8]) __attribute__((always_inline)) {
-    const float* a = abuf(s) + (wm * 128 + li) * P3_AST + kb;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const V v0 = *(const V*)(a + 32 * i * P3_AST), v1 = *(const V*)(a + 32 * i * P3_AST + 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        av[i][e] = v0[e];
-        av[i][4 + e] = v1[e];
-      }
-    }
-  };
-  // BT = 0: MFMA tile j's lane li is output column wn 128 + 32 j + li (four
-  // b32 reads per step); BT = 1: column wn 128 + 4 li + j, so a lane's four
-  // B values of a step are one ds_read_b128 and its four tiles' values of a
-  // row one 16-byte store in the epilogue
-  auto read_b = [&](int s, int kk, float (&b)[4]) __attribute__((always_inline)) {
-    if constexpr (BT) {
-      const V v = *(const V*)(abuf(s) + P3_SA + (kb + kk) * 256 + wn * 128 + 4 * li);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = v[j];
-    } else {
-      const float* p = abuf(s) + P3_SA + (kb + kk) * 256 + wn * 128 + li;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = p[32 * j];
-    }
-  };
-  auto ccol = [&](int j, int l) __attribute__((always_inline)) { return BT ? 4 * l + j : 32 * j + l; };
-  // K runs in chunks of FL K-tiles (FL > 0; one chunk otherwise), each with
-  // its own pipeline fill; between chunks the accumulators go into C (see
-  // flush below) -- there no pipeline state is live, so the flush needs no
-  // registers the K loop holds
-  const int nkt = (int)(K / 16);
-  int kb0 = 0, nk = nkt;
-  float avA[4][8], avB[4][8], bn[2][4];
-  // one K-tile: MFMAs from av (this tile's A fragments), B read a step
-  // ahead; woven between each step's four MFMA groups: one piece of tile
-  // kt + 2's LDS stage (its global loads were issued a tile earlier, piece
-  // by piece), the global load of the same piece of tile kt + 3 into the
-  // staging register it just freed, and one ds_read_b128 of tile kt + 1's A
-  // fragments -- one memory instruction between MFMA groups instead of
-  // bursts of eight (a burst held the wave's in-order issue, and with one
-  // wave per SIMD the matrix pipe, for ~9 % of the kernel: tools/gemm_tune
-  // p3abl).  Sched barriers pin the weave.
-  auto store_piece = [&](int sb, int q) __attribute__((always_inline)) {
-    if (q < 4)
-      *(V*)(abuf(sb) + (t >> 2) * P3_AST + 4 * (t & 3) + 64 * q * P3_AST) = ra[q];
-    else
-      *(V*)(abuf(sb) + P3_SA + (t >> 6) * 256 + 4 * (t & 63) + 4 * (q - 4) * 256) = rb[q - 4];
-  };
-  auto load_piece = [&](i64 k0, int q) __attribute__((always_inline)) {
-    if (q < 4)
-      ra[q] = *(const V*)(ag + (i64)64 * q * lda + k0);
-    else
-      rb[q - 4] = *(const V*)(bg + (k0 + 4 * (q - 4)) * ldb);
-  };
+  // a lane's A values of a whole K-tile (k = kb .. kb + 7 of rows wm 128 + 32 i + li): 8 pieces
   auto read_a_piece = [&](int sb, float (&av)[4][8], int q) __attribute__((always_inline)) {
     const int i = q >> 1, hf = q & 1;
     const V v = *(const V*)(abuf(sb) + (wm * 128 + li) * P3_AST + kb + 32 * i * P3_AST + 4 * hf);
 #pragma unroll
     for (int e = 0; e < 4; ++e) av[i][4 * hf + e] = v[e];
   };
+  auto read_a = [&](int sb, float (&av)[4][8]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) read_a_piece(sb, av, q);
+  };
+  // BT = 0: MFMA tile j's lane li is output column wn WTN + 32 j + li (TN
+  // b32 reads per step); BT = 1: column wn WTN + TN li + j, so a lane's TN
+  // B values of a step are one ds_read_b128 (b64 for TN = 2)
+  auto read_b = [&](int sb, int kk, float (&b)[TN]) __attribute__((always_inline)) {
+    if constexpr (BT) {
+      const VB v = *(const VB*)(abuf(sb) + P3_SA + (kb + kk) * 256 + wn * WTN + TN * li);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = v[j];
+    } else {
+      const float* p = abuf(sb) + P3_SA + (kb + kk) * 256 + wn * WTN + li;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = p[32 * j];
+    }
+  };
+  auto ccol = [&](int j, int l) __attribute__((always_inline)) { return BT ? TN * l + j : 32 * j + l; };
+  // K runs in chunks of FL K-tiles (FL > 0; one chunk otherwise), each with
+  // its own pipeline fill; between chunks the accumulators go into C (see
+  // flush below) -- there no pipeline state is live, so the flush needs no
+  // registers the K loop holds (in the loop it spilled)
+  const int nkt = (int)(K / 16);
+  int kb0 = 0, nk = nkt;
+  float avA[4][8], avB[4][8], bn[2][TN];
+  // one K-tile: MFMAs from av (this tile's A fragments), B read two steps
+  // ahead (a ring of three; steps 6 / 7 read the next tile's steps 0 / 1);
+  // woven between each step's four MFMA groups: a piece of tile kt + 2's LDS
+  // stage, the global load of the same piece of tile kt + 3 into the staging
+  // register it just freed, and one ds_read_b128 of tile kt + 1's A
+  // fragments -- one memory instruction between MFMA groups instead of
+  // bursts (a burst held the wave's in-order issue, and with one wave per
+  // SIMD the matrix pipe: tools/gemm_tune p3abl).  Sched barriers pin the
+  // weave.  The memory instructions are unconditional (a branch around one
+  // made hipcc wait vmcnt(0) at every store): past the last tile a stage
+  // writes a buffer nobody reads again and the loads re-read the last tile.
+  // (ABL: dev ablations, results wrong by design -- 1: no global loads or
+  // LDS stores in the loop, 2: also no barrier, 3: also no next-tile A reads,
+  // 4: also no per-step B reads; tools/gemm_tune.hip p3abl)
+  constexpr int PSTEP = 8 / NP;  // k-steps per staging piece
   auto tile = [&](int kt, int s, float (&av)[4][8], float (&avn)[4][8]) __attribute__((always_inline)) {
     const int s1 = s == 2 ? 0 : s + 1, s2 = s1 == 2 ? 0 : s1 + 1;
-    // unconditional (no branch around a memory instruction: hipcc then waits
-    // vmcnt(0) at every store): past the last tile the stage writes a
-    // buffer nobody reads again, the loads re-read the last tile
     constexpr bool st = ABL < 1, ld = ABL < 1, ra_ = ABL < 3;
     const i64 k3 = (i64)(kb0 + (kt + 3 < nk ? kt + 3 : nk - 1)) * 16;
-    // B two steps ahead (a ring of three): step kk reads step kk + 2's
-    // values, steps 6 / 7 the next tile's steps 0 / 1 (bn[0] / bn[1])
-    float b[3][4];
+    float b[3][TN];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < TN; ++j) {
       b[0][j] = bn[0][j];
       b[1][j] = bn[1][j];
     }
@@ -440,17 +429,19 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, const
       if (ABL < 4 && kk + 2 < 8) read_b(s, kk + 2, b[(kk + 2) % 3]);
       if (ABL >= 4 && kk + 2 < 8)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) b[(kk + 2) % 3][j] = bn[0][j];
+        for (int j = 0; j < TN; ++j) b[(kk + 2) % 3][j] = bn[0][j];
       if (kk >= 6) read_b(s1, kk - 6, bn[kk - 6]);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (SCH) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][kk], b[kk % 3][j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (i == 0 && st) store_piece(s2, kk);
-        if (i == 1 && ld) load_piece(k3, kk);
+        if constexpr (SCH) __builtin_amdgcn_sched_barrier(0);
+        if (kk % PSTEP == 0) {
+          if (i == 0 && st) store_piece(s2, kk / PSTEP);
+          if (i == 1 && ld) load_piece(k3, kk / PSTEP);
+        }
         if (i == 2 && ra_) read_a_piece(s1, avn, kk);
       }
     }
@@ -467,14 +458,14 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, const
     int fl = lane;
     i64 ldf = ldc;
     // the addresses are invariant across chunks: opaque operands keep the
-    // compiler from hoisting all 256 of them (512 registers) out of the loop
+    // compiler from hoisting all of them (two registers each) out of the loop
     asm volatile("" : "+v"(fl));
     asm volatile("" : "+s"(ldf));
-    float* const cb = C + (row0 + wm * 128 + Mfma<float>::crow(fl, 0)) * ldf + col0 + wn * 128 + ccol(0, fl & 31);
+    float* const cb = C + (row0 + wm * 128 + Mfma<float>::crow(fl, 0)) * ldf + col0 + wn * WTN + ccol(0, fl & 31);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < TN; ++j) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float* const pc = cb + (i64)(i * 32 + Mfma<float>::crow(0, r)) * ldf + ccol(j, 0);
@@ -525,11 +516,11 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, const
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const i64 gr = row0 + wm * 128 + i * 32 + Mfma<float>::crow(lane, r);
-        const i64 gc = col0 + wn * 128 + ccol(j, li);
+        const i64 gc = col0 + wn * WTN + ccol(j, li);
         float v = alpha * acc[i][j][r];
         if (use_beta) v += beta * C[gr * ldc + gc];
         C[gr * ldc + gc] = v;
@@ -726,18 +717,18 @@ __host__ inline bool p3_ok(i64 M, i64 N, i64 K, const void* A, i64 lda, const vo
          (uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0;
 }
 
-template <int GM, int ABL = 0, int FL = 0, int BT = 0>
+template <int GM, int ABL = 0, int FL = 0, int BT = 0, int WN = 2, int SCH = 1>
 __host__ inline hipError_t p3_launch(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i64 ldb,
                                      float* C, i64 ldc, float alpha, float beta, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_f32_p3<GM, ABL, FL, BT>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_f32_p3<GM, ABL, FL, BT, WN, SCH>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, P3_LDS);
     if (e != hipSuccess) return e;
     attr = true;
   }
   const i64 tn = N / 256, nt = (M / 256) * tn;
-  gemm_f32_p3<GM, ABL, FL, BT><<<(unsigned)nt, 256, P3_LDS, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, (int)tn, (int)nt);
+  gemm_f32_p3<GM, ABL, FL, BT, WN, SCH><<<(unsigned)nt, 128 * WN, P3_LDS, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, (int)tn, (int)nt);
   return hipGetLastError();
 }
 

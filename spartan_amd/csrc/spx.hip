@@ -730,8 +730,8 @@ extern "C" int spx_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* 
     if (big_tiles >= 512 && big_tiles <= 0x7fffffffLL && gemm_p3_on() && spx_mfma::p3_ok(M, N, K, A, lda, B, ldb)) {
       // one launch, K in chunks of SPX_GEMM_GFL K-tiles inside the kernel
       // (beta is 0 or 1 here, as the flush needs)
-      e = spx_mfma::p3_launch<8, 0, SPX_GEMM_GFL, 1>(M, N, K, a, lda, b, ldb, (float*)C, ldc, (float)alpha,
-                                                      (float)beta, S(stream));
+      e = spx_mfma::p3_launch<8, 0, SPX_GEMM_GFL, 1, 4>(M, N, K, a, lda, b, ldb, (float*)C, ldc, (float)alpha,
+                                                         (float)beta, S(stream));
     } else if (big_tiles >= 512) {
       if (big_tiles > 0x7fffffffLL) return set_err(SPX_EINVAL, "spx_gemm: too many tiles");
       e = GemmF32Big::launch(M, N, K, a, lda, b, ldb, (float*)C, ldc, (float)alpha, (float)beta,

@@ -84,6 +84,16 @@ hipError_t p3_bt(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i
                  float alpha, float beta, bool, hipStream_t s) {
   return spx_mfma::p3_launch<8, 0, 0, 1>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, s);
 }
+template <int ABL>
+hipError_t p3wa(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i64 ldb, float* C, i64 ldc, float alpha,
+                float beta, bool, hipStream_t s) {
+  return spx_mfma::p3_launch<8, ABL, 0, 1, 4>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, s);
+}
+template <int WN, int BT, int FL, int SCH = 1, int GM = 8>
+hipError_t p3w(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i64 ldb, float* C, i64 ldc, float alpha,
+               float beta, bool, hipStream_t s) {
+  return spx_mfma::p3_launch<GM, 0, FL, BT, WN, SCH>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, s);
+}
 // the K-chunked form spx_gemm runs: chains of at most 8192 k, beta = 1 after the first chunk
 hipError_t p3_8c(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i64 ldb, float* C, i64 ldc,
                  float alpha, float beta, bool, hipStream_t s) {
@@ -197,6 +207,31 @@ int main(int argc, char** argv) {
     run<float>(S, rounds,
                {VG(float, 256, 128, 16, 4, 2, 8, 512), Variant<float>{"p3 fl512", p3_fl},
                 Variant<float>{"p3 fl512 bt", p3_flbt}, Variant<float>{"p3", p3_8}, Variant<float>{"p3 bt", p3_bt}},
+               157.3);
+    return 0;
+  }
+  if (which == "p3wabl") {  // ablations of the 8-wave form (wrong results by design past 0)
+    run<float>(S, rounds,
+               {Variant<float>{"p3w8", p3wa<0>}, Variant<float>{"p3w8 abl1 no-ldst", p3wa<1>},
+                Variant<float>{"p3w8 abl2 +no-bar", p3wa<2>}, Variant<float>{"p3w8 abl3 +no-aread", p3wa<3>},
+                Variant<float>{"p3w8 abl4 +no-bread", p3wa<4>}},
+               157.3);
+    return 0;
+  }
+  if (which == "p3w2") {  // the 8-wave form: scheduling and grouping
+    run<float>(S, rounds,
+               {Variant<float>{"p3 w8 bt fl512", p3w<4, 1, 512>}, Variant<float>{"p3 w8 bt fl512 nosch", p3w<4, 1, 512, 0>},
+                Variant<float>{"p3 w8 bt fl512 g4", p3w<4, 1, 512, 1, 4>},
+                Variant<float>{"p3 w8 bt fl512 g16", p3w<4, 1, 512, 1, 16>},
+                Variant<float>{"p3 w8 bt fl1024", p3w<4, 1, 1024>}},
+               157.3);
+    return 0;
+  }
+  if (which == "p3w") {  // 4 waves (one per SIMD) vs 8 waves (two per SIMD) of the three-stage kernel
+    run<float>(S, rounds,
+               {VG(float, 256, 128, 16, 4, 2, 8, 512), Variant<float>{"p3 w4 bt fl512", p3w<2, 1, 512>},
+                Variant<float>{"p3 w8 bt fl512", p3w<4, 1, 512>}, Variant<float>{"p3 w8 fl512", p3w<4, 0, 512>},
+                Variant<float>{"p3 w8 bt", p3w<4, 1, 0>}},
                157.3);
     return 0;
   }
