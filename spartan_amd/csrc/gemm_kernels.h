@@ -319,7 +319,7 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm(i64 M, i64 N, i64 K, const T
 constexpr int P3_AST = 20;                            // A row stride (floats): k-contiguous, +4 pad
 constexpr int P3_SA = 256 * P3_AST, P3_SB = 16 * 256;  // floats per stage
 constexpr int P3_LDS = 3 * (P3_SA + P3_SB) * 4;       // bytes
-template <int GM, int ABL = 0, int FL = 0, int BT = 0, int WN = 2, int SCH = 1>
+template <int GM, int ABL = 0, int FL = 0, int BT = 0, int WN = 2, int SCH = 1, int GL = 0>
 __global__ __launch_bounds__(128 * WN, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, const float* __restrict__ A, i64 lda,
                                                          const float* __restrict__ B, i64 ldb, float* __restrict__ C,
                                                          i64 ldc, float alpha, float beta, int tiles_n, int ntiles) {
@@ -328,6 +328,14 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, 
   constexpr int NPA = 1024 / NT, NPB = 1024 / NT, NP = NPA + NPB;  // 16-byte staging pieces per thread
   static_assert(WN == 2 || WN == 4, "2 x 2 or 2 x 4 waves");
   typedef float VB __attribute__((ext_vector_type(TN)));
+  // GL = 1: tiles staged by global_load_lds (no staging registers, no LDS
+  // write instructions); A rows then unpadded (16 floats) with the 16-byte
+  // chunks XOR-swizzled by row ((row >> 2) & 3, on the global SOURCE address:
+  // the DMA's LDS destination is lane-linear) so the fragment reads stay
+  // conflict-free; NG pieces (1 KiB DMA instructions) per wave and tile
+  constexpr int AST = GL ? 16 : P3_AST, SA = 256 * AST, SST = SA + P3_SB;
+  constexpr int NG = 32 / (2 * WN), NGA = NG / 2;
+  typedef __attribute__((address_space(3))) void* lds_ptr;
   extern __shared__ __attribute__((aligned(16))) float p3_lds[];
   int tm, tn;
   tile_of(blockIdx.x, ntiles, tiles_n, GM, tm, tn);
@@ -345,7 +353,23 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, 
   V ra[NPA], rb[NPB];
   const float* ag = A + (row0 + (t >> 2)) * lda + 4 * (t & 3);
   const float* bg = B + (i64)(t >> 6) * ldb + col0 + 4 * (t & 63);
-  auto abuf = [&](int s) __attribute__((always_inline)) { return p3_lds + s * (P3_SA + P3_SB); };
+  auto abuf = [&](int s) __attribute__((always_inline)) { return p3_lds + s * SST; };
+  auto gl_piece = [&](i64 k0, int sb, int q) __attribute__((always_inline)) {
+    if (q < NGA) {
+      const int rb = NGA * w + q, m = 16 * rb + (lane >> 2);
+      const int c = (lane & 3) ^ ((lane >> 4) & 3);  // the source chunk of this lane's LDS slot
+      __builtin_amdgcn_global_load_lds(A + (row0 + m) * lda + k0 + 4 * c, (lds_ptr)(abuf(sb) + 16 * 16 * rb), 16, 0,
+                                       0);
+    } else {
+      const int r = (NG - NGA) * w + (q - NGA);
+      __builtin_amdgcn_global_load_lds(B + (k0 + r) * ldb + col0 + 4 * lane, (lds_ptr)(abuf(sb) + SA + 256 * r), 16,
+                                       0, 0);
+    }
+  };
+  auto gl_tile = [&](i64 k0, int sb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < NG; ++q) gl_piece(k0, sb, q);
+  };
   auto load_piece = [&](i64 k0, int q) __attribute__((always_inline)) {
     if (q < NPA)
       ra[q] = *(const V*)(ag + (i64)(NT / 4) * q * lda + k0);
@@ -354,9 +378,9 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, 
   };
   auto store_piece = [&](int sb, int q) __attribute__((always_inline)) {
     if (q < NPA)
-      *(V*)(abuf(sb) + ((t >> 2) + (NT / 4) * q) * P3_AST + 4 * (t & 3)) = ra[q];
+      *(V*)(abuf(sb) + ((t >> 2) + (NT / 4) * q) * AST + 4 * (t & 3)) = ra[q];
     else
-      *(V*)(abuf(sb) + P3_SA + ((t >> 6) + (NT / 64) * (q - NPA)) * 256 + 4 * (t & 63)) = rb[q - NPA];
+      *(V*)(abuf(sb) + SA + ((t >> 6) + (NT / 64) * (q - NPA)) * 256 + 4 * (t & 63)) = rb[q - NPA];
   };
   auto load = [&](i64 k0) __attribute__((always_inline)) {
 #pragma unroll
@@ -369,7 +393,8 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, 
   // a lane's A values of a whole K-tile (k = kb .. kb + 7 of rows wm 128 + 32 i + li): 8 pieces
   auto read_a_piece = [&](int sb, float (&av)[4][8], int q) __attribute__((always_inline)) {
     const int i = q >> 1, hf = q & 1;
-    const V v = *(const V*)(abuf(sb) + (wm * 128 + li) * P3_AST + kb + 32 * i * P3_AST + 4 * hf);
+    const int ch = GL ? (((kb >> 2) + hf) ^ ((li >> 2) & 3)) : (kb >> 2) + hf;  // (swizzled) 16-byte chunk
+    const V v = *(const V*)(abuf(sb) + (wm * 128 + li + 32 * i) * AST + 4 * ch);
 #pragma unroll
     for (int e = 0; e < 4; ++e) av[i][4 * hf + e] = v[e];
   };
@@ -382,11 +407,11 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, 
   // B values of a step are one ds_read_b128 (b64 for TN = 2)
   auto read_b = [&](int sb, int kk, float (&b)[TN]) __attribute__((always_inline)) {
     if constexpr (BT) {
-      const VB v = *(const VB*)(abuf(sb) + P3_SA + (kb + kk) * 256 + wn * WTN + TN * li);
+      const VB v = *(const VB*)(abuf(sb) + SA + (kb + kk) * 256 + wn * WTN + TN * li);
 #pragma unroll
       for (int j = 0; j < TN; ++j) b[j] = v[j];
     } else {
-      const float* p = abuf(sb) + P3_SA + (kb + kk) * 256 + wn * WTN + li;
+      const float* p = abuf(sb) + SA + (kb + kk) * 256 + wn * WTN + li;
 #pragma unroll
       for (int j = 0; j < TN; ++j) b[j] = p[32 * j];
     }
@@ -416,8 +441,9 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, 
   constexpr int PSTEP = 8 / NP;  // k-steps per staging piece
   auto tile = [&](int kt, int s, float (&av)[4][8], float (&avn)[4][8]) __attribute__((always_inline)) {
     const int s1 = s == 2 ? 0 : s + 1, s2 = s1 == 2 ? 0 : s1 + 1;
-    constexpr bool st = ABL < 1, ld = ABL < 1, ra_ = ABL < 3;
+    constexpr bool st = ABL < 1 && !GL, ld = ABL < 1 && !GL, ra_ = ABL < 3, gl = ABL < 1 && GL;
     const i64 k3 = (i64)(kb0 + (kt + 3 < nk ? kt + 3 : nk - 1)) * 16;
+    const i64 k2 = (i64)(kb0 + (kt + 2 < nk ? kt + 2 : nk - 1)) * 16;
     float b[3][TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -442,6 +468,9 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, 
           if (i == 0 && st) store_piece(s2, kk / PSTEP);
           if (i == 1 && ld) load_piece(k3, kk / PSTEP);
         }
+        // GL: tile kt + 2's DMA pieces early in the tile (the barrier that
+        // ends it waits for them)
+        if (gl && i == 1 && kk < NG) gl_piece(k2, s2, kk);
         if (i == 2 && ra_) read_a_piece(s1, avn, kk);
       }
     }
@@ -482,17 +511,23 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_f32_p3(i64 M, i64 N, i64 K, 
   constexpr int CH = FL > 0 ? FL : (1 << 30);
   for (kb0 = 0; kb0 < nkt; kb0 += CH) {
     nk = nkt - kb0 < CH ? nkt - kb0 : CH;
-    load((i64)kb0 * 16);
-    store(0);
-    if (nk > 1) {
-      load((i64)(kb0 + 1) * 16);
-      store(1);
+    if constexpr (GL) {
+      gl_tile((i64)kb0 * 16, 0);
+      gl_tile((i64)(kb0 + (nk > 1 ? 1 : 0)) * 16, 1);
+      __syncthreads();
+    } else {
+      load((i64)kb0 * 16);
+      store(0);
+      if (nk > 1) {
+        load((i64)(kb0 + 1) * 16);
+        store(1);
+      }
+      __syncthreads();
     }
-    __syncthreads();
     read_a(0, avA);
     read_b(0, 0, bn[0]);
     read_b(0, 1, bn[1]);
-    load((i64)(kb0 + (nk > 2 ? 2 : nk - 1)) * 16);
+    if constexpr (!GL) load((i64)(kb0 + (nk > 2 ? 2 : nk - 1)) * 16);
     int s = 0;
     int kt = 0;
     for (; kt + 1 < nk; kt += 2) {
@@ -717,18 +752,18 @@ __host__ inline bool p3_ok(i64 M, i64 N, i64 K, const void* A, i64 lda, const vo
          (uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0;
 }
 
-template <int GM, int ABL = 0, int FL = 0, int BT = 0, int WN = 2, int SCH = 1>
+template <int GM, int ABL = 0, int FL = 0, int BT = 0, int WN = 2, int SCH = 1, int GL = 0>
 __host__ inline hipError_t p3_launch(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i64 ldb,
                                      float* C, i64 ldc, float alpha, float beta, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_f32_p3<GM, ABL, FL, BT, WN, SCH>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_f32_p3<GM, ABL, FL, BT, WN, SCH, GL>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, P3_LDS);
     if (e != hipSuccess) return e;
     attr = true;
   }
   const i64 tn = N / 256, nt = (M / 256) * tn;
-  gemm_f32_p3<GM, ABL, FL, BT, WN, SCH><<<(unsigned)nt, 128 * WN, P3_LDS, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, (int)tn, (int)nt);
+  gemm_f32_p3<GM, ABL, FL, BT, WN, SCH, GL><<<(unsigned)nt, 128 * WN, P3_LDS, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, (int)tn, (int)nt);
   return hipGetLastError();
 }
 

@@ -84,6 +84,11 @@ hipError_t p3_bt(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i
                  float alpha, float beta, bool, hipStream_t s) {
   return spx_mfma::p3_launch<8, 0, 0, 1>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, s);
 }
+template <int WN, int FL>
+hipError_t p3g(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i64 ldb, float* C, i64 ldc, float alpha,
+               float beta, bool, hipStream_t s) {
+  return spx_mfma::p3_launch<8, 0, FL, 1, WN, 1, 1>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, s);
+}
 template <int ABL>
 hipError_t p3wa(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i64 ldb, float* C, i64 ldc, float alpha,
                 float beta, bool, hipStream_t s) {
@@ -207,6 +212,13 @@ int main(int argc, char** argv) {
     run<float>(S, rounds,
                {VG(float, 256, 128, 16, 4, 2, 8, 512), Variant<float>{"p3 fl512", p3_fl},
                 Variant<float>{"p3 fl512 bt", p3_flbt}, Variant<float>{"p3", p3_8}, Variant<float>{"p3 bt", p3_bt}},
+               157.3);
+    return 0;
+  }
+  if (which == "p3gl") {  // staging by global_load_lds
+    run<float>(S, rounds,
+               {Variant<float>{"p3 w8 bt fl512", p3w<4, 1, 512>}, Variant<float>{"p3 w8 bt fl512 glds", p3g<4, 512>},
+                Variant<float>{"p3 w4 bt fl512 glds", p3g<2, 512>}, Variant<float>{"p3 w8 bt glds", p3g<4, 0>}},
                157.3);
     return 0;
   }
