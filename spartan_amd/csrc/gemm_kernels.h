@@ -575,7 +575,7 @@ template <int BK>
 struct P3d {
   static constexpr int AST = BK + 2, BST = 132, SA = 128 * AST, SB = BK * BST, LDS = 3 * (SA + SB) * 8, KQ = BK / 4;
 };
-template <int GM, int BK>
+template <int GM, int BK, int ABL = 0>
 __global__ __launch_bounds__(256, 1) void gemm_f64_p3(i64 M, i64 N, i64 K, const double* __restrict__ A, i64 lda,
                                                     const double* __restrict__ B, i64 ldb, double* __restrict__ C,
                                                     i64 ldc, double alpha, double beta, int tiles_n, int ntiles) {
@@ -682,7 +682,10 @@ __global__ __launch_bounds__(256, 1) void gemm_f64_p3(i64 M, i64 N, i64 K, const
     for (int j = 0; j < 4; ++j) b[0][j] = bn[j];
 #pragma unroll
     for (int kk = 0; kk < KQ; ++kk) {
-      if (kk + 1 < KQ) read_b(s, kk + 1, b[(kk + 1) & 1]);
+      if (ABL < 4 && kk + 1 < KQ) read_b(s, kk + 1, b[(kk + 1) & 1]);
+      if (ABL >= 4 && kk + 1 < KQ)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[(kk + 1) & 1][j] = bn[j];
       if (kk == KQ - 1) read_b(s1, 0, bn);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -692,10 +695,12 @@ __global__ __launch_bounds__(256, 1) void gemm_f64_p3(i64 M, i64 N, i64 K, const
           acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i][kk], b[kk & 1][j], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
         const int q = 2 * kk + (i >> 1);
-        if ((i & 1) == 0) store_piece(s2, q);
+        // (ABL: dev ablations as in the fp32 kernel: 1 no staging, 3 also no
+        // next-tile A reads, 4 also no per-step B reads)
+        if (ABL < 1 && (i & 1) == 0) store_piece(s2, q);
         if ((i & 1) == 1) {
-          load_piece(k3, q);
-          read_a_piece(s1, avn, q);
+          if (ABL < 1) load_piece(k3, q);
+          if (ABL < 3) read_a_piece(s1, avn, q);
         }
       }
     }
@@ -731,18 +736,18 @@ __host__ inline bool p3d_ok(i64 M, i64 N, i64 K, const void* A, i64 lda, const v
          (uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0;
 }
 
-template <int GM, int BK>
+template <int GM, int BK, int ABL = 0>
 __host__ inline hipError_t p3d_launch(i64 M, i64 N, i64 K, const double* A, i64 lda, const double* B, i64 ldb,
                                       double* C, i64 ldc, double alpha, double beta, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_f64_p3<GM, BK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_f64_p3<GM, BK, ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        P3d<BK>::LDS);
     if (e != hipSuccess) return e;
     attr = true;
   }
   const i64 tn = N / 128, nt = (M / 128) * tn;
-  gemm_f64_p3<GM, BK><<<(unsigned)nt, 256, P3d<BK>::LDS, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, (int)tn,
+  gemm_f64_p3<GM, BK, ABL><<<(unsigned)nt, 256, P3d<BK>::LDS, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, (int)tn,
                                                              (int)nt);
   return hipGetLastError();
 }

@@ -110,6 +110,11 @@ hipError_t p3_8c(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i
   return hipSuccess;
 }
 
+template <int ABL>
+hipError_t p3da(i64 M, i64 N, i64 K, const double* A, i64 lda, const double* B, i64 ldb, double* C, i64 ldc,
+                double alpha, double beta, bool, hipStream_t s) {
+  return spx_mfma::p3d_launch<8, 16, ABL>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, s);
+}
 hipError_t p3d_16(i64 M, i64 N, i64 K, const double* A, i64 lda, const double* B, i64 ldb, double* C, i64 ldc,
                   double alpha, double beta, bool, hipStream_t s) {
   return spx_mfma::p3d_launch<8, 16>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, s);
@@ -253,6 +258,13 @@ int main(int argc, char** argv) {
                 Variant<float>{"p3 abl2 +no-bar", p3a<2>}, Variant<float>{"p3 abl3 +no-aread", p3a<3>},
                 Variant<float>{"p3 abl4 +no-bread", p3a<4>}},
                157.3);
+    return 0;
+  }
+  if (which == "p3dabl") {
+    run<double>(S, rounds,
+                {Variant<double>{"p3d", p3da<0>}, Variant<double>{"p3d abl1 no-ldst", p3da<1>},
+                 Variant<double>{"p3d abl3 +no-aread", p3da<3>}, Variant<double>{"p3d abl4 +no-bread", p3da<4>}},
+                78.6);
     return 0;
   }
   if (which == "p3d") {  // fp64 three-stage one-wave-per-SIMD kernels against the product
