@@ -575,98 +575,52 @@ template <int BK>
 struct P3d {
   static constexpr int AST = BK + 2, BST = 132, SA = 128 * AST, SB = BK * BST, LDS = 3 * (SA + SB) * 8, KQ = BK / 4;
 };
-template <int GM, int BK, int ABL = 0>
-__global__ __launch_bounds__(256, 1) void gemm_f64_p3(i64 M, i64 N, i64 K, const double* __restrict__ A, i64 lda,
-                                                    const double* __restrict__ B, i64 ldb, double* __restrict__ C,
-                                                    i64 ldc, double alpha, double beta, int tiles_n, int ntiles) {
+template <int GM, int BK, int ABL = 0, int WN = 2>
+__global__ __launch_bounds__(128 * WN, 1) void gemm_f64_p3(i64 M, i64 N, i64 K, const double* __restrict__ A,
+                                                         i64 lda, const double* __restrict__ B, i64 ldb,
+                                                         double* __restrict__ C, i64 ldc, double alpha, double beta,
+                                                         int tiles_n, int ntiles) {
   typedef P3d<BK> P;
   typedef double V __attribute__((ext_vector_type(2)));
+  // WN = 2: 4 waves of 64 x 64 (one per SIMD); WN = 4: 8 waves of 64 x 32
+  // (two per SIMD: 128 accumulator dwords fewer per wave, so hipcc keeps them
+  // in VGPRs instead of copying 256 of them between AGPRs and VGPRs every
+  // two K-tiles, as it did for the one-wave form)
+  constexpr int NT = 128 * WN, WTN = 128 / WN, TN = WTN / 16, KQ = P::KQ;
+  constexpr int APR = BK / 2, NPA = 128 * APR / NT, NPB = BK * 64 / NT, NP = NPA + NPB;
+  static_assert(BK == 16 && (WN == 2 || WN == 4), "BK 16; 2 x 2 or 2 x 4 waves");
   extern __shared__ __attribute__((aligned(16))) double p3d_lds[];
   int tm, tn;
   tile_of(blockIdx.x, ntiles, tiles_n, GM, tm, tn);
   const i64 row0 = (i64)tm * 128, col0 = (i64)tn * 128;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int wm = w >> 1, wn = w & 1;
-  const int li = lane & 15, g = lane >> 4, kb = P::KQ * g;
-  f64x4 acc[4][4];
+  const int wm = w / WN, wn = w % WN;
+  const int li = lane & 15, g = lane >> 4, kb = KQ * g;
+  f64x4 acc[4][TN];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f64x4){0, 0, 0, 0};
-  // staging, 16-byte pieces: A 128 rows x BK / 2 pieces, B BK rows x 64 pieces
-  constexpr int APR = BK / 2, NLA = 128 * APR / 256, NLB = BK * 64 / 256;
-  V ra[NLA], rb[NLB];
-  auto load = [&](i64 k0) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < NLA; ++i) {
-      const int idx = t + 256 * i, r = idx / APR, q = idx % APR;
-      ra[i] = *(const V*)(A + (row0 + r) * lda + k0 + 2 * q);
-    }
-#pragma unroll
-    for (int i = 0; i < NLB; ++i) {
-      const int idx = t + 256 * i, r = idx >> 6, q = idx & 63;
-      rb[i] = *(const V*)(B + (k0 + r) * ldb + col0 + 2 * q);
-    }
-  };
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f64x4){0, 0, 0, 0};
+  V ra[NPA], rb[NPB];
   auto abuf = [&](int s) __attribute__((always_inline)) { return p3d_lds + s * (P::SA + P::SB); };
-  auto store = [&](int s) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < NLA; ++i) {
-      const int idx = t + 256 * i, r = idx / APR, q = idx % APR;
-      *(V*)(abuf(s) + r * P::AST + 2 * q) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < NLB; ++i) {
-      const int idx = t + 256 * i, r = idx >> 6, q = idx & 63;
-      *(V*)(abuf(s) + P::SA + r * P::BST + 2 * q) = rb[i];
-    }
-  };
-  auto read_a = [&](int s, double (&av)[4][P::KQ]) __attribute__((always_inline)) {
-    const double* a = abuf(s) + (wm * 64 + li) * P::AST + kb;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int q = 0; q < P::KQ; q += 2) {
-        const V v = *(const V*)(a + 16 * i * P::AST + q);
-        av[i][q] = v[0];
-        av[i][q + 1] = v[1];
-      }
-  };
-  auto read_b = [&](int s, int kk, double (&b)[4]) __attribute__((always_inline)) {
-    const double* p = abuf(s) + P::SA + (kb + kk) * P::BST + wn * 64 + li;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = p[16 * j];
-  };
-  const int nk = (int)(K / BK);
-  double avA[4][P::KQ], avB[4][P::KQ], bn[4];
-  load(0);
-  store(0);
-  if (nk > 1) {
-    load(BK);
-    store(1);
-  }
-  __syncthreads();
-  read_a(0, avA);
-  read_b(0, 0, bn);
-  load((i64)(nk > 2 ? 2 : nk - 1) * BK);
-  constexpr int KQ = P::KQ;
-  static_assert(BK == 16 && NLA == 4 && NLB == 4, "the weave below places 8 staging pieces over 4 k-steps");
-  // the fp32 kernel's weave (see there): per k-step, between its four MFMA
-  // groups, two pieces of tile kt + 2's stage, the loads of the same pieces
-  // of tile kt + 3 and two of tile kt + 1's A fragment reads
-  auto store_piece = [&](int sb, int q) __attribute__((always_inline)) {
-    const int idx = t + 256 * (q & 3);
-    if (q < 4)
-      *(V*)(abuf(sb) + (idx / APR) * P::AST + 2 * (idx % APR)) = ra[q];
-    else
-      *(V*)(abuf(sb) + P::SA + (idx >> 6) * P::BST + 2 * (idx & 63)) = rb[q - 4];
-  };
+  // 16-byte staging pieces: A 128 rows x APR, B BK rows x 64
   auto load_piece = [&](i64 k0, int q) __attribute__((always_inline)) {
-    const int idx = t + 256 * (q & 3);
-    if (q < 4)
+    if (q < NPA) {
+      const int idx = t + NT * q;
       ra[q] = *(const V*)(A + (row0 + idx / APR) * lda + k0 + 2 * (idx % APR));
-    else
-      rb[q - 4] = *(const V*)(B + (k0 + (idx >> 6)) * ldb + col0 + 2 * (idx & 63));
+    } else {
+      const int idx = t + NT * (q - NPA);
+      rb[q - NPA] = *(const V*)(B + (k0 + (idx >> 6)) * ldb + col0 + 2 * (idx & 63));
+    }
+  };
+  auto store_piece = [&](int sb, int q) __attribute__((always_inline)) {
+    if (q < NPA) {
+      const int idx = t + NT * q;
+      *(V*)(abuf(sb) + (idx / APR) * P::AST + 2 * (idx % APR)) = ra[q];
+    } else {
+      const int idx = t + NT * (q - NPA);
+      *(V*)(abuf(sb) + P::SA + (idx >> 6) * P::BST + 2 * (idx & 63)) = rb[q - NPA];
+    }
   };
   auto read_a_piece = [&](int sb, double (&av)[4][KQ], int q) __attribute__((always_inline)) {
     const int i = q >> 1, hf = q & 1;
@@ -674,33 +628,60 @@ __global__ __launch_bounds__(256, 1) void gemm_f64_p3(i64 M, i64 N, i64 K, const
     av[i][2 * hf] = v[0];
     av[i][2 * hf + 1] = v[1];
   };
+  auto read_b = [&](int sb, int kk, double (&b)[TN]) __attribute__((always_inline)) {
+    const double* p = abuf(sb) + P::SA + (kb + kk) * P::BST + wn * WTN + li;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) b[j] = p[16 * j];
+  };
+  const int nk = (int)(K / BK);
+  double avA[4][KQ], avB[4][KQ], bn[TN];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) load_piece(0, q);
+#pragma unroll
+  for (int q = 0; q < NP; ++q) store_piece(0, q);
+  if (nk > 1) {
+#pragma unroll
+    for (int q = 0; q < NP; ++q) load_piece(BK, q);
+#pragma unroll
+    for (int q = 0; q < NP; ++q) store_piece(1, q);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 8; ++q) read_a_piece(0, avA, q);
+  read_b(0, 0, bn);
+#pragma unroll
+  for (int q = 0; q < NP; ++q) load_piece((i64)(nk > 2 ? 2 : nk - 1) * BK, q);
+  // the fp32 kernel's weave (see there): per k-step, between its four MFMA
+  // groups, NP / 4 pieces of tile kt + 2's stage, the loads of the same
+  // pieces of tile kt + 3 and two of tile kt + 1's A fragment reads
+  constexpr int PPS = NP / KQ;  // staging pieces per k-step: 2 or 1
   auto tile = [&](int kt, int s, double (&av)[4][KQ], double (&avn)[4][KQ]) __attribute__((always_inline)) {
     const int s1 = s == 2 ? 0 : s + 1, s2 = s1 == 2 ? 0 : s1 + 1;
     const i64 k3 = (i64)(kt + 3 < nk ? kt + 3 : nk - 1) * BK;
-    double b[2][4];
+    double b[2][TN];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[0][j] = bn[j];
+    for (int j = 0; j < TN; ++j) b[0][j] = bn[j];
 #pragma unroll
     for (int kk = 0; kk < KQ; ++kk) {
       if (ABL < 4 && kk + 1 < KQ) read_b(s, kk + 1, b[(kk + 1) & 1]);
       if (ABL >= 4 && kk + 1 < KQ)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) b[(kk + 1) & 1][j] = bn[j];
+        for (int j = 0; j < TN; ++j) b[(kk + 1) & 1][j] = bn[j];
       if (kk == KQ - 1) read_b(s1, 0, bn);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i][kk], b[kk & 1][j], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
-        const int q = 2 * kk + (i >> 1);
         // (ABL: dev ablations as in the fp32 kernel: 1 no staging, 3 also no
         // next-tile A reads, 4 also no per-step B reads)
-        if (ABL < 1 && (i & 1) == 0) store_piece(s2, q);
+        const int qs = PPS * kk + (i >> 1);
+        if (ABL < 1 && (i & 1) == 0 && (i >> 1) < PPS) store_piece(s2, qs);
         if ((i & 1) == 1) {
-          if (ABL < 1) load_piece(k3, q);
-          if (ABL < 3) read_a_piece(s1, avn, q);
+          if (ABL < 1 && (i >> 1) < PPS) load_piece(k3, qs);
+          if (ABL < 3) read_a_piece(s1, avn, 2 * kk + (i >> 1));
         }
       }
     }
@@ -719,11 +700,11 @@ __global__ __launch_bounds__(256, 1) void gemm_f64_p3(i64 M, i64 N, i64 K, const
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const i64 gr = row0 + wm * 64 + i * 16 + Mfma<double>::crow(lane, r);
-        const i64 gc = col0 + wn * 64 + j * 16 + li;
+        const i64 gc = col0 + wn * WTN + j * 16 + li;
         double v = alpha * acc[i][j][r];
         if (use_beta) v += beta * C[gr * ldc + gc];
         C[gr * ldc + gc] = v;
@@ -736,18 +717,18 @@ __host__ inline bool p3d_ok(i64 M, i64 N, i64 K, const void* A, i64 lda, const v
          (uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0;
 }
 
-template <int GM, int BK, int ABL = 0>
+template <int GM, int BK, int ABL = 0, int WN = 2>
 __host__ inline hipError_t p3d_launch(i64 M, i64 N, i64 K, const double* A, i64 lda, const double* B, i64 ldb,
                                       double* C, i64 ldc, double alpha, double beta, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_f64_p3<GM, BK, ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_f64_p3<GM, BK, ABL, WN>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        P3d<BK>::LDS);
     if (e != hipSuccess) return e;
     attr = true;
   }
   const i64 tn = N / 128, nt = (M / 128) * tn;
-  gemm_f64_p3<GM, BK, ABL><<<(unsigned)nt, 256, P3d<BK>::LDS, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, (int)tn,
+  gemm_f64_p3<GM, BK, ABL, WN><<<(unsigned)nt, 128 * WN, P3d<BK>::LDS, s>>>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, (int)tn,
                                                              (int)nt);
   return hipGetLastError();
 }

@@ -747,7 +747,7 @@ extern "C" int spx_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* 
     if (tiles >= 1024 && gemm_p3_on() > 1 && spx_mfma::p3d_ok<16>(M, N, K, A, lda, B, ldb)) {
       const double *a = (const double*)A, *b = (const double*)B;
       e = gemm_kchunks<double>(K, a, b, ldb, beta, [&](i64 kc, const double* ak, const double* bk, double bt) {
-        return spx_mfma::p3d_launch<8, 16>(M, N, kc, ak, lda, bk, ldb, (double*)C, ldc, alpha, bt, S(stream));
+        return spx_mfma::p3d_launch<8, 16, 0, 4>(M, N, kc, ak, lda, bk, ldb, (double*)C, ldc, alpha, bt, S(stream));
       });
     } else
     e = GemmF64::launch(M, N, K, (const double*)A, lda, (const double*)B, ldb, (double*)C, ldc, alpha, beta,

@@ -110,6 +110,11 @@ hipError_t p3_8c(i64 M, i64 N, i64 K, const float* A, i64 lda, const float* B, i
   return hipSuccess;
 }
 
+template <int WN, int GM = 8, int ABL = 0>
+hipError_t p3dw(i64 M, i64 N, i64 K, const double* A, i64 lda, const double* B, i64 ldb, double* C, i64 ldc,
+                double alpha, double beta, bool, hipStream_t s) {
+  return spx_mfma::p3d_launch<GM, 16, ABL, WN>(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, s);
+}
 template <int ABL>
 hipError_t p3da(i64 M, i64 N, i64 K, const double* A, i64 lda, const double* B, i64 ldb, double* C, i64 ldc,
                 double alpha, double beta, bool, hipStream_t s) {
@@ -258,6 +263,21 @@ int main(int argc, char** argv) {
                 Variant<float>{"p3 abl2 +no-bar", p3a<2>}, Variant<float>{"p3 abl3 +no-aread", p3a<3>},
                 Variant<float>{"p3 abl4 +no-bread", p3a<4>}},
                157.3);
+    return 0;
+  }
+  if (which == "p3dw") {
+    run<double>(S, rounds,
+                {V(double, 128, 128, 16, 4, 4, 0), Variant<double>{"p3d w4", p3dw<2>}, Variant<double>{"p3d w8", p3dw<4>},
+                 Variant<double>{"p3d w8 g0", p3dw<4, 0>}},
+                78.6);
+    return 0;
+  }
+  if (which == "p3dwabl") {
+    run<double>(S, rounds,
+                {V(double, 128, 128, 16, 4, 4, 0), Variant<double>{"p3d w8", p3dw<4>},
+                 Variant<double>{"p3d w8 abl1", p3dw<4, 8, 1>}, Variant<double>{"p3d w8 abl3", p3dw<4, 8, 3>},
+                 Variant<double>{"p3d w8 abl4", p3dw<4, 8, 4>}},
+                78.6);
     return 0;
   }
   if (which == "p3dabl") {
