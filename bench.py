@@ -617,8 +617,12 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
   counts (exact) and sums (1e-5 of sum |x|) of the last iteration."""
   import torch
   from spartan_amd import workloads
+  from spartan_amd.array import distarray, extent as ext
   X = expr.rand(npts * ctx.world_size, D, dtype=np.float32, seed=21).force()
-  workloads.kmeans_fit(X, K, iters)      # warm-up (every path of the timed loop) from the first K points
+  # the first K points as the initial centres, read before the timed region
+  # (as the API leg does: both legs time the same iterations)
+  c0 = distarray.glom_region(X, ext.create((0, 0), (K, D), X.shape)).astype(np.float64)
+  workloads.kmeans_fit(X, K, iters, centers=c0)      # warm-up (every path of the timed loop)
   from spartan_amd import backend
   be = backend.get()
   be.kmeans_timing(True)  # HIP events around the one-pass kernel of each step (no host sync inside)
@@ -627,7 +631,7 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
     comm.barrier()
     t0 = time.perf_counter()
     info = {}
-    c, labels = workloads.kmeans_fit(X, K, iters, info=info)
+    c, labels = workloads.kmeans_fit(X, K, iters, centers=c0, info=info)
     sync()
     comm.barrier()
     el = comm.max_over_ranks(time.perf_counter() - t0) / iters
@@ -647,6 +651,10 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
          'f16_mfma_frac_per_gpu': round(2.0 * n * K * D / el / 1e12 / (2500.0 * ctx.world_size), 4),
          'hbm_GBps_one_pass': round(4.0 * n * D / el / 1e9, 1),
          'checked': checked and checked_sums, 'checked_labels': checked, 'checked_sums_counts': checked_sums,
+         # iterations queued before the host read the previous counts (kept:
+         # device quotients bit-identical to the host's, no empty cluster) /
+         # queued again with the host's centres (workloads.kmeans_fit)
+         'speculated_iters': info.get('speculated'), 'respun_iters': info.get('respun'),
          'kernel_ms': [round(a, 3) for a, _ in kt], 'step_ms': [round(b, 3) for _, b in kt],
          'kernel_hbm_frac': (round(4.0 * npts * D / (float(np.mean([a for a, _ in kt])) * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                    4) if kt else None),
@@ -657,7 +665,9 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
                    'spx_kmeans_step: certified fp16-MFMA screen + per-centre sums of the rows it decides in one '
                    'pass over X, bf16x3-MFMA pass + exact-order fp64 recompute of its undecided rows (bit-exact '
                    'labels) + their gathered sums; centre sums in fp32 per block and window of 16128 rows, '
-                   'the windows combined in fp64' % (npts, D, K, K)}
+                   'the windows combined in fp64; iteration i + 1 queued with device-divided centres before '
+                   'the host checks iteration i (kept only when bit-identical to the host division)'
+                   % (npts, D, K, K)}
   del X, labels
   torch.cuda.empty_cache()
   return out

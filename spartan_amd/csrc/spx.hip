@@ -786,6 +786,27 @@ __device__ __forceinline__ void km_label(i64* labels, const unsigned int* counte
   }
   labels[row] = lab;
 }
+// km_label with the move bookkeeping read ahead: mv = the workspace's KmMove
+// (read once per kernel) and code = labels[row] as it was before this write
+// (read before the caller's next loads, so no wait on them)
+// (global-address-space pointers: the KmMove fields are generic pointers read
+// from memory, and flat stores / atomics would make the compiler's waits
+// count the LDS queue too, so every wait after them became a full drain)
+typedef __attribute__((address_space(1))) unsigned long long kg_u64;
+typedef __attribute__((address_space(1))) i64 kg_i64;
+__device__ __forceinline__ void km_label_pre(i64* labels, const KmMove& mv, i64 row, i64 lab, i64 code) {
+  if (mv.add) {
+    const i64 p = code <= -2 ? -2 - code : -1;
+    const bool sb = p >= 0 && p != lab;
+    const unsigned long long bit = 1ull << (row & 31);
+    if (code == -1 || sb) __hip_atomic_fetch_or((kg_u64*)mv.add + (row >> 5), bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (sb) {
+      __hip_atomic_fetch_or((kg_u64*)mv.sub + (row >> 5), bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ((kg_i64*)mv.pside)[row] = p;
+    }
+  }
+  labels[row] = lab;
+}
 __global__ void k_km_setmove(KmMove* dst, unsigned long long* add, unsigned long long* sub, i64* pside) {
   if (threadIdx.x == 0) *dst = KmMove{add, sub, pside};
 }
@@ -1850,10 +1871,15 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
   const i64 stride = (i64)gridDim.x * ks_waves(MODE);
   i64 tile = (i64)blockIdx.x * ks_waves(MODE) + w;
   kb_f4 ra[KS][2];
-  auto load = [&](i64 tl) {
+  // the point row lane (r, h) loads for tile tl (list mode: a gather through rows_in)
+  constexpr bool LPF = MODE == 0;  // (MODE 0 runs in list mode only: rows_in is never null)
+  auto lrow = [&](i64 tl) __attribute__((always_inline)) {
     i64 row = tl * 32 + r;
     row = row < nlim ? row : nlim - 1;
-    if (rows_in) row = rows_in[row];
+    if constexpr (LPF) return rows_in[row];
+    else return rows_in ? rows_in[row] : row;
+  };
+  auto load_row = [&](i64 row) __attribute__((always_inline)) {
     const float* p = P + row * ldp + 4 * h;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
@@ -1861,8 +1887,38 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
       ra[ks][1] = *(const kb_f4*)(p + ks * 16 + 8);  // dims 8+4h..8+4h+3
     }
   };
+  // list mode (LPF): the gather's two dependent loads (the row index, then
+  // the row) were issued at the top of each tile, and with two waves per
+  // SIMD the partner's sweep did not cover both latencies (the list pass ran
+  // at ~47 % of its MFMA time).  Now the next tile's row indices are loaded
+  // a whole tile ahead, its rows right after this tile's sweep (the split's
+  // registers are free again: |x'|^2 is pinned at the split) so that they
+  // land during the decision, and the decision's own row index (rows_in of
+  // its slot) at the top of the tile.  The screen (MODE 1) streams every row
+  // in order and keeps the measured top-of-tile load.
+  // Every load of the loop is unconditional (clamped to a valid row), so
+  // the compiler's count of outstanding loads is the same on every path and
+  // its waits stay partial: per tile, in issue order, the decision's row
+  // index (top), then after the sweep the row indices of the tile after
+  // next, the decided rows' old label codes and the next tile's rows.
+  const int qd = r >> 1, rtd = (qd & 3) + 8 * (qd >> 2) + 4 * h;  // the decision lanes' row in the tile
+  i64 nrow = 0;
+  KmMove mv{nullptr, nullptr, nullptr};
+  if constexpr (LPF) {
+    mv = *(const KmMove*)(counters + 4);
+    if (tile < ntiles) {
+      load_row(lrow(tile));
+      nrow = lrow(tile + stride);
+    }
+  }
   for (; tile < ntiles; tile += stride) {
-    load(tile);  // the partner wave's sweep covers the latency
+    if constexpr (!LPF) load_row(lrow(tile));  // the partner wave's sweep covers the latency
+    i64 grow_pf = 0;
+    if constexpr (LPF) {
+      const i64 sl = tile * 32 + rtd;
+      const i64 slc = sl < nlim ? sl : nlim - 1;
+      grow_pf = rows_in[slc];
+    }
     using AT = std::conditional_t<MODE == 0, kb_bf8, kh_f8>;
     AT ah[KS];
     kb_bf8 al[MODE == 0 ? KS : 1];
@@ -1894,7 +1950,12 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
     float p2 = (p2q[0] + p2q[1]) + (p2q[2] + p2q[3]);
     // (the compiler sinks the 64 |p|^2 fmas to the decision, keeping the raw
     // tile live through the sweep; pinning them here frees 47 registers but
-    // measured 2 % slower, gpurun_out ksv4)
+    // measured 2 % slower for the screen, gpurun_out ksv4; the list pass pins
+    // them: its next tile's rows land in those registers)
+    if constexpr (LPF) {
+      asm volatile("" : "+v"(p2));
+      __builtin_amdgcn_sched_barrier(0);
+    }
     // running top-2 of acc = S - cc/2 = -a'/2 (the best centre has the
     // LARGEST acc); lo / sec keep their names from the a' form
     float lo[16], sec[16];
@@ -2057,6 +2118,16 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
 #pragma unroll
     for (int q = 0; q < 16; ++q) lo0[q] = lo[q];
     ks_top2_vals(lo, sec, lane);
+    i64 code_pf = 0;
+    if constexpr (LPF) {
+      // the decided rows' old label codes (km_label_pre), then the next
+      // tile's rows (the split is dead since the sweep, the top-2 lists
+      // since the line above) and the row indices of the tile after it
+      const i64 nrow2 = lrow(tile + 2 * stride);
+      code_pf = labels[grow_pf];
+      load_row(nrow);
+      nrow = nrow2;
+    }
     // the centre of each row's best: lane (h, 2q) holds row rt(q, h)'s
     // b1; the lowest lane of that half whose own best equals it is the
     // centre r (ties in the tagged value share the tile, so the lowest r is
@@ -2081,11 +2152,10 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
     ks_unroll(rmin_q, std::make_integer_sequence<int, 16>{});
     p2 += __shfl_xor(p2, 32, 64);  // row r's |p|^2 in lanes r and r + 32
     // one decision per row, by the even lane of its pair (as in k_kmeans_filter_b3)
-    const int q = r >> 1;
-    const int rt = (q & 3) + 8 * (q >> 2) + 4 * h;
+    const int rt = rtd;
     const i64 slot = tile * 32 + rt;
     const bool live = slot < nlim && (r & 1) == 0;
-    const i64 grow = rows_in ? (live ? rows_in[slot] : 0) : slot;
+    const i64 grow = LPF ? grow_pf : rows_in ? (live ? rows_in[slot] : 0) : slot;
     const float b1 = lo[0], b2 = sec[0];
     const int i1 = 32 * (int)(__builtin_bit_cast(unsigned int, b1) & 7u) + rmin;
     const float p2f = __shfl(p2, rt, 64);
@@ -2099,7 +2169,13 @@ __global__ __launch_bounds__(ks_waves(MODE) * 64) void k_kmeans_filter_as(i64 N,
     const bool fin = cok && isfinite(p2f) && isfinite(e) && pn < pn_lim && isfinite(b1) && isfinite(b2);
     // acc = -a'/2: a' gap > 2e  <=>  acc gap b1 - b2 > e
     const bool dec = fin && b1 - b2 > 1.0001f * e;
-    if (live && dec) km_label(labels, counters, grow, i1);
+    // (the old codes are waited for here, on every path: a wait inside the
+    // label branch left a later reuse of their registers to a full drain)
+    if constexpr (LPF) asm volatile("" ::"v"(code_pf));
+    if (live && dec) {
+      if constexpr (LPF) km_label_pre(labels, mv, grow, i1, code_pf);
+      else km_label(labels, counters, grow, i1);
+    }
     if (MODE == 0 && live && !fin) full_list[atomicAdd(&counters[0], 1u)] = grow;
     const bool needc = live && !dec && (MODE == 1 || fin);
     // the tile's undecided rows as one lane mask, compacted into a row list

@@ -14,6 +14,8 @@ linear_regression_update -- LinearRegression.update
   optimised plan is replayed across iterations (expr/plan_cache.py).  Across
   GPUs the (d,) partials are combined with one RCCL all-reduce (spx_allreduce).
 """
+import os
+
 import numpy as np
 
 from . import expr
@@ -90,10 +92,10 @@ def kmeans_fit(X, n_clusters, n_iter, centers=None, seed=0, info=None):
   for ex in Xa.tiles:
     assert ex.ul[1] == 0 and ex.lr[1] == D, 'k-means needs row-strip tiles (k_means_.py:116)'
   label_tiles = {}
-  for it in range(n_iter):
-    if info is not None:
-      info['assign_centers'] = centers
-    cdev = torch.as_tensor(centers).to(ctx.device)
+
+  def run_step(cdev):
+    """One iteration's kernels on every local tile + the all-reduce, queued
+    on the stream (no host wait): the (K D + K) sums | counts buffer."""
     # sums and counts share one buffer: one D2H per iteration
     buf = torch.empty((K * D + K,), dtype=torch.float64, device=ctx.device)
     sums = buf[:K * D].view(K, D)
@@ -111,17 +113,63 @@ def kmeans_fit(X, n_clusters, n_iter, centers=None, seed=0, info=None):
       counts.zero_()
     comm.all_reduce(sums, 'sum')
     comm.all_reduce(counts, 'sum')
-    host = buf.cpu().numpy()
-    c_host = host[K * D:].view(np.int64)
+    return buf
+
+  # Speculation (SPARTAN_KMEANS_SPECULATE, default on): the next iteration is
+  # queued with centres divided on the device BEFORE the host has looked at
+  # this iteration's counts, so the GPU never idles on the host round trip
+  # (~0.25 ms per cfg3 iteration).  The host then computes the centres
+  # exactly as before (fp64 numpy, empty-cluster reseed) and keeps the queued
+  # step only if no cluster was empty AND the device quotients are
+  # bit-identical to its own (both are IEEE fp64 divisions; compared, not
+  # assumed); otherwise it queues the step again with its own centres, which
+  # overwrites the speculative results.  Returned values are those of the
+  # sequential loop either way.
+  spec = ctx.device.type == 'cuda' and os.environ.get('SPARTAN_KMEANS_SPECULATE', '1') != '0'
+  host_t = torch.empty((2 * K * D + K,), dtype=torch.float64, pin_memory=spec)
+  if info is not None:
+    info['speculated'] = 0
+    info['respun'] = 0
+  buf = run_step(torch.as_tensor(centers).to(ctx.device)) if n_iter > 0 else None
+  for it in range(n_iter):
+    if info is not None:
+      info['assign_centers'] = centers
+    more = it + 1 < n_iter
+    if spec:
+      host_t[:K * D + K].copy_(buf, non_blocking=True)
+      nbuf = None
+      if more:
+        cnext = buf[:K * D].view(K, D) / buf[K * D:].view(torch.int64).to(torch.float64).view(K, 1)
+        host_t[K * D + K:].copy_(cnext.view(-1), non_blocking=True)
+      ev = torch.cuda.Event()
+      ev.record()
+      if more:
+        nbuf = run_step(cnext)
+      ev.synchronize()
+      host = host_t.numpy()
+    else:
+      host = buf.cpu().numpy()
+    c_host = host[K * D:K * D + K].view(np.int64)
     s_host = host[:K * D].reshape(K, D)
     if info is not None:
       info['sums'], info['counts'] = s_host.copy(), c_host.copy()
     empty = c_host == 0
     if np.any(empty):
       c_host = c_host.copy()
+      s_host = s_host.copy()
       c_host[empty] = 1
       s_host[empty, :] = rng.standard_normal((int(empty.sum()), D))
     centers = s_host / c_host.reshape(K, 1)
+    if more:
+      if spec and not np.any(empty) and np.array_equal(
+          centers.view(np.int64), host[K * D + K:].reshape(K, D).view(np.int64)):
+        buf = nbuf
+        if info is not None:
+          info['speculated'] += 1
+      else:
+        if spec and info is not None:
+          info['respun'] += 1
+        buf = run_step(torch.as_tensor(centers).to(ctx.device))
   ltiles = {ext.create((ex.ul[0],), (ex.lr[0],), (N,)): w for ex, w in Xa.tiles.items()}
   llocal = {ext.create((ex.ul[0],), (ex.lr[0],), (N,)): t for ex, t in label_tiles.items()}
   labels = distarray.from_tiles((N,), np.int64, ltiles, llocal)

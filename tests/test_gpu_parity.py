@@ -873,6 +873,41 @@ def test_kmeans_fit_iterations(ex):
   assert (labels.glom() == l2).mean() > 0.999
 
 
+@pytest.mark.parametrize('case', ['plain', 'empty', 'screen'])
+def test_kmeans_fit_speculation_identical(ex, case, monkeypatch):
+  """workloads.kmeans_fit queues iteration i + 1 with device-divided centres
+  before the host has read iteration i's counts: the centres, labels, sums
+  and counts must be bit-identical to the sequential loop
+  (SPARTAN_KMEANS_SPECULATE=0).  'empty': a centre far from every point (an
+  empty cluster: the host reseeds it, the speculative step is re-run);
+  'screen': the certified screen's domain (D = 128, K = 256)."""
+  from spartan_amd import workloads
+  expr, setw = ex
+  setw(1)
+  D, K, n = (128, 256, 60000) if case == 'screen' else (32, 16, 20000)
+  pts = rng.rand((n, D), 23, np.float32)
+  c0 = pts[:K].astype(np.float64).copy()
+  if case == 'empty':
+    c0[3] = 1e3
+  runs = []
+  for spec in ('0', '1'):
+    monkeypatch.setenv('SPARTAN_KMEANS_SPECULATE', spec)
+    info = {}
+    c, lab = workloads.kmeans_fit(expr.from_numpy(pts), K, 3, centers=c0, info=info)
+    runs.append((c, lab.glom(), info))
+  (ca, la, ia), (cb, lb, ib) = runs
+  assert np.array_equal(ca.view(np.int64), cb.view(np.int64))
+  np.testing.assert_array_equal(la, lb)
+  assert np.array_equal(ia['sums'].view(np.int64), ib['sums'].view(np.int64))
+  np.testing.assert_array_equal(ia['counts'], ib['counts'])
+  assert ia['speculated'] == 0 and ia['respun'] == 0
+  assert ib['speculated'] + ib['respun'] == 2
+  if case == 'empty':
+    assert ib['respun'] >= 1
+  else:
+    assert ib['speculated'] == 2   # the device quotients matched the host's bit for bit
+
+
 @pytest.mark.parametrize('dt', [np.float32, np.float64])
 @pytest.mark.parametrize('N,D,K', [(1, 3, 1), (1000, 16, 8), (70001, 128, 256), (9000, 130, 300),
                                    (5000, 300, 1100), (4097, 33, 7), (0, 8, 4)])
