@@ -171,6 +171,34 @@ def _tiny_upload(arr, device):
   return out
 
 
+# Host shadows: a producer that knows the host will read a device tensor and
+# is about to queue long work behind it (examples/kmeans.py: the next k-means
+# step, queued before the host has read this iteration's centre sums) copies
+# the tensor to pinned memory first and attaches the copy here; the next
+# download of THAT tensor, unmodified since (same object, same torch version
+# counter), waits for that copy instead of queueing its own behind the work.
+# One-shot: the entry is taken by the first download that looks for it.
+_SHADOWS = {}
+
+
+def attach_shadow(t, host, event):
+  """``host`` (an ndarray of t's shape and dtype) holds t's current values
+  once ``event`` has completed."""
+  import weakref
+  _SHADOWS[id(t)] = (weakref.ref(t), t._version, host, event)
+
+
+def _take_shadow(t):
+  e = _SHADOWS.pop(id(t), None)
+  if e is None:
+    return None
+  ref, ver, host, ev = e
+  if ref() is not t or t._version != ver:
+    return None
+  ev.synchronize()
+  return host
+
+
 def download(t, out=None):
   """Copy device tensor ``t`` into host array ``out`` (any strides; a new
   C-order array when None) and return it."""
@@ -179,6 +207,11 @@ def download(t, out=None):
   shape = tuple(t.shape)
   if out is None:
     out = np.empty(shape, dtype=backend.np_dtype(t.dtype))
+  if _SHADOWS:
+    h = _take_shadow(t)
+    if h is not None:
+      out[...] = h.reshape(out.shape)
+      return out
   if t.device.type != 'cuda' or t.dim() == 0 or t.numel() * t.element_size() < SMALL:
     out[...] = t.cpu().numpy().reshape(out.shape)
     return out

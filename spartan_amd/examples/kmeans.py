@@ -159,6 +159,10 @@ def _count_join(kind, arrays, axes, fn_kw, target):
   if pre is not None:
     comm.all_reduce(pre, 'sum')
     _deliver_full(target, pre)
+    _RED.clear()
+    if len(target.local) == 1:  # the counts as the host will read them, for _speculate
+      (_ex, tile), = target.local.items()
+      _RED.update(labels=labels, counts=tile.data)
     return
   counts = torch.zeros((K,), dtype=torch.int64, device=ctx.device)
   for ex, tile in labels.local.items():
@@ -179,6 +183,8 @@ def _center_join(kind, arrays, axes, fn_kw, target):
   if pre is not None:  # the fused step of this labels array already summed X
     comm.all_reduce(pre, 'sum')
     _deliver_full(target, pre)
+    if _NEXT['on']:
+      _speculate(X, labels, K, target)
     return
   sums = torch.zeros((K, D), dtype=torch.float64, device=ctx.device)
   counts = torch.zeros((K,), dtype=torch.int64, device=ctx.device)
@@ -230,6 +236,7 @@ def _assign_fused(arrays, fn_kw, target, dist_dtype):
   K, D = c.shape
   blocks, got = _row_blocks(X, D)
   fused = _step_domain(X, K)
+  spec = _take_spec(X, K, c, dist_dtype) if fused else None
   _STEP.clear()
   if fused:  # the first local block's step writes them (zero_first), the others add
     sums = torch.empty((K, D), dtype=torch.float64, device=ctx.device)
@@ -243,19 +250,117 @@ def _assign_fused(arrays, fn_kw, target, dist_dtype):
       pts = got[qi]
       if pts.stride(-1) != 1:
         pts = be.contiguous(pts)
-      lab = torch.empty((tex.shape[0],), dtype=torch.int64, device=ctx.device)
-      if fused:
+      if spec is not None:  # the step queued for these very centres (_speculate)
+        lab = spec['labs'][qi]
+        first = False
+      elif fused:
+        lab = torch.empty((tex.shape[0],), dtype=torch.int64, device=ctx.device)
         be.kmeans_step(pts, c, lab, sums, counts, zero_first=first, dist_dtype=dist_dtype)
         first = False
       else:
+        lab = torch.empty((tex.shape[0],), dtype=torch.int64, device=ctx.device)
+      if not fused:
         be.kmeans_assign(pts, c, lab, dist_dtype=dist_dtype)
     updates.append((qi, tex, src, lab))
   _scatter_updates(target, updates)
   if fused:
-    if first:  # no local row block on this rank
+    if spec is not None:
+      sums, counts = spec['sums'], spec['counts']
+    elif first:  # no local row block on this rank
       sums.zero_()
       counts.zero_()
-    _STEP.update(labels=target, X=X, K=K, sums=sums, counts=counts)
+    _STEP.update(labels=target, X=X, K=K, sums=sums, counts=counts, dd=dist_dtype)
+
+
+# Speculation (world size 1; SPARTAN_KMEANS_SPECULATE, default on).  The
+# reference's loop reads the counts and the centre sums back to the host,
+# divides there and uploads the new centres (k_means_.py:140-150): the GPU
+# idles for that round trip and for the building of the next iteration's
+# expressions.  While KMeans.fit has an iteration to go (_NEXT), the centre
+# join, once the sums are all-reduced and delivered, (1) computes the next
+# centres on the device exactly as the host will (the sums and counts rounded
+# to the joins' target dtypes, divided in NumPy's result dtype), (2) copies
+# the delivered sums to pinned memory and attaches that copy as the host
+# shadow of the target tile (array/transfer.py), so the host's glom does not
+# wait behind (3), the next fused step queued on the same stream with those
+# centres.  The next fused assignment adopts that step's labels, sums and
+# counts only if ITS centres are bit-identical to the queued ones (compared
+# on the device); an empty cluster (reseeded on the host) or any other
+# centres run the step as usual, after the queued one.  Results are those of
+# the sequential loop.  (A side stream cannot overlap: k_kmeans_pp holds every
+# CU's register file and LDS, so any other kernel -- the runtime's copy
+# kernels too -- waits for it.)
+_RED = {}           # the last fused step's all-reduced counts (from _count_join)
+_SPEC = {}          # the queued step (one entry)
+_NEXT = {'on': False}
+_PIN = {}           # pinned staging for the shadows
+SPEC_STATS = {'queued': 0, 'adopted': 0, 'dropped': 0}
+
+
+def _speculate(X, labels, K, target):
+  import os
+  import torch
+  ctx = runtime.get()
+  _SPEC.clear()
+  if (ctx.world_size != 1 or ctx.device.type != 'cuda' or os.environ.get('SPARTAN_KMEANS_SPECULATE', '1') == '0'
+      or _RED.get('labels') is not labels or _STEP.get('labels') is not labels or len(target.local) != 1):
+    return
+  from ..array import transfer
+  counts = _RED.pop('counts')
+  (_ex, tile), = target.local.items()
+  tt = tile.data  # the centre sums as the host will read them (the target's dtype)
+  if tuple(tt.shape) != (K, X.shape[1]) or tuple(counts.shape) != (K,):
+    return
+  rdt = backend.torch_dtype(np.result_type(backend.np_dtype(tt.dtype), backend.np_dtype(counts.dtype)))
+  dd = _STEP.get('dd')
+  be = backend.get()
+  D = X.shape[1]
+  cn = (tt.to(rdt) / counts.to(rdt).view(K, 1)).to(torch.float64)
+  key = (tuple(tt.shape), tt.dtype)
+  hp = _PIN.get(key)
+  if hp is None:
+    hp = _PIN[key] = torch.empty(tt.shape, dtype=tt.dtype, pin_memory=True)
+  hp.copy_(tt, non_blocking=True)
+  ev = torch.cuda.Event()
+  ev.record()
+  transfer.attach_shadow(tt, hp.numpy(), ev)
+  blocks, got = _row_blocks(X, D)
+  s2 = torch.empty((K, D), dtype=torch.float64, device=ctx.device)
+  c2 = torch.empty((K,), dtype=torch.int64, device=ctx.device)
+  labs = {}
+  first = True
+  for qi, (src, _r) in enumerate(blocks):
+    if src != ctx.rank:
+      continue
+    pts = got[qi]
+    if pts.stride(-1) != 1:
+      pts = be.contiguous(pts)
+    lab = torch.empty((pts.shape[0],), dtype=torch.int64, device=ctx.device)
+    be.kmeans_step(pts, cn, lab, s2, c2, zero_first=first, dist_dtype=dd)
+    first = False
+    labs[qi] = lab
+  if first:
+    s2.zero_()
+    c2.zero_()
+  _SPEC.update(X=X, K=K, dd=dd, cn=cn, labs=labs, sums=s2, counts=c2)
+  SPEC_STATS['queued'] += 1
+
+
+def _take_spec(X, K, c, dist_dtype):
+  """The queued step if it ran for exactly these centres (bit for bit), X, K
+  and distance dtype, else None."""
+  import torch
+  sp = dict(_SPEC)
+  _SPEC.clear()
+  if not sp:
+    return None
+  # (the comparison's host sync waits for the queued step: the GPU is busy)
+  if not (sp['X'] is X and sp['K'] == K and sp['dd'] == dist_dtype and tuple(c.shape) == tuple(sp['cn'].shape)
+          and torch.equal(c.contiguous().view(torch.int64), sp['cn'].view(torch.int64))):
+    SPEC_STATS['dropped'] += 1
+    return None
+  SPEC_STATS['adopted'] += 1
+  return sp
 
 
 def _take_step(X, labels, K, what):
@@ -305,8 +410,13 @@ class KMeans(object):
       new_centers = expr.map2((X, labels), (0, 0), fn=kmeans_center_mapper,
                               fn_kw={'centers_count': self.n_clusters},
                               shape=(centers.shape[0], centers.shape[1]))
-      counts = counts.optimized().glom()
-      centers = new_centers.optimized().glom()
+      # (another iteration follows: the centre join may queue it, _speculate)
+      _NEXT['on'] = i + 1 < self.n_iter
+      try:
+        counts = counts.optimized().glom()
+        centers = new_centers.optimized().glom()
+      finally:
+        _NEXT['on'] = False
       zcount_indices = (counts == 0).reshape(self.n_clusters)
       if np.any(zcount_indices):
         n_points = np.count_nonzero(zcount_indices)

@@ -53,6 +53,20 @@ def sgd_train(x, y, w, alpha, iterations, device_w=True):
   return expr.glom(W)
 
 
+_PINNED = {}
+
+
+def _pinned_f64(n):
+  """A pinned host fp64 buffer of >= n elements, kept across calls (a fresh
+  pinned allocation inside a timed loop costs far more than the copies it
+  serves; every copy into it is waited for before kmeans_fit returns)."""
+  import torch
+  buf = _PINNED.get('f64')
+  if buf is None or buf.numel() < n:
+    buf = _PINNED['f64'] = torch.empty((n,), dtype=torch.float64, pin_memory=True)
+  return buf[:n]
+
+
 def kmeans_fit(X, n_clusters, n_iter, centers=None, seed=0, info=None):
   """KMeans.fit, 'outer' implementation (spartan/examples/sklearn/cluster/
   k_means_.py:108-152), one fused pass pair per iteration on every rank:
@@ -126,7 +140,7 @@ def kmeans_fit(X, n_clusters, n_iter, centers=None, seed=0, info=None):
   # overwrites the speculative results.  Returned values are those of the
   # sequential loop either way.
   spec = ctx.device.type == 'cuda' and os.environ.get('SPARTAN_KMEANS_SPECULATE', '1') != '0'
-  host_t = torch.empty((2 * K * D + K,), dtype=torch.float64, pin_memory=spec)
+  host_t = _pinned_f64(2 * K * D + K) if spec else None
   if info is not None:
     info['speculated'] = 0
     info['respun'] = 0

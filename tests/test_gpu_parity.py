@@ -908,6 +908,42 @@ def test_kmeans_fit_speculation_identical(ex, case, monkeypatch):
     assert ib['speculated'] == 2   # the device quotients matched the host's bit for bit
 
 
+@pytest.mark.parametrize('case', ['plain', 'empty', 'd64'])
+def test_kmeans_api_speculation_identical(ex, case, monkeypatch):
+  """examples.kmeans.KMeans.fit (the reference's loop through outer / argmin
+  / map2): the centre join queues the next fused step behind a pinned copy of
+  the sums the host is about to read; the next assignment adopts it only for
+  bit-identical centres.  Centres and labels must equal the run with
+  SPARTAN_KMEANS_SPECULATE=0; 'plain' / 'd64' adopt every queued step,
+  'empty' (a centre no point is nearest to: the host reseeds it) drops the
+  one queued for the reseeded centres."""
+  from spartan_amd.examples import kmeans as KM
+  expr, setw = ex
+  setw(1)
+  D, K, n = (64, 32, 30000) if case == 'd64' else (128, 64, 40000)
+  pts = rng.rand((n, D), 24, np.float32)
+  c0 = pts[:K].astype(np.float64).copy()
+  if case == 'empty':
+    c0[5] = 1e3
+  X = expr.from_numpy(pts).force()
+  runs = []
+  for spec in ('0', '1'):
+    monkeypatch.setenv('SPARTAN_KMEANS_SPECULATE', spec)
+    before = dict(KM.SPEC_STATS)
+    c, lab = KM.KMeans(K, 3).fit(X, c0)
+    stats = {k: KM.SPEC_STATS[k] - before[k] for k in before}
+    runs.append((c, lab.glom(), stats))
+  (ca, la, sa), (cb, lb, sb) = runs
+  assert np.array_equal(ca.view(np.int64), cb.view(np.int64))
+  np.testing.assert_array_equal(la, lb)
+  assert sa == {'queued': 0, 'adopted': 0, 'dropped': 0}
+  assert sb['queued'] == 2, sb
+  if case == 'empty':
+    assert sb['dropped'] >= 1 and sb['adopted'] + sb['dropped'] == 2, sb
+  else:
+    assert sb['adopted'] == 2, sb
+
+
 @pytest.mark.parametrize('dt', [np.float32, np.float64])
 @pytest.mark.parametrize('N,D,K', [(1, 3, 1), (1000, 16, 8), (70001, 128, 256), (9000, 130, 300),
                                    (5000, 300, 1100), (4097, 33, 7), (0, 8, 4)])
