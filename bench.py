@@ -656,6 +656,7 @@ def bench_kmeans(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
          # queued again with the host's centres (workloads.kmeans_fit)
          'speculated_iters': info.get('speculated'), 'respun_iters': info.get('respun'),
          'kernel_ms': [round(a, 3) for a, _ in kt], 'step_ms': [round(b, 3) for _, b in kt],
+         'host_overhead_ms_per_iter': (round(el * 1e3 - float(np.mean([b for _, b in kt])), 3) if kt else None),
          'kernel_hbm_frac': (round(4.0 * npts * D / (float(np.mean([a for a, _ in kt])) * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                    4) if kt else None),
          'kernel_note': 'kernel_ms / step_ms: HIP events (spx_kmeans_timing) around k_kmeans_pp (the one-pass '
@@ -685,14 +686,21 @@ def bench_kmeans_api(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
   c0 = distarray.glom_region(X, ext.create((0, 0), (K, D), X.shape)).astype(np.float64)
   KMeans(K, iters).fit(X, c0)  # warm-up: as many iterations as the timed fit (the direct leg's warm-up too),
   # so the timed run meets a caching allocator that already holds two label buffers
-  sync()
-  comm.barrier()
-  t0 = time.perf_counter()
-  km = KMeans(K, iters)
-  c_api, labels = km.fit(X, c0)
-  sync()
-  comm.barrier()
-  el = comm.max_over_ranks(time.perf_counter() - t0) / iters
+  from spartan_amd import backend
+  be = backend.get()
+  be.kmeans_timing(True)  # the same per-step HIP events as the direct leg
+  try:
+    sync()
+    comm.barrier()
+    t0 = time.perf_counter()
+    km = KMeans(K, iters)
+    c_api, labels = km.fit(X, c0)
+    sync()
+    comm.barrier()
+    el = comm.max_over_ranks(time.perf_counter() - t0) / iters
+    kt = be.kmeans_times()
+  finally:
+    be.kmeans_timing(False)
   n = npts * ctx.world_size
   # the last iteration's labels against the all-exact assignment kernel with
   # the centres that iteration used (a prefix of each local row strip)
@@ -701,6 +709,11 @@ def bench_kmeans_api(npts, ctx, expr, comm, sync, D=128, K=256, iters=2):
   checked = check_kmeans(X, labels.force() if hasattr(labels, 'force') else labels, ac, comm,
                          dist_dtype=X.dtype)  # kmeans_dist_mapper's target has the points' dtype
   out = {'ms_per_iter': round(el * 1e3, 3), 'points_per_s': round(n / el, 1), 'checked': checked,
+         'step_ms': [round(b, 3) for _, b in kt],
+         # the time per iteration outside the fused steps (HIP events around each
+         # spx_kmeans_step): the loop's host round trip and glue, comparable with
+         # the direct leg's figure whatever the clock does between the legs
+         'host_overhead_ms_per_iter': (round(el * 1e3 - float(np.mean([b for _, b in kt])), 3) if kt else None),
          'config': 'cfg3 via examples.kmeans.KMeans(%d, %d).fit(X, first %d points): outer + argmin '
                    '(OuterArgminFusion -> certified assignment), map2 bincount, map2 centre sums' % (K, iters, K)}
   del X
