@@ -321,9 +321,17 @@ def _speculate(X, labels, K, target):
   if hp is None:
     hp = _PIN[key] = torch.empty(tt.shape, dtype=tt.dtype, pin_memory=True)
   hp.copy_(tt, non_blocking=True)
+  # the centres the host will compute, to host too: its from_numpy of them
+  # then takes cn itself instead of a synchronous upload queued behind the
+  # step (transfer.register_upload_alias; bit-identical or not taken)
+  hc = _PIN.get('cn')
+  if hc is None or tuple(hc.shape) != tuple(cn.shape):
+    hc = _PIN['cn'] = torch.empty(tuple(cn.shape), dtype=torch.float64, pin_memory=True)
+  hc.copy_(cn, non_blocking=True)
   ev = torch.cuda.Event()
   ev.record()
   transfer.attach_shadow(tt, hp.numpy(), ev)
+  transfer.register_upload_alias(hc.numpy(), cn, ev)
   blocks, got = _row_blocks(X, D)
   s2 = torch.empty((K, D), dtype=torch.float64, device=ctx.device)
   c2 = torch.empty((K,), dtype=torch.int64, device=ctx.device)

@@ -31,12 +31,17 @@ def main():
   KMeans(K, 2).fit(X, c0)
   workloads.kmeans_fit(X, K, 2, centers=c0)
   torch.cuda.synchronize()
-  for name, fn in (('direct', lambda: workloads.kmeans_fit(X, K, iters, centers=c0)),
+  from spartan_amd.examples import kmeans as KM
+  info = {}
+  for name, fn in (('direct', lambda: workloads.kmeans_fit(X, K, iters, centers=c0, info=info)),
                    ('api', lambda: KMeans(K, iters).fit(X, c0))):
+    before = dict(KM.SPEC_STATS)
     t = time.perf_counter()
     fn()
     torch.cuda.synchronize()
-    print('%s: %.3f ms per iteration' % (name, (time.perf_counter() - t) / iters * 1e3))
+    print('%s: %.3f ms per iteration; direct speculated %s respun %s; api %s' % (
+        name, (time.perf_counter() - t) / iters * 1e3, info.get('speculated'), info.get('respun'),
+        {k: KM.SPEC_STATS[k] - before[k] for k in before}))
   pr = cProfile.Profile()
   pr.enable()
   KMeans(K, iters).fit(X, c0)
