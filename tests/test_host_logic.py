@@ -507,3 +507,57 @@ def test_tiny_uploads_of_other_dtypes(host_ctx):
   for a in (np.arange(6, dtype=np.float16), np.arange(6, dtype=np.int8), np.arange(6, dtype='>f8')):
     t = transfer.upload(a, torch.device('cpu'))
     np.testing.assert_array_equal(t.numpy().astype(np.float64), a.astype(np.float64))
+
+
+class _Ev:
+  """Stand-in for a torch.cuda.Event (host logic only): counts its waits."""
+  n = 0
+
+  def synchronize(self):
+    _Ev.n += 1
+
+
+def test_download_host_shadow_is_one_shot_and_versioned():
+  """array/transfer.py host shadows (examples/kmeans.py speculation): the next
+  download of the tensor reads the attached host copy after waiting for its
+  event; the entry is taken once; an in-place change of the tensor since
+  the attach (torch version counter) or another tensor ignores it."""
+  import torch
+  from spartan_amd.array import transfer
+  t = torch.arange(6, dtype=torch.float64).reshape(2, 3)
+  host = np.full((2, 3), 7.0)
+  n0 = _Ev.n
+  transfer.attach_shadow(t, host, _Ev())
+  np.testing.assert_array_equal(transfer.download(t), host)
+  assert _Ev.n == n0 + 1
+  np.testing.assert_array_equal(transfer.download(t), t.numpy())   # one-shot
+  transfer.attach_shadow(t, host, _Ev())
+  t.add_(1.0)                                                       # written since: stale
+  np.testing.assert_array_equal(transfer.download(t), t.numpy())
+  u = torch.zeros((2, 3), dtype=torch.float64)
+  transfer.attach_shadow(t, host, _Ev())
+  np.testing.assert_array_equal(transfer.download(u), u.numpy())   # another tensor
+  transfer._SHADOWS.clear()
+
+
+def test_upload_alias_bitwise_and_one_shot():
+  """array/transfer.py upload aliases: the registered tensor is handed out
+  only for an array bit-identical to its host copy (-0.0 vs 0.0 differ),
+  of the same shape and dtype; one-shot either way."""
+  import torch
+  from spartan_amd.array import transfer
+  dev = torch.tensor([[1.0, -0.0], [2.5, 3.0]], dtype=torch.float64)
+  host = dev.numpy().copy()
+  cpu = torch.device('cpu')
+  transfer.register_upload_alias(host, dev, _Ev())
+  assert transfer._take_alias(host.copy(), cpu) is dev
+  assert not transfer._ALIAS
+  transfer.register_upload_alias(host, dev, _Ev())
+  other = host.copy()
+  other[0, 1] = 0.0                                                 # +0.0: not bit-identical
+  assert transfer._take_alias(other, cpu) is None
+  assert not transfer._ALIAS
+  transfer.register_upload_alias(host, dev, _Ev())
+  assert transfer._take_alias(host.reshape(4), cpu) is None         # shape differs
+  transfer.register_upload_alias(host, dev, _Ev())
+  assert transfer._take_alias(host.astype(np.float32), cpu) is None  # dtype differs
