@@ -159,6 +159,8 @@ def _count_join(kind, arrays, axes, fn_kw, target):
   if pre is not None:
     comm.all_reduce(pre, 'sum')
     _deliver_full(target, pre)
+    _DT['cdt'] = np.dtype(target.dtype)
+    _early_shadow('counts', target)
     _RED.clear()
     if len(target.local) == 1:  # the counts as the host will read them, for _speculate
       (_ex, tile), = target.local.items()
@@ -183,7 +185,9 @@ def _center_join(kind, arrays, axes, fn_kw, target):
   if pre is not None:  # the fused step of this labels array already summed X
     comm.all_reduce(pre, 'sum')
     _deliver_full(target, pre)
-    if _NEXT['on']:
+    _DT['sdt'] = np.dtype(target.dtype)
+    _early_shadow('sums', target)
+    if _NEXT['on'] and not _SPEC:  # (not queued early, _speculate_early)
       _speculate(X, labels, K, target)
     return
   sums = torch.zeros((K, D), dtype=torch.float64, device=ctx.device)
@@ -270,6 +274,9 @@ def _assign_fused(arrays, fn_kw, target, dist_dtype):
       sums.zero_()
       counts.zero_()
     _STEP.update(labels=target, X=X, K=K, sums=sums, counts=counts, dd=dist_dtype)
+    _EARLY.clear()
+    if spec is not None and _NEXT['on'] and _spec_on():
+      _speculate_early(X, K, sums, counts, dist_dtype)
 
 
 # Speculation (world size 1; SPARTAN_KMEANS_SPECULATE, default on).  The
@@ -291,47 +298,36 @@ def _assign_fused(arrays, fn_kw, target, dist_dtype):
 # CU's register file and LDS, so any other kernel -- the runtime's copy
 # kernels too -- waits for it.)
 _RED = {}           # the last fused step's all-reduced counts (from _count_join)
+_DT = {}            # the dtypes the count / centre joins delivered in (the host reads them so)
+_EARLY = {}         # host copies staged by _speculate_early for this iteration's joins
 _SPEC = {}          # the queued step (one entry)
 _NEXT = {'on': False}
 _PIN = {}           # pinned staging for the shadows
 SPEC_STATS = {'queued': 0, 'adopted': 0, 'dropped': 0}
 
 
-def _speculate(X, labels, K, target):
+def _spec_on():
   import os
+  ctx = runtime.get()
+  return (ctx.world_size == 1 and ctx.device.type == 'cuda'
+          and os.environ.get('SPARTAN_KMEANS_SPECULATE', '1') != '0')
+
+
+def _pinned(key, shape, tdt):
+  import torch
+  hp = _PIN.get(key)
+  if hp is None or tuple(hp.shape) != tuple(shape) or hp.dtype != tdt:
+    hp = _PIN[key] = torch.empty(tuple(shape), dtype=tdt, pin_memory=True)
+  return hp
+
+
+def _queue(X, K, cn, dd):
+  """Queue the fused step of X for centres cn (device fp64) on the current
+  stream: labels, sums, counts in fresh buffers, recorded in _SPEC."""
   import torch
   ctx = runtime.get()
-  _SPEC.clear()
-  if (ctx.world_size != 1 or ctx.device.type != 'cuda' or os.environ.get('SPARTAN_KMEANS_SPECULATE', '1') == '0'
-      or _RED.get('labels') is not labels or _STEP.get('labels') is not labels or len(target.local) != 1):
-    return
-  from ..array import transfer
-  counts = _RED.pop('counts')
-  (_ex, tile), = target.local.items()
-  tt = tile.data  # the centre sums as the host will read them (the target's dtype)
-  if tuple(tt.shape) != (K, X.shape[1]) or tuple(counts.shape) != (K,):
-    return
-  rdt = backend.torch_dtype(np.result_type(backend.np_dtype(tt.dtype), backend.np_dtype(counts.dtype)))
-  dd = _STEP.get('dd')
   be = backend.get()
   D = X.shape[1]
-  cn = (tt.to(rdt) / counts.to(rdt).view(K, 1)).to(torch.float64)
-  key = (tuple(tt.shape), tt.dtype)
-  hp = _PIN.get(key)
-  if hp is None:
-    hp = _PIN[key] = torch.empty(tt.shape, dtype=tt.dtype, pin_memory=True)
-  hp.copy_(tt, non_blocking=True)
-  # the centres the host will compute, to host too: its from_numpy of them
-  # then takes cn itself instead of a synchronous upload queued behind the
-  # step (transfer.register_upload_alias; bit-identical or not taken)
-  hc = _PIN.get('cn')
-  if hc is None or tuple(hc.shape) != tuple(cn.shape):
-    hc = _PIN['cn'] = torch.empty(tuple(cn.shape), dtype=torch.float64, pin_memory=True)
-  hc.copy_(cn, non_blocking=True)
-  ev = torch.cuda.Event()
-  ev.record()
-  transfer.attach_shadow(tt, hp.numpy(), ev)
-  transfer.register_upload_alias(hc.numpy(), cn, ev)
   blocks, got = _row_blocks(X, D)
   s2 = torch.empty((K, D), dtype=torch.float64, device=ctx.device)
   c2 = torch.empty((K,), dtype=torch.int64, device=ctx.device)
@@ -352,6 +348,84 @@ def _speculate(X, labels, K, target):
     c2.zero_()
   _SPEC.update(X=X, K=K, dd=dd, cn=cn, labs=labs, sums=s2, counts=c2)
   SPEC_STATS['queued'] += 1
+
+
+def _speculate(X, labels, K, target):
+  """At the centre join (no step queued yet: the loop's first iteration, or
+  after a dropped one): queue the next step behind a pinned copy of the sums
+  the host is about to glom (a host shadow of the target tile)."""
+  import torch
+  _SPEC.clear()
+  if not _spec_on() or _RED.get('labels') is not labels or _STEP.get('labels') is not labels \
+      or len(target.local) != 1:
+    return
+  from ..array import transfer
+  counts = _RED.pop('counts')
+  (_ex, tile), = target.local.items()
+  tt = tile.data  # the centre sums as the host will read them (the target's dtype)
+  if tuple(tt.shape) != (K, X.shape[1]) or tuple(counts.shape) != (K,):
+    return
+  rdt = backend.torch_dtype(np.result_type(backend.np_dtype(tt.dtype), backend.np_dtype(counts.dtype)))
+  cn = (tt.to(rdt) / counts.to(rdt).view(K, 1)).to(torch.float64)
+  hp = _pinned('sums', tt.shape, tt.dtype)
+  hp.copy_(tt, non_blocking=True)
+  # the centres the host will compute, to host too: its from_numpy of them
+  # then takes cn itself instead of a synchronous upload queued behind the
+  # step (transfer.register_upload_alias; bit-identical or not taken)
+  hc = _pinned('cn', cn.shape, torch.float64)
+  hc.copy_(cn, non_blocking=True)
+  ev = torch.cuda.Event()
+  ev.record()
+  transfer.attach_shadow(tt, hp.numpy(), ev)
+  transfer.register_upload_alias(hc.numpy(), cn, ev)
+  _queue(X, K, cn, _STEP.get('dd'))
+
+
+def _speculate_early(X, K, sums, counts, dd):
+  """At the adoption of a queued step (world size 1: its sums and counts ARE
+  the values this iteration's joins deliver): queue the step after it right
+  away, computing its centres as the host will (the joins' target dtypes of
+  the last iteration, NumPy's result dtype), and stage pinned copies of what
+  the host will glom -- the counts, the sums in the centre target's dtype --
+  and of those centres, all before the step, so that neither the gloms nor
+  the upload of the centres wait behind it.  The joins attach the copies as
+  host shadows of their target tiles (_EARLY)."""
+  import torch
+  from ..array import transfer
+  sdt, cdt = _DT.get('sdt'), _DT.get('cdt')
+  if sdt is None or cdt is None:
+    return
+  tdt = backend.torch_dtype
+  rdt = tdt(np.result_type(sdt, cdt))
+  st = sums.to(tdt(sdt))
+  ct = counts.to(tdt(cdt))
+  cn = (st.to(rdt) / ct.to(rdt).view(K, 1)).to(torch.float64)
+  hs = _pinned('e_sums', st.shape, st.dtype)
+  hk = _pinned('e_counts', ct.shape, ct.dtype)
+  hc = _pinned('cn', cn.shape, torch.float64)
+  hs.copy_(st, non_blocking=True)
+  hk.copy_(ct, non_blocking=True)
+  hc.copy_(cn, non_blocking=True)
+  ev = torch.cuda.Event()
+  ev.record()
+  _EARLY.clear()
+  _EARLY.update(sums=(hs.numpy(), ev, sdt), counts=(hk.numpy(), ev, cdt))
+  transfer.register_upload_alias(hc.numpy(), cn, ev)
+  _queue(X, K, cn, dd)
+
+
+def _early_shadow(what, target):
+  """Attach the early-staged host copy of ``what`` to target's tile (if the
+  dtype and shape match what was staged)."""
+  from ..array import transfer
+  e = _EARLY.pop(what, None)
+  if e is None or len(target.local) != 1:
+    return
+  host, ev, dt = e
+  (_ex, tile), = target.local.items()
+  tt = tile.data
+  if np.dtype(target.dtype) == dt and tuple(tt.shape) == tuple(host.shape):
+    transfer.attach_shadow(tt, host, ev)
 
 
 def _take_spec(X, K, c, dist_dtype):
