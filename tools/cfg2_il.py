@@ -24,7 +24,7 @@ def main():
   z = expr.rand(S, S, dtype=np.float32, seed=13, low=-1.0, high=1.0).force()
   X, Y, Z = expr.lazify(x), expr.lazify(y), expr.lazify(z)
   be = backend.get()
-  confs = [(False, 2), (True, 1), (True, 2), (True, 4), (False, 1)]
+  confs = [(False, 2), (False, 3), (False, 4), (True, 4), (False, 1)]
   res = {c: [] for c in confs}
   ref = None
   real = (backend.COLS_INTERLEAVE, backend.COLS_BLOCKS_PER_CU)
