@@ -275,8 +275,11 @@ def _assign_fused(arrays, fn_kw, target, dist_dtype):
       counts.zero_()
     _STEP.update(labels=target, X=X, K=K, sums=sums, counts=counts, dd=dist_dtype)
     _EARLY.clear()
-    if spec is not None and _NEXT['on'] and _spec_on():
-      _speculate_early(X, K, sums, counts, dist_dtype)
+    if spec is not None and _spec_on():
+      # (the loop's last iteration queues nothing, but still stages the
+      # copies: its gloms and the upload of the final centres then need no
+      # round trip of their own)
+      _speculate_early(X, K, sums, counts, dist_dtype, queue=_NEXT['on'])
 
 
 # Speculation (world size 1; SPARTAN_KMEANS_SPECULATE, default on).  The
@@ -381,7 +384,7 @@ def _speculate(X, labels, K, target):
   _queue(X, K, cn, _STEP.get('dd'))
 
 
-def _speculate_early(X, K, sums, counts, dd):
+def _speculate_early(X, K, sums, counts, dd, queue=True):
   """At the adoption of a queued step (world size 1: its sums and counts ARE
   the values this iteration's joins deliver): queue the step after it right
   away, computing its centres as the host will (the joins' target dtypes of
@@ -411,7 +414,8 @@ def _speculate_early(X, K, sums, counts, dd):
   _EARLY.clear()
   _EARLY.update(sums=(hs.numpy(), ev, sdt), counts=(hk.numpy(), ev, cdt))
   transfer.register_upload_alias(hc.numpy(), cn, ev)
-  _queue(X, K, cn, dd)
+  if queue:
+    _queue(X, K, cn, dd)
 
 
 def _early_shadow(what, target):
