@@ -48,6 +48,12 @@ def main():
   torch.cuda.synchronize()
   print('%s: %.3f ms per iteration' % ('assign+accumulate' if two else mode, ev[0].elapsed_time(ev[1]) / reps),
         flush=True)
+  # checksums of the last step's results (A/B of variant builds: equal bits)
+  import hashlib
+  h = hashlib.sha256()
+  for t in (lab, sums, cnt):
+    h.update(t.cpu().numpy().tobytes())
+  print('checksum labels+sums+counts: %s' % h.hexdigest()[:16], flush=True)
 
 
 if __name__ == '__main__':
